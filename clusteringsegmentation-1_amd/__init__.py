@@ -1,0 +1,216 @@
+"""clusteringsegmentation-1_amd -- MI355X-native DivQuant hot path.
+
+Python mirror of the reference's DivQuant interface (DivQuant/quant_util.h,
+DivQuant/DivQuantHeader.h) over the C ABI of ``libdivquant_hip.so``
+(include/dq_hip.h).  The compute runs in hand-written gfx950 kernels; there is
+no CPU fallback: without the built library or without a HIP device every
+compute call raises.
+
+The directory name is not a Python identifier, so load it with
+``load_package()`` (tests/, bench.py and __graft_entry__.py do).
+
+Reference-named entry points (same argument meaning, host numpy arrays):
+    quant_recurse(pixels, num_clusters, all_pixels_unique=1) -> (out, colortable)
+    map_colors_mps(pixels, colortable)                       -> out
+    quant_varpart_fast(pixels, num_clusters, max_iters=10)   -> colortable
+Device-resident entry points (torch tensors / raw device pointers on HBM):
+    quant_device, cluster_device, map_device
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libdivquant_hip.so")
+
+STAT_KINDS = ["pass_init", "pass_split", "pass_kmeans", "pass_klast",
+              "epilogue", "partition", "map_cells", "map"]
+
+_lib = None
+
+
+class DivQuantError(RuntimeError):
+    pass
+
+
+def lib():
+    """The ctypes handle of libdivquant_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DivQuantError("libdivquant_hip.so is not built (run __graft_entry__.build() "
+                            "or make -C clusteringsegmentation-1_amd)")
+    L = ctypes.CDLL(LIB_PATH)
+    u32p, vp = ctypes.POINTER(ctypes.c_uint32), ctypes.c_void_p
+    c = ctypes
+    sigs = {
+        "dq_hip_abi_version": ([], c.c_int),
+        "dq_hip_device_count": ([], c.c_int),
+        "dq_hip_quant": ([vp, c.c_uint32, vp, u32p, vp, c.c_int, c.c_int], c.c_int),
+        "dq_hip_map": ([vp, c.c_uint32, vp, vp, c.c_int], c.c_int),
+        "dq_hip_quant_dev": ([c.c_int, vp, c.c_uint32, vp, u32p, vp, c.c_int, vp], c.c_int),
+        "dq_hip_cluster_dev": ([c.c_int, vp, c.c_uint32, u32p, vp, c.c_int, vp], c.c_int),
+        "dq_hip_map_dev": ([c.c_int, vp, c.c_uint32, vp, vp, c.c_int, vp], c.c_int),
+        "dq_hip_last_centroids": ([c.c_int, vp, vp, c.c_int], c.c_int),
+        "dq_hip_last_trace": ([c.c_int, vp, c.c_int], c.c_int),
+        "dq_hip_last_rounds": ([c.c_int], c.c_int),
+        "dq_hip_last_points_swept": ([c.c_int], c.c_uint64),
+        "dq_hip_set_timing": ([c.c_int, c.c_int], None),
+        "dq_hip_reset_stats": ([c.c_int], None),
+        "dq_hip_get_stat": ([c.c_int, c.c_int, c.POINTER(c.c_uint64), c.POINTER(c.c_double),
+                             c.POINTER(c.c_double)], c.c_int),
+        "dq_hip_stat_name": ([c.c_int], c.c_char_p),
+        "quant_recurse": ([c.c_uint32, vp, vp, u32p, vp, c.c_int], None),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _require_gpu():
+    if lib().dq_hip_device_count() < 1:
+        raise DivQuantError("no HIP device visible: the DivQuant hot path runs only on the GPU")
+
+
+def _u32(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+# ---------------------------------------------------------------------------
+# Reference-named host entry points.
+def quant_recurse(pixels, num_clusters, all_pixels_unique=1):
+    """quant_recurse (DivQuant/quant_util.cpp:20-158): returns (out, colortable)."""
+    _require_gpu()
+    px = _u32(pixels).reshape(-1)
+    if px.size == 0 or num_clusters <= 0:
+        raise DivQuantError("numPixels and numClusters must be > 0")
+    out = np.zeros(px.size, np.uint32)
+    ct = np.zeros(num_clusters, np.uint32)
+    k = ctypes.c_uint32(num_clusters)
+    lib().quant_recurse(px.size, _ptr(px), _ptr(out), ctypes.byref(k), _ptr(ct), int(all_pixels_unique))
+    return out, ct[:k.value].copy()
+
+
+def map_colors_mps(pixels, colortable):
+    """map_colors_mps (DivQuant/DivQuantMapColors.cpp:243-539)."""
+    _require_gpu()
+    px = _u32(pixels).reshape(-1)
+    ct = _u32(colortable).reshape(-1)
+    if ct.size == 0:
+        raise DivQuantError("colormapSize must be > 0")
+    out = np.zeros(px.size, np.uint32)
+    if lib().dq_hip_map(_ptr(px), px.size, _ptr(out), _ptr(ct), ct.size) < 0:
+        raise DivQuantError("dq_hip_map failed")
+    return out
+
+
+def quant_varpart_fast(pixels, num_clusters, max_iters=10, device=0):
+    """quant_varpart_fast (DivQuantCluster.cpp:1099-1179), uniform-weight path:
+    the non-empty cluster colours in cluster-index order (not deduplicated)."""
+    import torch
+    _require_gpu()
+    px = torch.from_numpy(_u32(pixels).reshape(-1).view(np.int32)).to(f"cuda:{device}")
+    ct, _ = cluster_device(px, num_clusters, max_iters=max_iters, device=device)
+    return ct
+
+
+# ---------------------------------------------------------------------------
+# Device-resident entry points.  `t_in` / `t_out` are torch tensors (int32 or
+# uint32 storage, contiguous, on cuda:device) or raw integer device pointers.
+def _dptr(t):
+    return ctypes.c_void_p(t if isinstance(t, int) else t.data_ptr())
+
+
+def _nelem(t, n):
+    return n if n is not None else t.numel()
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def quant_device(t_in, t_out, num_clusters, max_iters=10, device=0, n=None, stream=None):
+    """Cluster + dedup + map of device-resident pixels; returns (colortable, empty)."""
+    n = _nelem(t_in, n)
+    ct = np.zeros(num_clusters, np.uint32)
+    k = ctypes.c_uint32(num_clusters)
+    r = lib().dq_hip_quant_dev(device, _dptr(t_in), n, _dptr(t_out), ctypes.byref(k), _ptr(ct),
+                               max_iters, _stream_ptr(stream))
+    if r < 0:
+        raise DivQuantError("dq_hip_quant_dev: bad arguments")
+    return ct[:k.value].copy(), r
+
+
+def cluster_device(t_in, num_clusters, max_iters=10, device=0, n=None, stream=None):
+    """DivQuantCluster on device-resident pixels; returns (colortable, empty)."""
+    n = _nelem(t_in, n)
+    ct = np.zeros(num_clusters, np.uint32)
+    k = ctypes.c_uint32(num_clusters)
+    r = lib().dq_hip_cluster_dev(device, _dptr(t_in), n, ctypes.byref(k), _ptr(ct), max_iters,
+                                 _stream_ptr(stream))
+    if r < 0:
+        raise DivQuantError("dq_hip_cluster_dev: bad arguments")
+    return ct[:k.value].copy(), r
+
+
+def map_device(t_in, t_out, colortable, device=0, n=None, stream=None):
+    n = _nelem(t_in, n)
+    ct = _u32(colortable).reshape(-1)
+    if lib().dq_hip_map_dev(device, _dptr(t_in), n, _dptr(t_out), _ptr(ct), ct.size,
+                            _stream_ptr(stream)) < 0:
+        raise DivQuantError("dq_hip_map_dev: bad arguments")
+
+
+def last_centroids(k, device=0):
+    """(means[k,3] float64, sizes[k] int64) of the last clustering on `device`."""
+    means = np.zeros((k, 3), np.float64)
+    sizes = np.zeros(k, np.int64)
+    if lib().dq_hip_last_centroids(device, _ptr(means), _ptr(sizes), k) < 0:
+        raise DivQuantError("k does not match the last clustering")
+    return means, sizes
+
+
+def last_trace(k, device=0):
+    tr = np.zeros((max(k - 1, 0), 4), np.int64)
+    if lib().dq_hip_last_trace(device, _ptr(tr) if tr.size else None, k) < 0:
+        raise DivQuantError("k does not match the last clustering")
+    return tr
+
+
+def last_rounds(device=0):
+    return lib().dq_hip_last_rounds(device)
+
+
+def last_points_swept(device=0):
+    return int(lib().dq_hip_last_points_swept(device))
+
+
+def set_timing(on, device=0):
+    lib().dq_hip_set_timing(device, 1 if on else 0)
+
+
+def reset_stats(device=0):
+    lib().dq_hip_reset_stats(device)
+
+
+def get_stats(device=0):
+    """{kind: (launches, total_ms, algorithmic_bytes)} from HIP events on the launch stream."""
+    res = {}
+    for i, name in enumerate(STAT_KINDS):
+        l, ms, b = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+        lib().dq_hip_get_stat(device, i, ctypes.byref(l), ctypes.byref(ms), ctypes.byref(b))
+        res[name] = (int(l.value), float(ms.value), float(b.value))
+    return res

@@ -1,0 +1,355 @@
+// dq_abi.cpp -- the exported surface of libdivquant_hip.so:
+//   * the C ABI of include/dq_hip.h (device- and host-pointer entry points);
+//   * the reference signatures of include/DivQuantHeader.h and
+//     include/quant_util.h, implemented on top of it.
+// The product path has no CPU fallback: without a HIP device every compute
+// entry point aborts with a message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/DivQuantHeader.h"
+#include "../../include/dq_hip.h"
+#include "../../include/quant_util.h"
+#include "dq_engine.h"
+
+using dq::Engine;
+using dq::engine_for;
+
+namespace {
+
+int current_device() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    dq::die("no HIP device", __FILE__, __LINE__,
+            "libdivquant_hip has no CPU fallback; run on an MI355X (gfx950)");
+  int d = 0;
+  DQ_HIP(hipGetDevice(&d));
+  return d;
+}
+
+bool quiet() {
+  const char* q = std::getenv("DQ_HIP_QUIET");
+  return q && *q && *q != '0';
+}
+
+double now_ms() {
+  using namespace std::chrono;
+  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+// First-occurrence colortable dedup (quant_util.cpp:93-118).
+uint32_t dedup_colortable(uint32_t* ct, uint32_t k) {
+  std::unordered_set<uint32_t> seen;
+  seen.reserve(k * 2 + 1);
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < k; ++i)
+    if (seen.insert(ct[i]).second) ct[m++] = ct[i];
+  return m;
+}
+
+void report_empty(int num_empty) {
+  if (num_empty) std::fprintf(stderr, "# empty clusters: %d\n", num_empty);   // :1067-1069
+}
+
+}  // namespace
+
+// =========================================================================
+// C ABI (include/dq_hip.h)
+// =========================================================================
+extern "C" {
+
+int dq_hip_abi_version(void) { return DQ_HIP_ABI_VERSION; }
+
+int dq_hip_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int dq_hip_cluster_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* k,
+                       uint32_t* ct, int max_iters, void* stream) {
+  if (!d_in || !k || !ct || n == 0 || *k == 0 || max_iters < 1) return -1;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  int empty = 0;
+  const int out = e.cluster(d_in, n, (int)*k, max_iters, ct, &empty, (hipStream_t)stream);
+  *k = (uint32_t)out;
+  return empty;
+}
+
+int dq_hip_map_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out,
+                   const uint32_t* ct, int k, void* stream) {
+  if (!d_in || !d_out || !ct || k <= 0) return -1;
+  if (n == 0) return 0;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  e.map(d_in, n, d_out, ct, k, (hipStream_t)stream);
+  return 0;
+}
+
+int dq_hip_quant_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out,
+                     uint32_t* k, uint32_t* ct, int max_iters, void* stream) {
+  if (!d_in || !d_out || !k || !ct || n == 0 || *k == 0 || max_iters < 1) return -1;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  int empty = 0;
+  uint32_t kk = (uint32_t)e.cluster(d_in, n, (int)*k, max_iters, ct, &empty, (hipStream_t)stream);
+  kk = dedup_colortable(ct, kk);
+  e.map(d_in, n, d_out, ct, (int)kk, (hipStream_t)stream);
+  *k = kk;
+  return empty;
+}
+
+int dq_hip_quant(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* k,
+                 uint32_t* ct, int uniq, int ngpus) {
+  (void)uniq;
+  (void)ngpus;
+  if (!in || !out || !k || !ct || n == 0 || *k == 0) return -1;
+  Engine& e = engine_for(current_device());
+  std::lock_guard<std::mutex> g(e.mutex());
+  hipStream_t st = e.stream();
+  e.stage_in(in, n, st);
+  int empty = 0;
+  uint32_t kk = (uint32_t)e.cluster(e.staged_in(), n, (int)*k, 10, ct, &empty, st);
+  kk = dedup_colortable(ct, kk);
+  e.map(e.staged_in(), n, e.staged_out(), ct, (int)kk, st);
+  DQ_HIP(hipMemcpyAsync(out, e.staged_out(), (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  DQ_HIP(hipStreamSynchronize(st));
+  *k = kk;
+  return empty;
+}
+
+int dq_hip_map(const uint32_t* in, uint32_t n, uint32_t* out, const uint32_t* ct, int k) {
+  if (!in || !out || !ct || k <= 0) return -1;
+  if (n == 0) return 0;
+  Engine& e = engine_for(current_device());
+  std::lock_guard<std::mutex> g(e.mutex());
+  hipStream_t st = e.stream();
+  e.stage_in(in, n, st);
+  e.map(e.staged_in(), n, e.staged_out(), ct, k, st);
+  DQ_HIP(hipMemcpyAsync(out, e.staged_out(), (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  DQ_HIP(hipStreamSynchronize(st));
+  return 0;
+}
+
+int dq_hip_last_centroids(int device, double* means, int64_t* sizes, int k) {
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  if ((size_t)k != e.last_sizes.size()) return -1;
+  if (means) std::memcpy(means, e.last_means.data(), sizeof(double) * 3 * k);
+  if (sizes) std::memcpy(sizes, e.last_sizes.data(), sizeof(int64_t) * k);
+  return 0;
+}
+
+int dq_hip_last_trace(int device, int64_t* trace, int k) {
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  if (k < 1 || (size_t)(k - 1) * 4 != e.last_trace.size()) return -1;
+  if (trace && k > 1) std::memcpy(trace, e.last_trace.data(), sizeof(int64_t) * 4 * (k - 1));
+  return 0;
+}
+
+int dq_hip_last_rounds(int device) { return engine_for(device).last_rounds; }
+
+uint64_t dq_hip_last_points_swept(int device) { return engine_for(device).last_points_swept; }
+
+void dq_hip_set_timing(int device, int on) { engine_for(device).set_timing(on != 0); }
+
+void dq_hip_reset_stats(int device) { engine_for(device).reset_stats(); }
+
+int dq_hip_get_stat(int device, int kind, uint64_t* launches, double* ms, double* bytes) {
+  if (kind < 0 || kind >= dq::ST_COUNT) return -1;
+  const dq::KernelStat& s = engine_for(device).stats[kind];
+  if (launches) *launches = s.launches;
+  if (ms) *ms = s.ms;
+  if (bytes) *bytes = s.bytes;
+  return 0;
+}
+
+const char* dq_hip_stat_name(int kind) {
+  static const char* names[] = {"pass_init", "pass_split", "pass_kmeans", "pass_klast",
+                                "epilogue", "partition", "map_cells", "map"};
+  if (kind < 0 || kind >= dq::ST_COUNT) return "";
+  return names[kind];
+}
+
+// =========================================================================
+// Reference signatures (include/quant_util.h, include/DivQuantHeader.h)
+// =========================================================================
+
+// quant_util.cpp:20-158.
+void quant_recurse(uint32_t numPixels, const uint32_t* inPixelsPtr, uint32_t* outPixelsPtr,
+                   uint32_t* numClustersPtr, uint32_t* outColortablePtr, int allPixelsUnique) {
+  (void)allPixelsUnique;   // both paths run the uniform-weight kernels
+  if (numPixels == 0 || *numClustersPtr == 0)
+    dq::die("quant_recurse", __FILE__, __LINE__, "numPixels and *numClustersPtr must be > 0");
+  Engine& e = engine_for(current_device());
+  std::lock_guard<std::mutex> g(e.mutex());
+  hipStream_t st = e.stream();
+  const double t0 = now_ms();
+  e.stage_in(inPixelsPtr, numPixels, st);
+  int empty = 0;
+  uint32_t k = (uint32_t)e.cluster(e.staged_in(), numPixels, (int)*numClustersPtr, 10,
+                                   outColortablePtr, &empty, st);
+  report_empty(empty);
+  *numClustersPtr = k;
+  const double t1 = now_ms();
+  if (!quiet()) {
+    long el = (long)(t1 - t0);
+    std::printf("quant_varpart_fast() elapsed: %ld ms aka %0.2f s\n", el, el / 1000.0f);
+  }
+  k = dedup_colortable(outColortablePtr, k);
+  *numClustersPtr = k;
+  e.map(e.staged_in(), numPixels, e.staged_out(), outColortablePtr, (int)k, st);
+  DQ_HIP(hipMemcpyAsync(outPixelsPtr, e.staged_out(), (size_t)numPixels * 4,
+                        hipMemcpyDeviceToHost, st));
+  DQ_HIP(hipStreamSynchronize(st));
+  if (!quiet()) {
+    long el = (long)(now_ms() - t1);
+    std::printf("map_colors_mps() elapsed: %ld ms aka %0.2f s\n", el, el / 1000.0f);
+  }
+}
+
+}  // extern "C"
+
+// DivQuantMapColors.cpp:243-539.
+void map_colors_mps(const uint32_t* inPixelsPtr, uint32_t numPixels, uint32_t* outPixelsPtr,
+                    uint32_t* outColortablePtr, int colormapSize) {
+  if (colormapSize <= 0)
+    dq::die("map_colors_mps", __FILE__, __LINE__, "colormapSize must be > 0");
+  dq_hip_map(inPixelsPtr, numPixels, outPixelsPtr, outColortablePtr, colormapSize);
+}
+
+// DivQuantCluster.cpp:1099-1179.
+void quant_varpart_fast(const uint32_t numPixels, const uint32_t* inPixels, uint32_t* tmpPixels,
+                        const uint32_t numRows, const uint32_t numCols, uint32_t* numClustersPtr,
+                        uint32_t* colortablePtr, const int num_bits, const int dec_factor,
+                        const int max_iters, const int allPixelsUnique) {
+  (void)tmpPixels;
+  (void)numRows;
+  (void)numCols;
+  (void)allPixelsUnique;
+  if (!validate_num_bits((uchar)num_bits))
+    dq::die("quant_varpart_fast", __FILE__, __LINE__, "invalid num_bits");
+  if (num_bits != 8 || dec_factor != 1)
+    dq::die("quant_varpart_fast", __FILE__, __LINE__,
+            "num_bits != 8 or dec_factor != 1 (cut_bits/decimation path) is out of scope; "
+            "quant_recurse never uses it (quant_util.cpp:31-36)");
+  if (max_iters < 1)
+    dq::die("quant_varpart_fast", __FILE__, __LINE__, "max_iters < 1 is not supported");
+  Engine& e = engine_for(current_device());
+  std::lock_guard<std::mutex> g(e.mutex());
+  hipStream_t st = e.stream();
+  e.stage_in(inPixels, numPixels, st);
+  int empty = 0;
+  const int k = e.cluster(e.staged_in(), numPixels, (int)*numClustersPtr, max_iters,
+                          colortablePtr, &empty, st);
+  report_empty(empty);
+  *numClustersPtr = (uint32_t)k;
+}
+
+// DivQuantMapColors.cpp:205-220.
+double get_double_scale(const uint32_t* inPixels, const uint32_t numPixels) {
+  (void)inPixels;
+  const int numRows = 1, dec = 1;
+  const int numCols = (int)numPixels;
+  return 1.0 / (ceil(numRows / (double)dec) * ceil(numCols / (double)dec));
+}
+
+// DivQuantMapColors.cpp:43-51.
+void check_mem(const int x) {
+  if (x != 0) {
+    std::fprintf(stderr, "Insufficient memory !\n");
+    std::abort();
+  }
+}
+
+// DivQuantMisc.cpp:18-46.
+clock_t start_timer(void) { return clock(); }
+double stop_timer(const clock_t start_time) {
+  return ((double)(clock() - start_time)) / CLOCKS_PER_SEC;
+}
+long timediff(clock_t t1, clock_t t2) {
+  return (long)(((double)t2 - t1) / CLOCKS_PER_SEC * 1000);
+}
+int validate_num_bits(const uchar num_bits) {
+  if (!(0 < num_bits && num_bits <= 8)) {
+    std::fprintf(stderr, "Number of bits per channel ( %d ) must be in [1,8] !\n", num_bits);
+    return 0;
+  }
+  return 1;
+}
+
+// DivQuantUni.cpp:28-100: drop the low (8 - num_bits) bits of each channel
+// and shift the rest down (in place allowed).
+void cut_bits(const uint32_t* inPixels, const uint32_t numPixels, uint32_t* outPixels,
+              const uchar num_bits_red, const uchar num_bits_green, const uchar num_bits_blue) {
+  if (!validate_num_bits(num_bits_red) || !validate_num_bits(num_bits_green) ||
+      !validate_num_bits(num_bits_blue))
+    return;
+  const uint32_t sr = 8 - num_bits_red, sg = 8 - num_bits_green, sb = 8 - num_bits_blue;
+  for (uint32_t i = 0; i < numPixels; ++i) {
+    const uint32_t p = inPixels[i];
+    const uint32_t R = ((p >> 16) & 0xFF) >> sr;
+    const uint32_t G = ((p >> 8) & 0xFF) >> sg;
+    const uint32_t B = (p & 0xFF) >> sb;
+    outPixels[i] = (R << 16) | (G << 8) | B;
+  }
+}
+
+// DivQuantMapColors.cpp:82-203: unique colours with weights count*norm in the
+// reference's output order -- hash buckets ascending (HASH(R,G,B) =
+// (R*33023 + G*30013 + B*27011) & 0x7fffffff) % 20023), and inside a bucket
+// the most recently first-seen colour first (the chains are prepended).
+// The pixel index quirk inPixels[ic + ir*numRows] is kept (:124).
+double* calc_color_table(const uint32_t* inPixels, const uint32_t numPixels, uint32_t* outPixels,
+                         const uint32_t numRows, const uint32_t numCols, const int dec_factor,
+                         int* num_colors) {
+  (void)numPixels;
+  if (dec_factor <= 0) {
+    std::fprintf(stderr, "Decimation factor ( %d ) should be positive !\n", dec_factor);
+    return NULL;
+  }
+  struct Ent { uint32_t color; uint32_t first; uint32_t count; uint32_t hash; };
+  std::unordered_map<uint32_t, uint32_t> where;
+  std::vector<Ent> ents;
+  for (uint32_t ir = 0; ir < numRows; ir += dec_factor) {
+    for (uint32_t ic = 0; ic < numCols; ic += dec_factor) {
+      const uint32_t p = inPixels[ic + (ir * numRows)] & 0xFFFFFF;
+      auto it = where.find(p);
+      if (it != where.end()) {
+        ents[it->second].count++;
+      } else {
+        const long R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
+        const uint32_t h = (uint32_t)(((R * 33023 + G * 30013 + B * 27011) & 0x7fffffff) % 20023);
+        where.emplace(p, (uint32_t)ents.size());
+        ents.push_back({p, (uint32_t)ents.size(), 1u, h});
+      }
+    }
+  }
+  std::vector<uint32_t> order(ents.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    if (ents[a].hash != ents[b].hash) return ents[a].hash < ents[b].hash;
+    return ents[a].first > ents[b].first;
+  });
+  *num_colors = (int)ents.size();
+  double* weights = new double[ents.size()];
+  const double norm = 1.0 / (ceil(numRows / (double)dec_factor) * ceil(numCols / (double)dec_factor));
+  for (size_t i = 0; i < order.size(); ++i) {
+    const Ent& en = ents[order[i]];
+    outPixels[i] = en.color;
+    weights[i] = norm * en.count;
+  }
+  return weights;
+}

@@ -1,0 +1,76 @@
+/*
+ * dq_hip.h -- the thin C ABI of libdivquant_hip.so (MI355X / gfx950).
+ *
+ * Plain pointers and sizes only (no torch, no HIP types in the signatures;
+ * `stream` is a hipStream_t passed as void*, NULL = the library's stream).
+ * The reference-signature wrappers (include/DivQuantHeader.h,
+ * include/quant_util.h) are implemented on top of these entry points; an FFI
+ * (ctypes, cgo, JNI...) can bind them directly -- see INTEGRATION.md.
+ *
+ * Errors: HIP/runtime failures abort the process with a message on stderr,
+ * like the reference's abort() paths (DivQuantCluster.cpp:1021-1026,
+ * DivQuantMapColors.cpp:43-51).  Invalid arguments return a negative code.
+ */
+#ifndef DQ_HIP_H
+#define DQ_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQ_HIP_ABI_VERSION 1
+
+int dq_hip_abi_version(void);
+/* Number of visible HIP devices (0 when none). */
+int dq_hip_device_count(void);
+
+/* ---- host-pointer entry points (SURVEY 8b build-side shim) ---------------
+ * dq_hip_quant: quant_recurse semantics (quant_util.cpp:20-158) without the
+ * stdout timer lines.  uniq: allPixelsUnique (both values run the
+ * uniform-weight kernels).  ngpus <= 1: current device.
+ * Returns the number of empty clusters (>= 0) or < 0 on bad arguments. */
+int dq_hip_quant(const uint32_t *in, uint32_t n, uint32_t *out, uint32_t *k,
+                 uint32_t *ct, int uniq, int ngpus);
+/* map_colors_mps semantics (DivQuantMapColors.cpp:243-539). */
+int dq_hip_map(const uint32_t *in, uint32_t n, uint32_t *out,
+               const uint32_t *ct, int k);
+
+/* ---- device-pointer entry points (inputs already resident in HBM) --------
+ * d_in/d_out: device pointers on `device`; k/ct: host.  Synchronous with
+ * respect to the host on return (ct and *k are final). */
+int dq_hip_quant_dev(int device, const uint32_t *d_in, uint32_t n,
+                     uint32_t *d_out, uint32_t *k, uint32_t *ct,
+                     int max_iters, void *stream);
+/* Clustering only (quant_varpart_fast, DivQuantCluster.cpp:1099-1179):
+ * writes the non-empty cluster colours (cluster-index order, NOT deduped). */
+int dq_hip_cluster_dev(int device, const uint32_t *d_in, uint32_t n,
+                       uint32_t *k, uint32_t *ct, int max_iters, void *stream);
+int dq_hip_map_dev(int device, const uint32_t *d_in, uint32_t n,
+                   uint32_t *d_out, const uint32_t *ct, int k, void *stream);
+
+/* ---- diagnostics of the last clustering on `device` ----------------------
+ * means: k*3 doubles (the reference's mean[ic] per cluster index, the north
+ * star's "float centroids"); sizes: k cluster sizes; trace: (k-1)*4 of
+ * new_index, old_index, |C|, |new| per split.  Return 0 or < 0. */
+int dq_hip_last_centroids(int device, double *means, int64_t *sizes, int k);
+int dq_hip_last_trace(int device, int64_t *trace, int k);
+int dq_hip_last_rounds(int device);
+/* Points read by all statistics passes of the last clustering. */
+uint64_t dq_hip_last_points_swept(int device);
+
+/* ---- per-kernel timing (HIP events on the launch stream) -----------------
+ * kinds: 0 init pass, 1 split pass, 2 2-means pass, 3 last 2-means pass,
+ * 4 epilogue, 5 partition, 6 map cells, 7 map.  bytes = algorithmic bytes. */
+void dq_hip_set_timing(int device, int on);
+void dq_hip_reset_stats(int device);
+int dq_hip_get_stat(int device, int kind, uint64_t *launches, double *ms,
+                    double *bytes);
+const char *dq_hip_stat_name(int kind);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DQ_HIP_H */

@@ -1,0 +1,326 @@
+// =============================================================================
+// oracle/dq_oracle.cpp -- CPU restatement of the DivQuant hot path.
+//
+// TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+// cpu_baseline leg of bench.py may load this library, and only as the checker
+// (or the timed CPU baseline) -- never as the thing measured or shipped.  The
+// product library (clusteringsegmentation-1_amd/csrc) must not link it.
+//
+// What it restates (all citations relative to /root/reference):
+//   * quant_recurse                    DivQuant/quant_util.cpp:20-158
+//   * quant_varpart_fast, UW dispatch  DivQuant/DivQuantCluster.cpp:1099-1179
+//   * DivQuantClusterInitMeanAndVar    DivQuant/DivQuantCluster.cpp:36-123
+//   * DivQuantCluster<true,MT,true>    DivQuant/DivQuantCluster.cpp:133-1097
+//   * map_colors_mps                   DivQuant/DivQuantMapColors.cpp:243-539
+//
+// How it is restated (deliberately NOT the reference's code shape):
+//   - every cluster keeps its own vector of packed pixels instead of the
+//     reference's member[] array + O(N) gather per split (:894-1026).  Uniform
+//     weight sums are exact integers, so visiting order is irrelevant;
+//   - sums are uint64 integers converted to double once; the reference's
+//     0xFFFF-point uint32 chunks folded into doubles (:438-559, :639-777) are
+//     exact too (every partial < 2^53), so the doubles are identical;
+//   - the FP64 epilogue is spelled out operation by operation with the same
+//     evaluation order as the reference (no contraction: built -ffp-contract=off).
+//
+// Parity pin: tests/test_oracle_golden.py checks this file against the 7
+// Test/DivQuantTest.m known-answer tests and against outputs of the unmodified
+// reference compiled by oracle/Makefile (fixtures in tests/golden/).
+// =============================================================================
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+struct Sums {            // exact integer statistics of a point set
+  uint64_t n = 0;
+  uint64_t s[3] = {0, 0, 0};   // sum R, G, B
+  uint64_t q[3] = {0, 0, 0};   // sum R^2, G^2, B^2
+};
+
+inline void unpack(uint32_t p, uint32_t c[3]) {
+  c[0] = (p >> 16) & 0xFF;  // R
+  c[1] = (p >> 8) & 0xFF;   // G
+  c[2] = p & 0xFF;          // B
+}
+
+struct Cluster {
+  std::vector<uint32_t> px;  // packed 0x00RRGGBB points of this cluster
+  double weight = 0.0;
+  double mean[3] = {0, 0, 0};
+  double var[3] = {0, 0, 0};
+  double tse = 0.0;
+  int64_t size = 0;
+};
+
+}  // namespace
+
+extern "C" {
+
+// One greedy DivQuant run, uniform-weight path (allPixelsUnique=1, num_bits=8,
+// dec_factor=1).  Writes <=K colours to ct and the number to *k_inout, exactly
+// like DivQuantCluster's tail (DivQuantCluster.cpp:1029-1094).
+//   means_out  : optional [K*3] final double centroids per cluster index
+//                (NaN-free only where sizes_out>0) -- the north star's 1e-5 check.
+//   sizes_out  : optional [K] cluster sizes per index.
+//   trace_out  : optional [(K-1)*4] per split: new_index, old_index, |C|, |new|.
+int dqo_cluster(uint32_t num_points, const uint32_t* data, uint32_t* k_inout,
+                uint32_t* ct, int max_iters, double* means_out,
+                int64_t* sizes_out, int64_t* trace_out) {
+  if (num_points == 0 || *k_inout == 0 || max_iters < 1) return -1;
+  const int K = (int)*k_inout;
+  // get_double_scale: 1/(ceil(1/1)*ceil(N/1)) (DivQuantMapColors.cpp:205-220)
+  const double s = 1.0 / (std::ceil(1 / 1.0) * std::ceil(num_points / 1.0));
+
+  std::vector<Cluster> cl(K);
+  cl[0].px.assign(data, data + num_points);
+  for (auto& p : cl[0].px) p &= 0xFFFFFF;
+  cl[0].weight = 1.0;                       // :329, literal 1.0 (not N*s)
+  cl[0].size = num_points;
+  int old_index = 0;
+
+  for (int new_index = 1; new_index < K; ++new_index) {
+    Cluster& C = cl[old_index];
+    const double tw = C.weight;
+    double tm[3], tv[3];
+    if (new_index == 1) {                   // :355-358 -> InitMeanAndVar :49-104
+      Sums r;
+      for (uint32_t p : C.px) {
+        uint32_t c[3];
+        unpack(p, c);
+        for (int a = 0; a < 3; ++a) { r.s[a] += c[a]; r.q[a] += c[a] * c[a]; }
+      }
+      for (int a = 0; a < 3; ++a) {
+        double m = (double)r.s[a];
+        double v = (double)r.q[a];
+        m *= s;
+        v *= s;
+        v -= m * m;
+        tm[a] = m;
+        tv[a] = v;
+      }
+    } else {                                // :365-374
+      for (int a = 0; a < 3; ++a) { tm[a] = C.mean[a]; tv[a] = C.var[a]; }
+    }
+
+    // STEPS 1&2 (:388-403): max-variance axis, strict '<' keeps lower axis.
+    int axis = 0;
+    double maxv = tv[0], cut = tm[0];
+    if (maxv < tv[1]) { maxv = tv[1]; axis = 1; cut = tm[1]; }
+    if (maxv < tv[2]) { axis = 2; cut = tm[2]; }
+
+    // STEP 3 split pass (:438-559): new side iff cut_pos < v_axis.
+    Sums ns;
+    for (uint32_t p : C.px) {
+      uint32_t c[3];
+      unpack(p, c);
+      if (cut < (double)c[axis]) {
+        ns.n++;
+        for (int a = 0; a < 3; ++a) ns.s[a] += c[a];
+      }
+    }
+    double nm[3], om[3], nw, ow;
+    nw = (double)ns.n * s;                               // :566
+    ow = tw - nw;                                        // :576
+    for (int a = 0; a < 3; ++a) nm[a] = ((double)ns.s[a] * s) / nw;   // :562,579
+    for (int a = 0; a < 3; ++a) om[a] = (tw * tm[a] - nw * nm[a]) / ow;  // :596
+
+    // Local 2-means (:613-811).
+    std::vector<uint32_t> keep, moved;
+    double nvq[3] = {0, 0, 0};
+    int64_t new_size = 0;
+    for (int it = 0; it < max_iters; ++it) {
+      const bool last = (it == max_iters - 1);
+      double lhs = 0.5 * (om[0] * om[0] - nm[0] * nm[0] + om[1] * om[1] -
+                          nm[1] * nm[1] + om[2] * om[2] - nm[2] * nm[2]);  // :616
+      double rr = om[0] - nm[0], rg = om[1] - nm[1], rb = om[2] - nm[2];
+      Sums k;
+      if (last) { keep.clear(); moved.clear(); }
+      for (uint32_t p : C.px) {
+        uint32_t c[3];
+        unpack(p, c);
+        double red = c[0], green = c[1], blue = c[2];
+        if (lhs < ((rr * red) + (rg * green) + (rb * blue))) {   // :683 -> old
+          if (last) keep.push_back(p);
+        } else {                                                 // new (ties, NaN)
+          k.n++;
+          for (int a = 0; a < 3; ++a) k.s[a] += c[a];
+          if (last) {
+            for (int a = 0; a < 3; ++a) k.q[a] += c[a] * c[a];
+            moved.push_back(p);
+          }
+        }
+      }
+      new_size = (int64_t)k.n;
+      double nsum[3], nsq[3];
+      for (int a = 0; a < 3; ++a) {
+        nsum[a] = (double)k.s[a] * s;                   // :788-790
+        nsq[a] = (double)k.q[a] * s;                    // :794-796
+      }
+      nw = (double)new_size * s;                        // :792
+      for (int a = 0; a < 3; ++a) nm[a] = nsum[a] / nw; // :800-802
+      ow = tw - nw;                                     // :805
+      for (int a = 0; a < 3; ++a) om[a] = (tw * tm[a] - nw * nm[a]) / ow;  // :808
+      for (int a = 0; a < 3; ++a) nvq[a] = nsq[a];
+    }
+
+    Cluster& D = cl[new_index];
+    const int64_t parent_size = C.size;
+    if (trace_out) {
+      int64_t* t = trace_out + 4 * (new_index - 1);
+      t[0] = new_index; t[1] = old_index; t[2] = parent_size; t[3] = new_size;
+    }
+    C.size = parent_size - new_size;                    // :820-821
+    D.size = new_size;
+    for (int a = 0; a < 3; ++a) { C.mean[a] = om[a]; D.mean[a] = nm[a]; }
+    C.px.swap(keep);
+    D.px.swap(moved);
+    std::vector<uint32_t>().swap(keep);
+    std::vector<uint32_t>().swap(moved);
+
+    if (new_index == K - 1) break;                      // :823-832
+
+    double nv[3], ov[3];
+    for (int a = 0; a < 3; ++a) nv[a] = nvq[a] / nw - nm[a] * nm[a];   // :836-838
+    for (int a = 0; a < 3; ++a) {                                       // :845-855
+      double dn = nm[a] - tm[a];
+      double dox = om[a] - tm[a];
+      ov[a] = ((tw * tv[a] - nw * (nv[a] + dn * dn)) / ow) - dox * dox;
+    }
+    for (int a = 0; a < 3; ++a) { C.var[a] = ov[a]; D.var[a] = nv[a]; }
+    C.weight = ow;                                      // :862-863
+    D.weight = nw;
+    C.tse = ow * (ov[0] + ov[1] + ov[2]);               // :870-871
+    D.tse = nw * (nv[0] + nv[1] + nv[2]);
+
+    // STEP 4 (:876-887): first index with max TSE above DBL_MIN; if none,
+    // old_index is left unchanged (the old half is split again).
+    double best = DBL_MIN;
+    for (int ic = 0; ic <= new_index; ++ic) {
+      if (best < cl[ic].tse) { best = cl[ic].tse; old_index = ic; }
+    }
+  }
+
+  // Final centres (:1029-1094): round, pack, drop empty clusters.
+  int out = 0;
+  for (int ic = 0; ic < K; ++ic) {
+    if (means_out) {
+      for (int a = 0; a < 3; ++a) means_out[3 * ic + a] = cl[ic].mean[a];
+    }
+    if (sizes_out) sizes_out[ic] = cl[ic].size;
+    if (cl[ic].size > 0) {
+      uint32_t R = (uint8_t)(cl[ic].mean[0] + 0.5);
+      uint32_t G = (uint8_t)(cl[ic].mean[1] + 0.5);
+      uint32_t B = (uint8_t)(cl[ic].mean[2] + 0.5);
+      ct[out++] = (R << 16) | (G << 8) | B;
+    }
+  }
+  *k_inout = (uint32_t)out;
+  return K - out;   // number of empty clusters
+}
+
+// map_colors_mps restated (DivQuantMapColors.cpp:243-539): palette sorted by
+// R+G+B with std::sort (same comparator => same unstable order on the same
+// libstdc++, :227-238), start entry from a rounded-midpoint LUT (:331-383),
+// alternating up/down walk pruned by floor(d^2/3) (:285-311, :385-521).
+struct PalEntry { int r, g, b, w; };
+
+void dqo_map(const uint32_t* in, uint32_t n, uint32_t* out,
+             const uint32_t* ct, int k) {
+  std::vector<PalEntry> pal(k);
+  for (int i = 0; i < k; ++i) {
+    uint32_t c[3];
+    unpack(ct[i], c);
+    pal[i] = {(int)c[0], (int)c[1], (int)c[2], (int)(c[0] + c[1] + c[2])};
+  }
+  std::sort(pal.begin(), pal.end(),
+            [](const PalEntry& a, const PalEntry& b) { return a.w < b.w; });
+  int ssd_buf[2 * 765 + 1];
+  int* ssd = ssd_buf + 765;
+  ssd[0] = 0;
+  for (int d = 1; d <= 765; ++d) ssd[d] = ssd[-d] = (int)((d * d) / 3.0);
+  int start[766];
+  auto mid = [&](int i) { return (int)(0.5 * (pal[i].w + pal[i + 1].w) + 0.5); };
+  int lo = k >= 2 ? mid(0) : 1;
+  for (int v = 0; v < lo; ++v) start[v] = 0;
+  int hi = k >= 2 ? mid(k - 2) : 1;
+  for (int v = hi; v < 766; ++v) start[v] = k - 1;
+  for (int i = 1; i < k - 1; ++i)
+    for (int v = mid(i - 1); v < mid(i); ++v) start[v] = i;
+
+  for (uint32_t ip = 0; ip < n; ++ip) {
+    uint32_t c[3];
+    unpack(in[ip], c);
+    const int r = c[0], g = c[1], b = c[2], sum = r + g + b;
+    int best = start[sum];
+    auto d2 = [&](int i) {
+      int dr = r - pal[i].r, dg = g - pal[i].g, db = b - pal[i].b;
+      return dr * dr + dg * dg + db * db;
+    };
+    int bestd = d2(best);
+    int up = best, dn = best;
+    bool go_up = true, go_dn = true;
+    while (go_up || go_dn) {
+      if (go_up) {
+        ++up;
+        if (up > k - 1 || ssd[sum - pal[up].w] >= bestd) go_up = false;
+        else { int d = d2(up); if (d < bestd) { bestd = d; best = up; } }
+      }
+      if (go_dn) {
+        --dn;
+        if (dn < 0 || ssd[sum - pal[dn].w] >= bestd) go_dn = false;
+        else { int d = d2(dn); if (d < bestd) { bestd = d; best = dn; } }
+      }
+    }
+    out[ip] = ((uint32_t)pal[best].r << 16) | ((uint32_t)pal[best].g << 8) |
+              (uint32_t)pal[best].b;
+  }
+}
+
+// quant_recurse restated (quant_util.cpp:20-158), UW path only, no stdout
+// timer lines: cluster -> first-seen colortable dedup (:93-118) -> map (:139).
+int dqo_quant_recurse(uint32_t n, const uint32_t* in, uint32_t* out,
+                      uint32_t* k_inout, uint32_t* ct) {
+  int empty = dqo_cluster(n, in, k_inout, ct, 10, nullptr, nullptr, nullptr);
+  if (empty < 0) return empty;
+  std::unordered_set<uint32_t> seen;
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < *k_inout; ++i)
+    if (seen.insert(ct[i]).second) ct[m++] = ct[i];
+  *k_inout = m;
+  dqo_map(in, n, out, ct, (int)m);
+  return empty;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Fixture helpers shared by tests/ and bench.py (test infrastructure too).
+// SURVEY 8c generator: xorshift64 (s^=s<<13; s^=s>>7; s^=s<<17), one draw per
+// pixel in row-major order, pixel = draw & 0xFFFFFF.
+extern "C" void dqo_xorshift_fill(uint32_t* out, uint64_t n, uint64_t seed) {
+  uint64_t s = seed;
+  for (uint64_t i = 0; i < n; ++i) {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    out[i] = (uint32_t)(s & 0xFFFFFF);
+  }
+}
+
+// SURVEY 8c hash: word-wise FNV-1a-64 over uint32 words.
+extern "C" uint64_t dqo_fnv1a64(const uint32_t* w, uint64_t n) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint64_t i = 0; i < n; ++i) {
+    h ^= w[i];
+    h *= 0x100000001b3ull;
+  }
+  return h;
+}

@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures in tests/golden/ from the REFERENCE.
+
+Run here (the container that has /root/reference), never on the GPU box:
+
+    make -C oracle ref && tests/golden/instrument_ref.sh
+    python tests/golden/make_golden.py [--big]
+
+Sources of truth:
+  * oracle/_ref/libdqref.so        -- the unmodified reference DivQuant sources
+                                      (/root/reference/DivQuant/*.cpp) built by
+                                      oracle/Makefile; gives out[] and ct[].
+  * oracle/_ref/libdqref_instr.so  -- scratch copy of the same sources with two
+                                      fprintf lines (instrument_ref.sh); gives the
+                                      split trace and the double centroids (%a).
+
+Input generator: xorshift64 s^=s<<13; s^=s>>7; s^=s<<17, one draw
+per pixel, pixel = draw & 0xFFFFFF, default seed 0x9E3779B97F4A7C15 (the
+oracle's dqo_xorshift_fill).  Hash: word-wise FNV-1a-64 (dqo_fnv1a64).
+NOTE: SURVEY 8c lists hash values for these configs that this generator+hash
+do not reproduce (its harness details are not recoverable); the fixtures below
+are regenerated from the reference itself by this script and are the pin.
+
+Fixture files (all data, no code): kats.json, cases.json/.npz, c1.npz,
+big.json/.npz, png.json/.npz, map.json, weighted.json, png/*.png (the two
+sample images the reference ships in tests/).
+"""
+import argparse
+import ctypes
+import json
+import os
+import shutil
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import dq_fixtures as fx  # noqa: E402  (shared generator/hash helpers)
+
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libdqref.so")
+INSTR_SO = os.path.join(ROOT, "oracle", "_ref", "libdqref_instr.so")
+PNG_SRC = {"batman": "/root/reference/tests/Batman/batman.png",
+           "cookie": "/root/reference/tests/Cookie/cookie.png"}
+
+
+class Ref:
+    """ctypes view of a reference build (C linkage quant_recurse, C++ linkage map)."""
+
+    def __init__(self, path):
+        self.lib = ctypes.CDLL(path)
+        self.lib.quant_recurse.restype = None
+        self.map = getattr(self.lib, "_Z14map_colors_mpsPKjjPjS1_i")
+        self.map.restype = None
+
+    def quant(self, px, k, uniq=1):
+        px = np.ascontiguousarray(px, np.uint32)
+        out = np.zeros(len(px), np.uint32)
+        ct = np.zeros(k, np.uint32)
+        kk = ctypes.c_uint32(k)
+        with Capture() as cap:
+            self.lib.quant_recurse(ctypes.c_uint32(len(px)), fx.vp(px), fx.vp(out),
+                                   ctypes.byref(kk), fx.vp(ct), ctypes.c_int(uniq))
+        return out, ct[:kk.value].copy(), cap.err
+
+    def map_colors(self, px, pal):
+        px = np.ascontiguousarray(px, np.uint32)
+        pal = np.ascontiguousarray(pal, np.uint32)
+        out = np.zeros(len(px), np.uint32)
+        self.map(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(out), fx.vp(pal), ctypes.c_int(len(pal)))
+        return out
+
+
+class Capture:
+    """Redirect fd 1 (timer lines) to /dev/null and fd 2 to a temp file."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        sys.stderr.flush()
+        self.tmp = tempfile.TemporaryFile(mode="w+b")
+        self.o1, self.o2 = os.dup(1), os.dup(2)
+        dn = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(dn, 1)
+        os.close(dn)
+        os.dup2(self.tmp.fileno(), 2)
+        return self
+
+    def __exit__(self, *a):
+        libc = ctypes.CDLL(None)
+        libc.fflush(None)
+        os.dup2(self.o1, 1)
+        os.dup2(self.o2, 2)
+        os.close(self.o1)
+        os.close(self.o2)
+        self.tmp.seek(0)
+        self.err = self.tmp.read().decode()
+        self.tmp.close()
+
+
+def parse_instr(err, k):
+    """DQTRACE/DQMEAN lines -> trace int64[(k-1),4], means float64[k,3] (NaN = empty)."""
+    trace, means = [], np.full((k, 3), np.nan)
+    for line in err.splitlines():
+        f = line.split()
+        if not f:
+            continue
+        if f[0] == "DQTRACE":
+            trace.append([int(v) for v in f[1:5]])
+        elif f[0] == "DQMEAN":
+            means[int(f[1])] = [float.fromhex(v) for v in f[2:5]]
+    return np.array(trace, np.int64).reshape(-1, 4), means
+
+
+def full_run(ref, instr, px, k, uniq=1):
+    out, ct, _ = ref.quant(px, k, uniq)
+    out2, ct2, err = instr.quant(px, k, uniq)
+    assert np.array_equal(out, out2) and np.array_equal(ct, ct2), "instrumented build diverged"
+    trace, means = parse_instr(err, k)
+    return out, ct, trace, means
+
+
+def rec(out, ct, trace=None):
+    d = {"out_fnv": "%016x" % fx.fnv(out), "ct": [int(v) for v in ct], "k_out": int(len(ct))}
+    if trace is not None and len(trace):
+        d["sum_split_sizes"] = int(trace[:, 2].sum())
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--big", action="store_true", help="also the 4K / 4096^2 configs (minutes)")
+    ap.add_argument("--only", default="", help="comma list of sections")
+    a = ap.parse_args()
+    only = set(a.only.split(",")) if a.only else None
+    ref, instr = Ref(REF_SO), Ref(INSTR_SO)
+
+    def want(s):
+        return only is None or s in only
+
+    # ---- 1. Test/DivQuantTest.m known-answer tests (inputs restated in dq_fixtures)
+    if want("kats"):
+        kats = {}
+        for name, (px, k) in fx.kat_inputs().items():
+            out, ct, trace, means = full_run(ref, instr, px, k)
+            kats[name] = dict(rec(out, ct, trace), out=[int(v) for v in out],
+                              trace=trace.tolist(), means=[[float(x).hex() for x in m] for m in means])
+        fx.dump_json("kats.json", kats)
+
+    # ---- 2. small synthetic cases (inputs regenerated from their spec)
+    if want("cases"):
+        cases = []
+        arrs = {}
+        for i, spec in enumerate(fx.small_case_specs()):
+            px = fx.make_case(spec)
+            out, ct, trace, means = full_run(ref, instr, px, spec["k"])
+            r = dict(spec=spec, **rec(out, ct, trace))
+            cases.append(r)
+            arrs["trace_%d" % i] = trace
+            arrs["means_%d" % i] = means
+        fx.dump_json("cases.json", cases)
+        np.savez_compressed(os.path.join(HERE, "cases.npz"), **arrs)
+
+    # ---- 3. C1: 256x256 K=16 full label map (u8 index into ct) + centroids
+    if want("c1"):
+        px = fx.xorshift(256 * 256)
+        out, ct, trace, means = full_run(ref, instr, px, 16)
+        lab = fx.labels_of(out, ct).astype(np.uint8)
+        np.savez_compressed(os.path.join(HERE, "c1.npz"), labels=lab, ct=ct, trace=trace, means=means)
+
+    # ---- 4. bigger synthetic configs: hashes + colortables + traces + centroids
+    if want("big"):
+        cfgs = [(512, 512, 64), (1920, 1080, 256), (1920, 1080, 1024)]
+        if a.big:
+            cfgs += [(3840, 2160, 256), (4096, 4096, 1024)]
+        path = os.path.join(HERE, "big.json")
+        big = json.load(open(path)) if os.path.exists(path) else {}
+        arrs = dict(np.load(os.path.join(HERE, "big.npz"))) if os.path.exists(os.path.join(HERE, "big.npz")) else {}
+        for (w, h, k) in cfgs:
+            key = "%dx%d_k%d" % (w, h, k)
+            px = fx.xorshift(w * h)
+            out, ct, trace, means = full_run(ref, instr, px, k)
+            big[key] = dict(w=w, h=h, k=k, **rec(out, ct, trace))
+            arrs["trace_" + key] = trace.astype(np.int32)
+            arrs["means_" + key] = means
+            print("big", key, big[key]["out_fnv"], flush=True)
+        fx.dump_json("big.json", big)
+        np.savez_compressed(os.path.join(HERE, "big.npz"), **arrs)
+
+    # ---- 5. the reference's two sample images (tests/*/...png), UW and weighted
+    if want("png"):
+        os.makedirs(os.path.join(HERE, "png"), exist_ok=True)
+        png, arrs = {}, {}
+        for name, src in PNG_SRC.items():
+            dst = os.path.join(HERE, "png", name + ".png")
+            shutil.copyfile(src, dst)
+            px, w, h = fx.load_png_u32(dst)
+            png[name] = {"w": w, "h": h, "px_fnv": "%016x" % fx.fnv(px),
+                         "unique": int(len(np.unique(px)))}
+            for k in (4, 16, 125, 256):
+                out, ct, trace, means = full_run(ref, instr, px, k, 1)
+                png[name]["k%d" % k] = rec(out, ct, trace)
+                arrs["trace_%s_k%d" % (name, k)] = trace.astype(np.int32)
+                arrs["means_%s_k%d" % (name, k)] = means
+                out0, ct0, _ = ref.quant(px, k, 0)
+                png[name]["k%d_weighted" % k] = rec(out0, ct0)
+                print("png", name, k, flush=True)
+        fx.dump_json("png.json", png)
+        np.savez_compressed(os.path.join(HERE, "png.npz"), **arrs)
+
+    # ---- 6. map_colors_mps alone on random / tie-heavy / subdivided palettes
+    if want("map"):
+        px = fx.xorshift(1 << 16, seed=fx.SEED + 7)
+        res = []
+        for spec in fx.map_palette_specs():
+            pal = fx.make_palette(spec)
+            out = ref.map_colors(px, pal)
+            res.append({"spec": spec, "out_fnv": "%016x" % fx.fnv(out),
+                        "first": [int(v) for v in out[:64]]})
+        fx.dump_json("map.json", res)
+
+    # ---- 7. weighted path (allPixelsUnique=0) on synthetic inputs
+    if want("weighted"):
+        wres = []
+        for spec in fx.small_case_specs()[:12]:
+            px = fx.make_case(spec)
+            out, ct, _ = ref.quant(px, spec["k"], 0)
+            wres.append(dict(spec=spec, **rec(out, ct)))
+        for (w, h, k) in [(512, 512, 64), (1920, 1080, 256)]:
+            px = fx.xorshift(w * h)
+            out, ct, _ = ref.quant(px, k, 0)
+            wres.append(dict(spec={"w": w, "h": h, "k": k, "kind": "xorshift"}, **rec(out, ct)))
+        fx.dump_json("weighted.json", wres)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,201 @@
+"""GPU parity tests: the HIP path (through the C ABI of libdivquant_hip.so)
+against the reference's own outputs (tests/golden/, generated from the
+unmodified reference by tests/golden/make_golden.py) and against the CPU
+oracle on seeded inputs.
+
+Bar (BASELINE.json north star): output colours (the label map) and the
+colortable bit-exact; the double centroids mean[ic] within 1e-5 -- they are
+in fact asserted bit-exact here.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import dq_fixtures as fx
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_cluster(px, k, max_iters=10):
+    orc = fx.oracle()
+    ct = np.zeros(k, np.uint32)
+    kk = ctypes.c_uint32(k)
+    means = np.zeros((k, 3), np.float64)
+    sizes = np.zeros(k, np.int64)
+    trace = np.zeros((max(k - 1, 1), 4), np.int64)
+    orc.dqo_cluster(ctypes.c_uint32(len(px)), fx.vp(px), ctypes.byref(kk), fx.vp(ct),
+                    ctypes.c_int(max_iters), fx.vp(means), fx.vp(sizes), fx.vp(trace))
+    return ct[:kk.value], means, sizes, trace[:k - 1]
+
+
+def _quant_dev(gpu, px, k):
+    import torch
+    t_in = torch.from_numpy(np.ascontiguousarray(px, np.uint32).view(np.int32)).to("cuda:0")
+    t_out = torch.empty_like(t_in)
+    ct, empty = gpu.quant_device(t_in, t_out, k)
+    torch.cuda.synchronize()
+    return t_out.cpu().numpy().view(np.uint32), ct
+
+
+def _check_centroids(gpu, k, ref_means):
+    """Reference mean[ic] is recorded only for non-empty clusters (NaN elsewhere)."""
+    means, sizes = gpu.last_centroids(k)
+    filled = ~np.isnan(ref_means[:, 0])
+    assert np.array_equal(filled, sizes > 0)
+    assert np.array_equal(means[filled].view(np.uint64), ref_means[filled].view(np.uint64)), \
+        np.abs(means[filled] - ref_means[filled]).max()
+    assert np.all(np.abs(means[filled] - ref_means[filled]) <= 1e-5)
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", sorted(fx.KAT_EXPECTED))
+def test_kat_quant_recurse(gpu, name):
+    """Test/DivQuantTest.m known answers through the reference-named C entry."""
+    px, k = fx.kat_inputs()[name]
+    out, ct = gpu.quant_recurse(px, k, 1)
+    assert [int(v) for v in ct] == fx.KAT_EXPECTED[name]
+    fix = fx.load_json("kats.json")[name]
+    assert [int(v) for v in out] == fix["out"]
+
+
+@pytest.mark.parametrize("name", sorted(fx.KAT_EXPECTED))
+def test_kat_trace_and_centroids(gpu, name):
+    px, k = fx.kat_inputs()[name]
+    out, ct = _quant_dev(gpu, px, k)
+    fix = fx.load_json("kats.json")[name]
+    assert [int(v) for v in ct] == fix["ct"]
+    if k > 1:
+        assert gpu.last_trace(k).tolist() == fix["trace"]
+        ref_means = np.array([[float.fromhex(v) for v in m] for m in fix["means"]])
+        _check_centroids(gpu, k, ref_means)
+
+
+def test_cases(gpu):
+    """Small seeded inputs: uniform, tie-heavy, grey, clustered, coarse, top-byte garbage;
+    N from 1 to 70001, K from 1 to 1024 (K > N gives empty clusters)."""
+    cases = fx.load_json("cases.json")
+    arrs = fx.load_npz("cases.npz")
+    bad = []
+    for i, c in enumerate(cases):
+        spec = c["spec"]
+        px = fx.make_case(spec)
+        out, ct = _quant_dev(gpu, px, spec["k"])
+        if "%016x" % fx.fnv(out) != c["out_fnv"] or [int(v) for v in ct] != c["ct"]:
+            bad.append((i, spec))
+            continue
+        if spec["k"] > 1:
+            tr = gpu.last_trace(spec["k"])
+            if not np.array_equal(tr, arrs["trace_%d" % i]):
+                bad.append((i, spec, "trace"))
+            _check_centroids(gpu, spec["k"], arrs["means_%d" % i])
+    assert not bad, bad
+
+
+def test_c1_full_label_map(gpu):
+    """C1 256x256 K=16: the whole label map against the reference's."""
+    z = fx.load_npz("c1.npz")
+    px = fx.xorshift(256 * 256)
+    out, ct = _quant_dev(gpu, px, 16)
+    assert np.array_equal(ct, z["ct"])
+    assert np.array_equal(z["ct"][z["labels"]], out)
+    assert np.array_equal(gpu.last_trace(16), z["trace"])
+    _check_centroids(gpu, 16, z["means"])
+
+
+@pytest.mark.parametrize("key", ["512x512_k64", "1920x1080_k256", "1920x1080_k1024",
+                                 "3840x2160_k256", "4096x4096_k1024"])
+def test_big_configs(gpu, key):
+    big = fx.load_json("big.json")
+    if key not in big:
+        pytest.skip("fixture not generated")
+    c = big[key]
+    arrs = fx.load_npz("big.npz")
+    px = fx.xorshift(c["w"] * c["h"])
+    out, ct = _quant_dev(gpu, px, c["k"])
+    assert [int(v) for v in ct] == c["ct"]
+    assert "%016x" % fx.fnv(out) == c["out_fnv"]
+    assert np.array_equal(gpu.last_trace(c["k"]), arrs["trace_" + key])
+    _check_centroids(gpu, c["k"], arrs["means_" + key])
+
+
+@pytest.mark.parametrize("name", ["batman", "cookie"])
+@pytest.mark.parametrize("k", [4, 16, 125, 256])
+def test_sample_images(gpu, name, k):
+    """The reference's own sample images (tests/*/...png), both allPixelsUnique values."""
+    fix = fx.load_json("png.json")[name]
+    px, w, h = fx.load_png_u32(fx.os.path.join(fx.GOLDEN, "png", name + ".png"))
+    assert "%016x" % fx.fnv(px) == fix["px_fnv"]
+    for uniq, key in ((1, "k%d" % k), (0, "k%d_weighted" % k)):
+        out, ct = gpu.quant_recurse(px, k, uniq)
+        assert [int(v) for v in ct] == fix[key]["ct"], key
+        assert "%016x" % fx.fnv(out) == fix[key]["out_fnv"], key
+    arrs = fx.load_npz("png.npz")
+    _quant_dev(gpu, px, k)
+    assert np.array_equal(gpu.last_trace(k), arrs["trace_%s_k%d" % (name, k)])
+    _check_centroids(gpu, k, arrs["means_%s_k%d" % (name, k)])
+
+
+def test_map_colors_mps(gpu):
+    """map_colors_mps alone: random, equal-sum (sort-tie), duplicate, grey and the
+    125-colour getSubdividedColors palettes."""
+    px = fx.xorshift(1 << 16, seed=fx.SEED + 7)
+    bad = []
+    for c in fx.load_json("map.json"):
+        pal = fx.make_palette(c["spec"])
+        out = gpu.map_colors_mps(px, pal)
+        if "%016x" % fx.fnv(out) != c["out_fnv"]:
+            bad.append(c["spec"])
+    assert not bad, bad
+
+
+def test_weighted_path(gpu):
+    """allPixelsUnique=0 (the live app call site, ClusteringSegmentation.cpp:1803)."""
+    bad = []
+    for c in fx.load_json("weighted.json"):
+        s = c["spec"]
+        px = fx.xorshift(s["w"] * s["h"]) if s.get("kind") == "xorshift" else fx.make_case(s)
+        out, ct = gpu.quant_recurse(px, s["k"], 0)
+        if [int(v) for v in ct] != c["ct"] or "%016x" % fx.fnv(out) != c["out_fnv"]:
+            bad.append(s)
+    assert not bad, bad
+
+
+def test_oracle_random_sweep(gpu):
+    """Fresh seeded inputs (not in any fixture) against the CPU oracle."""
+    rng = np.random.default_rng(12345)
+    for trial in range(24):
+        n = int(rng.integers(1, 300000))
+        k = int(rng.choice([2, 3, 8, 16, 64, 100, 256, 512, 1024]))
+        mode = trial % 3
+        if mode == 0:
+            px = rng.integers(0, 1 << 24, n, dtype=np.uint32)
+        elif mode == 1:
+            px = (rng.integers(0, 6, n, dtype=np.uint32) * 0x2A2A2A) ^ rng.integers(0, 4, n, dtype=np.uint32)
+        else:
+            px = rng.integers(0, 1 << 24, n, dtype=np.uint32) & 0xF0C0F0
+        out, ct = _quant_dev(gpu, px, k)
+        ref_ct, ref_means, ref_sizes, ref_trace = _oracle_cluster(px, k)
+        orc_out = np.zeros(n, np.uint32)
+        kk = ctypes.c_uint32(k)
+        ct2 = np.zeros(k, np.uint32)
+        fx.oracle().dqo_quant_recurse(ctypes.c_uint32(n), fx.vp(px), fx.vp(orc_out), ctypes.byref(kk), fx.vp(ct2))
+        assert np.array_equal(ct, ct2[:kk.value]), (trial, n, k)
+        assert np.array_equal(out, orc_out), (trial, n, k)
+        assert np.array_equal(gpu.last_trace(k), ref_trace), (trial, n, k)
+
+
+def test_host_and_device_entry_points_agree(gpu):
+    px = fx.xorshift(200003, seed=99)
+    a_out, a_ct = gpu.quant_recurse(px, 128, 1)
+    b_out, b_ct = _quant_dev(gpu, px, 128)
+    assert np.array_equal(a_ct, b_ct) and np.array_equal(a_out, b_out)
+    c_out = gpu.map_colors_mps(px, a_ct)
+    assert np.array_equal(c_out, a_out)
+
+
+def test_repeatable(gpu):
+    px = fx.xorshift(1 << 20, seed=5)
+    r = [_quant_dev(gpu, px, 256) for _ in range(3)]
+    for out, ct in r[1:]:
+        assert np.array_equal(out, r[0][0]) and np.array_equal(ct, r[0][1])
