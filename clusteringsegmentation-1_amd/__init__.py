@@ -39,6 +39,14 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP/HSA runtime per process: when PyTorch is present, import it first
+    # so the library binds (by soname) to the libamdhip64 torch already mapped
+    # instead of mapping /opt/rocm's copy beside it -- two runtimes in one
+    # process cannot both open the GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise DivQuantError("libdivquant_hip.so is not built (run __graft_entry__.build() "
                             "or make -C clusteringsegmentation-1_amd)")
