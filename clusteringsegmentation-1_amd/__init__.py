@@ -59,6 +59,8 @@ def lib():
         "dq_hip_quant": ([vp, c.c_uint32, vp, u32p, vp, c.c_int, c.c_int], c.c_int),
         "dq_hip_map": ([vp, c.c_uint32, vp, vp, c.c_int], c.c_int),
         "dq_hip_quant_dev": ([c.c_int, vp, c.c_uint32, vp, u32p, vp, c.c_int, vp], c.c_int),
+        "dq_hip_quant_batch_dev": ([c.c_int, c.c_int, vp, vp, vp, c.c_uint32, vp, vp, c.c_int, vp],
+                                   c.c_int),
         "dq_hip_cluster_dev": ([c.c_int, vp, c.c_uint32, u32p, vp, c.c_int, vp], c.c_int),
         "dq_hip_map_dev": ([c.c_int, vp, c.c_uint32, vp, vp, c.c_int, vp], c.c_int),
         "dq_hip_last_centroids": ([c.c_int, vp, vp, c.c_int], c.c_int),
@@ -160,6 +162,24 @@ def quant_device(t_in, t_out, num_clusters, max_iters=10, device=0, n=None, stre
     if r < 0:
         raise DivQuantError("dq_hip_quant_dev: bad arguments")
     return ct[:k.value].copy(), r
+
+
+def quant_batch_device(t_ins, t_outs, num_clusters, max_iters=10, device=0, stream=None):
+    """quant_recurse over a batch of device-resident frames in one call (every
+    pass of every split round is one launch over all frames).
+    Returns ([colortable per frame], total_empty)."""
+    nf = len(t_ins)
+    ins = (ctypes.c_void_p * nf)(*[_dptr(t).value for t in t_ins])
+    outs = (ctypes.c_void_p * nf)(*[_dptr(t).value for t in t_outs])
+    ns = np.array([t.numel() for t in t_ins], np.uint32)
+    ct = np.zeros((nf, num_clusters), np.uint32)
+    kout = np.zeros(nf, np.uint32)
+    r = lib().dq_hip_quant_batch_dev(device, nf, ctypes.cast(ins, ctypes.c_void_p),
+                                     _ptr(ns), ctypes.cast(outs, ctypes.c_void_p), num_clusters,
+                                     _ptr(ct), _ptr(kout), max_iters, _stream_ptr(stream))
+    if r < 0:
+        raise DivQuantError("dq_hip_quant_batch_dev: bad arguments")
+    return [ct[i, :kout[i]].copy() for i in range(nf)], r
 
 
 def cluster_device(t_in, num_clusters, max_iters=10, device=0, n=None, stream=None):

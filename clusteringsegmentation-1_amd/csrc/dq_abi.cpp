@@ -81,10 +81,14 @@ int dq_hip_cluster_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* k
   if (!d_in || !k || !ct || n == 0 || *k == 0 || max_iters < 1) return -1;
   Engine& e = engine_for(device);
   std::lock_guard<std::mutex> g(e.mutex());
-  int empty = 0;
-  const int out = e.cluster(d_in, n, (int)*k, max_iters, ct, &empty, (hipStream_t)stream);
-  *k = (uint32_t)out;
-  return empty;
+  dq::FrameJob j;
+  j.d_in = d_in;
+  j.n = n;
+  j.k = (int)*k;
+  j.ct = ct;
+  e.run(&j, 1, max_iters, false, (hipStream_t)stream);
+  *k = (uint32_t)j.k_out;
+  return j.num_empty;
 }
 
 int dq_hip_map_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out,
@@ -97,17 +101,39 @@ int dq_hip_map_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out
   return 0;
 }
 
+int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
+                           const uint32_t* n, uint32_t* const* d_out, uint32_t k,
+                           uint32_t* ct, uint32_t* k_out, int max_iters, void* stream) {
+  if (nframes <= 0 || !d_in || !n || !d_out || !ct || !k_out || k == 0 || max_iters < 1)
+    return -1;
+  for (int i = 0; i < nframes; ++i)
+    if (!d_in[i] || !d_out[i] || n[i] == 0) return -1;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  std::vector<dq::FrameJob> jobs(nframes);
+  for (int i = 0; i < nframes; ++i) {
+    jobs[i].d_in = d_in[i];
+    jobs[i].n = n[i];
+    jobs[i].d_out = d_out[i];
+    jobs[i].k = (int)k;
+    jobs[i].ct = ct + (size_t)i * k;
+  }
+  e.run(jobs.data(), nframes, max_iters, true, (hipStream_t)stream);
+  int empty = 0;
+  for (int i = 0; i < nframes; ++i) {
+    k_out[i] = (uint32_t)jobs[i].k_out;
+    empty += jobs[i].num_empty;
+  }
+  return empty;
+}
+
 int dq_hip_quant_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out,
                      uint32_t* k, uint32_t* ct, int max_iters, void* stream) {
   if (!d_in || !d_out || !k || !ct || n == 0 || *k == 0 || max_iters < 1) return -1;
-  Engine& e = engine_for(device);
-  std::lock_guard<std::mutex> g(e.mutex());
-  int empty = 0;
-  uint32_t kk = (uint32_t)e.cluster(d_in, n, (int)*k, max_iters, ct, &empty, (hipStream_t)stream);
-  kk = dedup_colortable(ct, kk);
-  e.map(d_in, n, d_out, ct, (int)kk, (hipStream_t)stream);
-  *k = kk;
-  return empty;
+  uint32_t kk = 0;
+  const int r = dq_hip_quant_batch_dev(device, 1, &d_in, &n, &d_out, *k, ct, &kk, max_iters, stream);
+  if (r >= 0) *k = kk;
+  return r;
 }
 
 int dq_hip_quant(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* k,
@@ -119,14 +145,17 @@ int dq_hip_quant(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* k,
   std::lock_guard<std::mutex> g(e.mutex());
   hipStream_t st = e.stream();
   e.stage_in(in, n, st);
-  int empty = 0;
-  uint32_t kk = (uint32_t)e.cluster(e.staged_in(), n, (int)*k, 10, ct, &empty, st);
-  kk = dedup_colortable(ct, kk);
-  e.map(e.staged_in(), n, e.staged_out(), ct, (int)kk, st);
+  dq::FrameJob j;
+  j.d_in = e.staged_in();
+  j.n = n;
+  j.d_out = e.staged_out();
+  j.k = (int)*k;
+  j.ct = ct;
+  e.run(&j, 1, 10, true, st);
   DQ_HIP(hipMemcpyAsync(out, e.staged_out(), (size_t)n * 4, hipMemcpyDeviceToHost, st));
   DQ_HIP(hipStreamSynchronize(st));
-  *k = kk;
-  return empty;
+  *k = (uint32_t)j.k_out;
+  return j.num_empty;
 }
 
 int dq_hip_map(const uint32_t* in, uint32_t n, uint32_t* out, const uint32_t* ct, int k) {
@@ -198,10 +227,14 @@ void quant_recurse(uint32_t numPixels, const uint32_t* inPixelsPtr, uint32_t* ou
   hipStream_t st = e.stream();
   const double t0 = now_ms();
   e.stage_in(inPixelsPtr, numPixels, st);
-  int empty = 0;
-  uint32_t k = (uint32_t)e.cluster(e.staged_in(), numPixels, (int)*numClustersPtr, 10,
-                                   outColortablePtr, &empty, st);
-  report_empty(empty);
+  dq::FrameJob j;
+  j.d_in = e.staged_in();
+  j.n = numPixels;
+  j.k = (int)*numClustersPtr;
+  j.ct = outColortablePtr;
+  e.run(&j, 1, 10, false, st);
+  report_empty(j.num_empty);
+  uint32_t k = (uint32_t)j.k_out;
   *numClustersPtr = k;
   const double t1 = now_ms();
   if (!quiet()) {
@@ -251,10 +284,14 @@ void quant_varpart_fast(const uint32_t numPixels, const uint32_t* inPixels, uint
   std::lock_guard<std::mutex> g(e.mutex());
   hipStream_t st = e.stream();
   e.stage_in(inPixels, numPixels, st);
-  int empty = 0;
-  const int k = e.cluster(e.staged_in(), numPixels, (int)*numClustersPtr, max_iters,
-                          colortablePtr, &empty, st);
-  report_empty(empty);
+  dq::FrameJob j;
+  j.d_in = e.staged_in();
+  j.n = numPixels;
+  j.k = (int)*numClustersPtr;
+  j.ct = colortablePtr;
+  e.run(&j, 1, max_iters, false, st);
+  report_empty(j.num_empty);
+  const int k = j.k_out;
   *numClustersPtr = (uint32_t)k;
 }
 

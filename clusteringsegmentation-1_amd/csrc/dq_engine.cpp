@@ -8,8 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
-#include <memory>
-#include <queue>
+#include <unordered_set>
 
 namespace dq {
 
@@ -22,35 +21,17 @@ void die(const char* what, const char* file, int line, const char* detail) {
 
 namespace {
 
-template <typename T>
-void dev_grow(T** p, size_t* cap, size_t want) {
-  if (want <= *cap && *p) return;
-  if (*p) DQ_HIP(hipFree(*p));
-  size_t n = std::max<size_t>(want, 1);
-  DQ_HIP(hipMalloc((void**)p, n * sizeof(T)));
-  *cap = n;
-}
+constexpr int BUF_IN = 0, BUF_P0 = 1, BUF_P1 = 2;
+inline int child_buf(int b) { return b == BUF_P0 ? BUF_P1 : BUF_P0; }
+inline size_t align4(size_t x) { return (x + 3) & ~(size_t)3; }
 
-template <typename T>
-void host_grow(T** p, size_t want_old_cap, size_t want) {
-  (void)want_old_cap;
-  if (*p) DQ_HIP(hipHostFree(*p));
-  DQ_HIP(hipHostMalloc((void**)p, std::max<size_t>(want, 1) * sizeof(T), hipHostMallocDefault));
+// Split-pass threshold (:473): cut_pos < v <=> v >= thr for integer v.
+int32_t split_threshold(double cut) {
+  if (!(cut == cut)) return 256;
+  if (cut < 0.0) return 0;
+  if (cut >= 255.0) return 256;
+  return (int32_t)std::floor(cut) + 1;
 }
-
-// Greedy order of the reference's STEP 4 (:876-887): the largest TSE wins,
-// the lowest cluster index among equal TSEs (first strict '<' in index order).
-struct Cand {
-  double tse;
-  int idx;
-  int node;
-};
-struct CandLess {
-  bool operator()(const Cand& a, const Cand& b) const {
-    if (a.tse != b.tse) return a.tse < b.tse;   // max-heap on tse
-    return a.idx > b.idx;                       // then lowest index first
-  }
-};
 
 }  // namespace
 
@@ -59,7 +40,7 @@ Engine::Engine(int device) : device_(device) {
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   DQ_HIP(hipMalloc((void**)&d_pal_, 16384 * sizeof(uint32_t)));
   DQ_HIP(hipMalloc((void**)&d_lut_, 768 * sizeof(uint16_t)));
-  DQ_HIP(hipMalloc((void**)&d_cell_cnt_, kCells * sizeof(uint16_t)));
+  DQ_HIP(hipMalloc((void**)&d_cell_rec_, kCells * sizeof(uint4)));
   DQ_HIP(hipMalloc((void**)&d_cell_idx_, (size_t)kCells * kCellCap * sizeof(uint16_t)));
   DQ_HIP(hipHostMalloc((void**)&h_pal_, 16384 * sizeof(uint32_t), hipHostMallocDefault));
   DQ_HIP(hipHostMalloc((void**)&h_lut_, 768 * sizeof(uint16_t), hipHostMallocDefault));
@@ -70,6 +51,8 @@ Engine::~Engine() {
   // so release nothing here (the driver reclaims device memory).
 }
 
+// ---------------------------------------------------------------------------
+// timing
 hipEvent_t Engine::take_event() {
   if (!event_pool_.empty()) {
     hipEvent_t e = event_pool_.back();
@@ -83,11 +66,7 @@ hipEvent_t Engine::take_event() {
 
 void Engine::timed_begin(hipStream_t stream) {
   if (!timing_) return;
-  PendingEvent pe;
-  pe.a = take_event();
-  pe.b = nullptr;
-  pe.kind = -1;
-  pe.bytes = 0;
+  PendingEvent pe{take_event(), nullptr, -1, 0.0};
   DQ_HIP(hipEventRecord(pe.a, stream));
   pending_.push_back(pe);
 }
@@ -120,20 +99,20 @@ void Engine::reset_stats() {
   for (auto& s : stats) s = KernelStat();
 }
 
-void Engine::ensure_pixels(uint32_t n) {
-  // +kSweep slack: a tile's clamped loads never leave the allocation.
-  const size_t want = (size_t)n + 64;
-  if (want > cap_px_ || !d_p0_) {
+// ---------------------------------------------------------------------------
+// buffers
+void Engine::ensure_pixels(size_t total) {
+  if (total > cap_px_ || !d_p0_) {
     if (d_p0_) DQ_HIP(hipFree(d_p0_));
     if (d_p1_) DQ_HIP(hipFree(d_p1_));
-    DQ_HIP(hipMalloc((void**)&d_p0_, want * sizeof(uint32_t)));
-    DQ_HIP(hipMalloc((void**)&d_p1_, want * sizeof(uint32_t)));
-    cap_px_ = want;
+    DQ_HIP(hipMalloc((void**)&d_p0_, total * sizeof(uint32_t)));
+    DQ_HIP(hipMalloc((void**)&d_p1_, total * sizeof(uint32_t)));
+    cap_px_ = total;
   }
 }
 
 void Engine::stage_in(const uint32_t* h_in, uint32_t n, hipStream_t stream) {
-  const size_t want = (size_t)n + 64;
+  const size_t want = align4((size_t)n) + 4;
   if (want > cap_stage_ || !d_stage_in_) {
     if (d_stage_in_) DQ_HIP(hipFree(d_stage_in_));
     if (d_stage_out_) DQ_HIP(hipFree(d_stage_out_));
@@ -145,9 +124,9 @@ void Engine::stage_in(const uint32_t* h_in, uint32_t n, hipStream_t stream) {
                         hipMemcpyHostToDevice, stream));
 }
 
-void Engine::ensure_round(size_t nnodes, size_t ntiles) {
+void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nshards) {
   if (nnodes > cap_nodes_ || !d_nodes_) {
-    size_t c = std::max<size_t>(nnodes, 64);
+    size_t c = std::max<size_t>(nnodes, 256);
     if (d_nodes_) DQ_HIP(hipFree(d_nodes_));
     if (h_nodes_) DQ_HIP(hipHostFree(h_nodes_));
     DQ_HIP(hipMalloc((void**)&d_nodes_, c * sizeof(DevNode)));
@@ -155,71 +134,102 @@ void Engine::ensure_round(size_t nnodes, size_t ntiles) {
     cap_nodes_ = c;
   }
   if (ntiles > cap_tiles_ || !d_tiles_) {
-    size_t c = std::max<size_t>(ntiles, 1024);
+    size_t c = std::max<size_t>(ntiles, 4096);
     if (d_tiles_) DQ_HIP(hipFree(d_tiles_));
-    if (d_parts_) DQ_HIP(hipFree(d_parts_));
+    if (d_tile_cnt_) DQ_HIP(hipFree(d_tile_cnt_));
     if (h_tiles_) DQ_HIP(hipHostFree(h_tiles_));
     DQ_HIP(hipMalloc((void**)&d_tiles_, c * sizeof(Tile)));
-    DQ_HIP(hipMalloc((void**)&d_parts_, c * sizeof(TilePartial)));
+    DQ_HIP(hipMalloc((void**)&d_tile_cnt_, c * sizeof(uint32_t)));
     DQ_HIP(hipHostMalloc((void**)&h_tiles_, c * sizeof(Tile), hipHostMallocDefault));
     cap_tiles_ = c;
   }
+  if (nshards > cap_shards_ || !d_acc_) {
+    size_t c = std::max<size_t>(nshards, 4096);
+    if (d_acc_) DQ_HIP(hipFree(d_acc_));
+    DQ_HIP(hipMalloc((void**)&d_acc_, (size_t)kAccSets * c * kAccStride * sizeof(uint64_t)));
+    cap_shards_ = c;
+  }
 }
 
+const uint32_t* Engine::buf_ptr(int buf, const FrameState& f) const {
+  if (buf == BUF_IN) return f.in;
+  return (buf == BUF_P0 ? d_p0_ : d_p1_) + f.base;
+}
+
+// ---------------------------------------------------------------------------
 // One round: split every node in `active` (one launch per pass for all).
-void Engine::run_round(const std::vector<int>& active, bool root_round,
-                       int max_iters, double s, hipStream_t stream) {
+void Engine::run_round(const std::vector<int>& active, bool root_round, int max_iters,
+                       hipStream_t stream) {
   const int nn = (int)active.size();
   uint64_t total = 0;
   for (int id : active) total += nodes_[id].len;
-  // Tile length: 4096-point steps, ~2048 tiles per round for big rounds.
+  // Tile length: whole 4096-point sweeps, ~2048 tiles for big rounds.
   uint64_t tl = (total + 2047) / 2048;
   tl = ((tl + kSweep - 1) / kSweep) * kSweep;
   tl = std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, kMaxTilePx));
-  size_t ntiles = 0;
-  for (int id : active) ntiles += (nodes_[id].len + tl - 1) / tl;
-  ensure_round(nn, ntiles);
+  size_t ntiles = 0, nshards = 0;
+  for (int id : active) {
+    const size_t t = std::max<size_t>(1, (nodes_[id].len + tl - 1) / tl);   // empty nodes get one empty tile
+    ntiles += t;
+    nshards += std::max<size_t>(1, std::min<size_t>(t, kMaxShards));
+  }
+  ensure_round(nn, ntiles, nshards);
 
-  int t = 0;
+  int t = 0, sh = 0;
   for (int a = 0; a < nn; ++a) {
     const Node& n = nodes_[active[a]];
+    const FrameState& fs = frames_[n.frame];
     DevNode& d = h_nodes_[a];
     std::memset(&d, 0, sizeof(d));
+    d.src = buf_ptr(n.buf, fs);
+    d.dst = (child_buf(n.buf) == BUF_P0 ? d_p0_ : d_p1_) + fs.base;
     d.off = n.off;
     d.len = n.len;
-    d.buf = n.buf;
+    d.root = root_round ? 1 : 0;
+    d.s = fs.s;
     d.tw = n.w;
     for (int c = 0; c < 3; ++c) { d.tm[c] = n.mean[c]; d.tv[c] = n.var[c]; }
     // Cut axis/position (:388-403): comparisons and copies only.
-    double maxv = n.var[0];
+    double maxv = n.var[0], cut = n.mean[0];
     d.axis = 0;
-    d.cut = n.mean[0];
-    if (maxv < n.var[1]) { maxv = n.var[1]; d.axis = 1; d.cut = n.mean[1]; }
-    if (maxv < n.var[2]) { d.axis = 2; d.cut = n.mean[2]; }
+    if (maxv < n.var[1]) { maxv = n.var[1]; d.axis = 1; cut = n.mean[1]; }
+    if (maxv < n.var[2]) { d.axis = 2; cut = n.mean[2]; }
+    d.thr = split_threshold(cut);
     d.tile_begin = t;
-    for (uint64_t o = 0; o < n.len; o += tl) {
+    uint32_t local = 0;
+    for (uint64_t o = 0; o == 0 || o < n.len; o += tl) {
       Tile& tt = h_tiles_[t++];
       tt.node = a;
       tt.start = n.off + (uint32_t)o;
       tt.end = n.off + (uint32_t)std::min<uint64_t>(n.len, o + tl);
-      tt.old_base = 0;
+      tt.local = local++;
     }
     d.tile_end = t;
+    d.shard_base = sh;
+    d.nshard = (int32_t)std::max<uint32_t>(1, std::min<uint32_t>(local, kMaxShards));
+    sh += d.nshard;
   }
   DQ_HIP(hipMemcpyAsync(d_nodes_, h_nodes_, nn * sizeof(DevNode), hipMemcpyHostToDevice, stream));
   DQ_HIP(hipMemcpyAsync(d_tiles_, h_tiles_, ntiles * sizeof(Tile), hipMemcpyHostToDevice, stream));
+  // All sets start at zero; from then on every pass zeroes the set of the
+  // pass after it (whose previous contents were read two passes ago).
+  DQ_HIP(hipMemsetAsync(d_acc_, 0, (size_t)kAccSets * sh * kAccStride * sizeof(uint64_t), stream));
 
-  PixelBufs bufs{staged_root_, d_p0_, d_p1_};
+  RoundArgs ra;
+  ra.tiles = d_tiles_;
+  ra.nodes = d_nodes_;
+  ra.acc = d_acc_;
+  ra.tile_cnt = d_tile_cnt_;
+  ra.total_shards = sh;
+  ra.pass = 0;
   const double bytes = 4.0 * (double)total;
   const int nt = (int)ntiles;
   auto pass = [&](int kind, int st) {
     timed_begin(stream);
-    launch_pass(kind, d_tiles_, nt, d_nodes_, bufs, d_parts_, stream);
+    launch_pass(kind, ra, nt, stream);
     timed_end(st, bytes, stream);
-    timed_begin(stream);
-    launch_epilogue(kind, d_nodes_, nn, d_tiles_, d_parts_, s, stream);
-    timed_end(ST_EPILOGUE, 0.0, stream);
     last_points_swept += total;
+    ra.pass++;
   };
   if (root_round) pass(PASS_INIT, ST_INIT);
   pass(PASS_SPLIT, ST_SPLIT);
@@ -228,7 +238,7 @@ void Engine::run_round(const std::vector<int>& active, bool root_round,
     pass(last ? PASS_KLAST : PASS_KMEANS, last ? ST_KLAST : ST_KMEANS);
   }
   timed_begin(stream);
-  launch_partition(d_tiles_, nt, d_nodes_, bufs, stream);
+  launch_partition(ra, nt, stream);
   timed_end(ST_PARTITION, 2.0 * bytes, stream);
 
   DQ_HIP(hipMemcpyAsync(h_nodes_, d_nodes_, nn * sizeof(DevNode), hipMemcpyDeviceToHost, stream));
@@ -238,14 +248,14 @@ void Engine::run_round(const std::vector<int>& active, bool root_round,
   for (int a = 0; a < nn; ++a) {
     const int id = active[a];
     const DevNode& d = h_nodes_[a];
-    Node& p = nodes_[id];
     if (root_round) {
-      for (int c = 0; c < 3; ++c) { p.mean[c] = d.tm[c]; p.var[c] = d.tv[c]; }
+      for (int c = 0; c < 3; ++c) { nodes_[id].mean[c] = d.tm[c]; nodes_[id].var[c] = d.tv[c]; }
     }
+    const Node& p = nodes_[id];
     const uint32_t n_new = (uint32_t)d.n_new;
     const uint32_t n_old = p.len - n_new;
     Node co, cn;
-    co.parent = cn.parent = id;
+    co.frame = cn.frame = p.frame;
     co.w = d.ow;
     cn.w = d.nw;
     for (int c = 0; c < 3; ++c) {
@@ -271,115 +281,194 @@ void Engine::run_round(const std::vector<int>& active, bool root_round,
   }
 }
 
-int Engine::cluster(const uint32_t* d_in, uint32_t n, int k, int max_iters,
-                    uint32_t* ct, int* num_empty, hipStream_t stream) {
-  DQ_CHECK(n > 0, "num_points must be > 0 (DivQuantCluster.cpp:211)");
-  DQ_CHECK(k > 0, "num_colors must be > 0 (DivQuantCluster.cpp:229)");
+// ---------------------------------------------------------------------------
+// Replay the reference's greedy order (:346-892) as far as the expanded tree
+// allows; f.need = the unexpanded node it stopped at (-1 when all K-1 splits
+// are known).
+void Engine::replay(FrameState& f) {
+  const int k = f.job->k;
+  f.need = -1;
+  while (f.new_index < k) {
+    const int x = f.leaf[f.old_index];
+    if (!nodes_[x].expanded) { f.need = x; return; }
+    const int co = nodes_[x].child_old, cn = nodes_[x].child_new;
+    f.trace.push_back(f.new_index);
+    f.trace.push_back(f.old_index);
+    f.trace.push_back(nodes_[x].len);
+    f.trace.push_back(nodes_[cn].len);
+    f.leaf[f.old_index] = co;
+    f.leaf[f.new_index] = cn;
+    if (f.new_index == k - 1) { ++f.new_index; return; }     // :823-832
+    // STEP 4 (:876-887): max TSE above DBL_MIN, lowest index among equals;
+    // if none qualifies old_index stays (the old half is split again).
+    if (nodes_[co].tse > DBL_MIN) f.heap.push({{nodes_[co].tse, -f.old_index}, co});
+    if (nodes_[cn].tse > DBL_MIN) f.heap.push({{nodes_[cn].tse, -f.new_index}, cn});
+    while (!f.heap.empty() && f.leaf[-f.heap.top().first.second] != f.heap.top().second)
+      f.heap.pop();
+    if (!f.heap.empty()) f.old_index = -f.heap.top().first.second;
+    ++f.new_index;
+  }
+}
+
+// Next round's nodes of a frame: the node the replay waits for plus every
+// unexpanded leaf among the top r = (splits left) of the greedy order -- a
+// leaf outside the current top r can never be picked in the remaining splits.
+void Engine::next_active(FrameState& f, std::vector<int>* active) {
+  if (f.need < 0) return;
+  const int r = f.job->k - f.new_index;
+  active->push_back(f.need);
+  auto h = f.heap;
+  int taken = 0;
+  while (!h.empty() && taken < r) {
+    const auto top = h.top();
+    h.pop();
+    const int idx = -top.first.second, node = top.second;
+    if (f.leaf[idx] != node) continue;
+    ++taken;
+    if (!nodes_[node].expanded && node != f.need) active->push_back(node);
+  }
+}
+
+// Final centres (:1029-1094): round, pack, drop empty clusters.
+void Engine::finish_frame(FrameState& f, bool last) {
+  FrameJob& job = *f.job;
+  const int k = job.k;
+  int out = 0, empty = 0;
+  if (last) {
+    last_means.assign((size_t)k * 3, 0.0);
+    last_sizes.assign(k, 0);
+    last_trace = f.trace;
+  }
+  if (k == 1) {
+    // No split happens: mean[0] keeps its zero initialisation (:309).
+    job.ct[out++] = 0;
+    if (last) last_sizes[0] = job.n;
+  } else {
+    for (int ic = 0; ic < k; ++ic) {
+      const Node& nd = nodes_[f.leaf[ic]];
+      if (last) {
+        for (int c = 0; c < 3; ++c) last_means[3 * ic + c] = nd.mean[c];
+        last_sizes[ic] = nd.len;
+      }
+      if (nd.len > 0) {
+        const uint32_t R = (uint8_t)(nd.mean[0] + 0.5);
+        const uint32_t G = (uint8_t)(nd.mean[1] + 0.5);
+        const uint32_t B = (uint8_t)(nd.mean[2] + 0.5);
+        job.ct[out++] = (R << 16) | (G << 8) | B;
+      } else {
+        ++empty;
+      }
+    }
+  }
+  job.k_out = out;
+  job.num_empty = empty;
+}
+
+void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
+                 hipStream_t stream) {
+  DQ_CHECK(nframes > 0, "empty batch");
   DQ_CHECK(max_iters >= 1, "max_iters < 1 is not supported (the reference never writes member[] then)");
   DQ_HIP(hipSetDevice(device_));
   if (!stream) stream = stream_;
-  // get_double_scale (DivQuantMapColors.cpp:205-220)
-  const double s = 1.0 / (std::ceil(1 / 1.0) * std::ceil(n / 1.0));
 
-  last_means.assign((size_t)k * 3, 0.0);
-  last_sizes.assign(k, 0);
-  last_trace.clear();
+  frames_.assign(nframes, FrameState());
+  nodes_.clear();
   last_rounds = 0;
   last_points_swept = 0;
-  nodes_.clear();
-  nodes_.reserve(4 * (size_t)k + 8);
-  Node root;
-  root.w = 1.0;          // :329
-  root.off = 0;
-  root.len = n;
-  root.buf = BUF_IN;
-  nodes_.push_back(root);
+  size_t total = 0, align_need = 0;
+  for (int i = 0; i < nframes; ++i) {
+    FrameJob& j = jobs[i];
+    DQ_CHECK(j.n > 0, "num_points must be > 0 (DivQuantCluster.cpp:211)");
+    DQ_CHECK(j.k > 0, "num_colors must be > 0 (DivQuantCluster.cpp:229)");
+    DQ_CHECK(j.d_in && j.ct, "null buffer");
+    frames_[i].job = &j;
+    frames_[i].base = (uint32_t)total;
+    total += align4(j.n) + 4;
+    if (((uintptr_t)j.d_in & 15) != 0) align_need += align4(j.n) + 4;
+  }
+  DQ_CHECK(total < (1ull << 32), "batch larger than 2^32 points");
+  ensure_pixels(total);
+  if (align_need > cap_align_) {
+    if (d_align_) DQ_HIP(hipFree(d_align_));
+    DQ_HIP(hipMalloc((void**)&d_align_, align_need * sizeof(uint32_t)));
+    cap_align_ = align_need;
+  }
+  size_t aoff = 0;
+  std::vector<int> active;
+  for (int i = 0; i < nframes; ++i) {
+    FrameState& f = frames_[i];
+    FrameJob& j = *f.job;
+    // get_double_scale (DivQuantMapColors.cpp:205-220)
+    f.s = 1.0 / (std::ceil(1 / 1.0) * std::ceil(j.n / 1.0));
+    f.in = j.d_in;
+    if (((uintptr_t)j.d_in & 15) != 0) {   // the sweeps use 16-B loads
+      DQ_HIP(hipMemcpyAsync(d_align_ + aoff, j.d_in, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
+      f.in = d_align_ + aoff;
+      aoff += align4(j.n) + 4;
+    }
+    Node root;
+    root.frame = i;
+    root.w = 1.0;          // :329
+    root.len = j.n;
+    root.buf = BUF_IN;
+    f.leaf.assign(j.k, -1);
+    f.leaf[0] = (int)nodes_.size();
+    nodes_.push_back(root);
+    if (j.k > 1) active.push_back(f.leaf[0]);
+  }
 
-  std::vector<int> leaf(k, -1);
-  leaf[0] = 0;
-  if (k > 1) {
-    ensure_pixels(n);
-    staged_root_ = d_in;
-    std::priority_queue<Cand, std::vector<Cand>, CandLess> heap;
-    int new_index = 1, old_index = 0;
-    std::vector<int> active{0};
-    bool root_round = true;
-    while (true) {
-      run_round(active, root_round, max_iters, s, stream);
-      root_round = false;
-      last_rounds++;
-      // Replay the greedy order as far as the expanded tree allows.
-      int need = -1;
-      while (new_index < k) {
-        const int x = leaf[old_index];
-        if (!nodes_[x].expanded) { need = x; break; }
-        const int co = nodes_[x].child_old, cn = nodes_[x].child_new;
-        last_trace.push_back(new_index);
-        last_trace.push_back(old_index);
-        last_trace.push_back(nodes_[x].len);
-        last_trace.push_back(nodes_[cn].len);
-        leaf[old_index] = co;
-        leaf[new_index] = cn;
-        if (new_index == k - 1) { ++new_index; break; }   // :823-832
-        if (nodes_[co].tse > DBL_MIN) heap.push({nodes_[co].tse, old_index, co});
-        if (nodes_[cn].tse > DBL_MIN) heap.push({nodes_[cn].tse, new_index, cn});
-        while (!heap.empty() && leaf[heap.top().idx] != heap.top().node) heap.pop();
-        if (!heap.empty()) old_index = heap.top().idx;   // else unchanged (:876)
-        ++new_index;
-      }
-      if (need < 0) break;
-      // Next round: the leaf the replay is waiting for, plus every unexpanded
-      // leaf that ranks among the next r greedy picks (r splits remain; a
-      // leaf outside the top r of the current frontier can never be picked).
-      const int r = k - new_index;
-      std::vector<Cand> cands;
-      {
-        auto h2 = heap;
-        while (!h2.empty() && (int)cands.size() < r) {
-          Cand c = h2.top();
-          h2.pop();
-          if (leaf[c.idx] != c.node) continue;
-          cands.push_back(c);
-        }
-      }
-      active.clear();
-      active.push_back(need);
-      for (const Cand& c : cands)
-        if (!nodes_[c.node].expanded && c.node != need) active.push_back(c.node);
+  bool root_round = true;
+  while (!active.empty()) {
+    run_round(active, root_round, max_iters, stream);
+    root_round = false;
+    last_rounds++;
+    active.clear();
+    for (auto& f : frames_) {
+      if (f.job->k <= 1 || (f.need < 0 && f.new_index >= f.job->k)) continue;
+      replay(f);
+      next_active(f, &active);
     }
   }
 
-  // Final centres (:1029-1094).
-  int out = 0, empty = 0;
-  for (int ic = 0; ic < k; ++ic) {
-    const Node& nd = nodes_[leaf[ic]];
-    if (k == 1) {
-      // mean[0] is never assigned when no split happens: it stays 0.0.
-      last_sizes[0] = n;
-      ct[out++] = 0;
-      break;
-    }
-    for (int c = 0; c < 3; ++c) last_means[3 * ic + c] = nd.mean[c];
-    last_sizes[ic] = nd.len;
-    if (nd.len > 0) {
-      const uint32_t R = (uint8_t)(nd.mean[0] + 0.5);
-      const uint32_t G = (uint8_t)(nd.mean[1] + 0.5);
-      const uint32_t B = (uint8_t)(nd.mean[2] + 0.5);
-      ct[out++] = (R << 16) | (G << 8) | B;
-    } else {
-      ++empty;
+  for (int i = 0; i < nframes; ++i) finish_frame(frames_[i], i == nframes - 1);
+
+  if (dedup_map) {
+    for (auto& f : frames_) {
+      FrameJob& j = *f.job;
+      // First-occurrence colortable dedup (quant_util.cpp:93-118).
+      std::unordered_set<uint32_t> seen;
+      int m = 0;
+      for (int i = 0; i < j.k_out; ++i)
+        if (seen.insert(j.ct[i]).second) j.ct[m++] = j.ct[i];
+      j.k_out = m;
+      if (j.d_out) map(f.in, j.n, j.d_out, j.ct, m, stream);
     }
   }
-  if (num_empty) *num_empty = empty;
-  return out;
 }
 
+// ---------------------------------------------------------------------------
 void Engine::map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
                  const uint32_t* ct, int k, hipStream_t stream) {
   DQ_CHECK(k > 0, "colormapSize must be > 0 (DivQuantMapColors.cpp:264)");
   DQ_CHECK(k <= 16384, "colormapSize > 16384 is not supported by the LDS palette");
   DQ_HIP(hipSetDevice(device_));
   if (!stream) stream = stream_;
+  if (((uintptr_t)d_in & 15) != 0 || ((uintptr_t)d_out & 15) != 0) {
+    // the map kernel uses 16-B loads/stores: go through aligned staging
+    const size_t want = align4(n) + 4;
+    if (2 * want > cap_map_align_) {
+      if (d_map_align_) DQ_HIP(hipFree(d_map_align_));
+      DQ_HIP(hipMalloc((void**)&d_map_align_, want * 2 * sizeof(uint32_t)));
+      cap_map_align_ = want * 2;
+    }
+    uint32_t* ain = d_map_align_;
+    uint32_t* aout = d_map_align_ + want;
+    DQ_HIP(hipMemcpyAsync(ain, d_in, (size_t)n * 4, hipMemcpyDeviceToDevice, stream));
+    map(ain, n, aout, ct, k, stream);
+    DQ_HIP(hipMemcpyAsync(d_out, aout, (size_t)n * 4, hipMemcpyDeviceToDevice, stream));
+    DQ_HIP(hipStreamSynchronize(stream));
+    return;
+  }
   // Palette sorted by R+G+B with std::sort and the reference comparator
   // (:227-238, :314-323) -- same algorithm, same input => same tie order.
   struct Ent { int red, green, blue, weight; };
@@ -395,28 +484,29 @@ void Engine::map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
             [](const Ent& a, const Ent& b) { return a.weight < b.weight; });
   // Start-entry LUT from rounded midpoints (:331-383).
   int lut[766];
-  int low = k >= 2 ? (int)(0.5 * (pal[0].weight + pal[1].weight) + 0.5) : 1;
+  const int low = k >= 2 ? (int)(0.5 * (pal[0].weight + pal[1].weight) + 0.5) : 1;
   for (int v = 0; v < low; ++v) lut[v] = 0;
-  int high = k >= 2 ? (int)(0.5 * (pal[k - 2].weight + pal[k - 1].weight) + 0.5) : 1;
+  const int high = k >= 2 ? (int)(0.5 * (pal[k - 2].weight + pal[k - 1].weight) + 0.5) : 1;
   for (int v = high; v < 766; ++v) lut[v] = k - 1;
   for (int i = 1; i < k - 1; ++i) {
     const int lo = (int)(0.5 * (pal[i - 1].weight + pal[i].weight) + 0.5);
     const int hi = (int)(0.5 * (pal[i].weight + pal[i + 1].weight) + 0.5);
     for (int v = lo; v < hi; ++v) lut[v] = i;
   }
+  // The pinned staging below is reused by the next call: wait for the
+  // previous map's copies first.
+  DQ_HIP(hipStreamSynchronize(stream));
   for (int i = 0; i < k; ++i)
     h_pal_[i] = ((uint32_t)pal[i].red << 16) | ((uint32_t)pal[i].green << 8) | (uint32_t)pal[i].blue;
   for (int v = 0; v < 766; ++v) h_lut_[v] = (uint16_t)lut[v];
   DQ_HIP(hipMemcpyAsync(d_pal_, h_pal_, k * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
   DQ_HIP(hipMemcpyAsync(d_lut_, h_lut_, 766 * sizeof(uint16_t), hipMemcpyHostToDevice, stream));
   timed_begin(stream);
-  launch_build_cells(d_pal_, k, d_cell_cnt_, d_cell_idx_, stream);
+  launch_build_cells(d_pal_, k, d_cell_rec_, d_cell_idx_, stream);
   timed_end(ST_CELLS, 0.0, stream);
   timed_begin(stream);
-  launch_map(d_in, n, d_out, d_pal_, k, d_lut_, d_cell_cnt_, d_cell_idx_, stream);
+  launch_map(d_in, n, d_out, d_pal_, k, d_lut_, d_cell_rec_, d_cell_idx_, stream);
   timed_end(ST_MAP, 8.0 * (double)n, stream);
-  // The host staging buffers (h_pal_/h_lut_) are reused by the next call:
-  // wait for the copies (and the map) before returning.
   DQ_HIP(hipStreamSynchronize(stream));
   collect_timing();
 }

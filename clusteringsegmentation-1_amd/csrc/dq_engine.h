@@ -6,17 +6,17 @@
 // only on that cluster's points and its stored weight/mean/variance, never on
 // the order in which clusters are split.  The engine therefore expands the
 // binary split tree in ROUNDS: a round splits a whole batch of leaves at once
-// (every pass of the round is ONE kernel launch over all their points), and
-// a host-side replay of the reference's greedy max-TSE order (:873-892)
-// decides which leaves the next round must expand.  The replay needs no
-// floating point of its own: the TSEs it compares come from the device
-// epilogue, which evaluates the reference's FP64 expressions verbatim.
+// -- of every frame in the batch -- and every pass of the round is ONE kernel
+// launch over all their points.  A host-side replay of the reference's greedy
+// max-TSE order (:873-892) decides which leaves the next round must expand.
+// The replay needs no floating point of its own: the TSEs it compares come
+// from the device, which evaluates the reference's FP64 expressions verbatim.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <mutex>
-#include <string>
+#include <queue>
 #include <vector>
 
 #include "dq_internal.h"
@@ -35,17 +35,29 @@ namespace dq {
     if (!(cond)) ::dq::die(#cond, __FILE__, __LINE__, msg);               \
   } while (0)
 
-// A node of the split tree: one cluster as it exists between two splits.
+// A node of a frame's split tree: one cluster as it exists between splits.
 struct Node {
-  int parent = -1;
+  int frame = 0;
   int child_old = -1, child_new = -1;
   bool expanded = false;
+  int32_t buf = 0;                   // 0: caller's input, 1: P0, 2: P1
   double w = 0.0;                    // weight[]   (:290, :862-863)
   double mean[3] = {0, 0, 0};        // mean[]     (:309)
   double var[3] = {0, 0, 0};         // var[]      (:314)
   double tse = 0.0;                  // tse[]      (:304)
   uint32_t off = 0, len = 0;         // segment (len == size[] of the cluster)
-  int32_t buf = BUF_IN;
+};
+
+// One quant_recurse / DivQuantCluster input.
+struct FrameJob {
+  const uint32_t* d_in = nullptr;    // device, n points
+  uint32_t n = 0;
+  uint32_t* d_out = nullptr;         // device, mapped colours (nullptr: cluster only)
+  int k = 0;                         // requested clusters
+  uint32_t* ct = nullptr;            // host, >= k entries
+  // outputs
+  int k_out = 0;                     // colours written to ct
+  int num_empty = 0;                 // empty clusters (:1067-1069)
 };
 
 // Per-kernel-kind timing (filled only when timing is enabled).
@@ -64,12 +76,10 @@ class Engine {
   Engine(const Engine&) = delete;
   Engine& operator=(const Engine&) = delete;
 
-  // DivQuantCluster<true,*,true> (:133-1097) over n device-resident points.
-  // Writes the non-empty cluster colours to ct (host, >= k entries) in
-  // cluster-index order and returns their number; *num_empty gets the
-  // number of empty clusters (:1067-1069).
-  int cluster(const uint32_t* d_in, uint32_t n, int k, int max_iters,
-              uint32_t* ct, int* num_empty, hipStream_t stream);
+  // DivQuantCluster<true,*,true> (:133-1097) over every frame of the batch;
+  // with dedup_map, also the colortable dedup (quant_util.cpp:93-118) and
+  // map_colors_mps into each frame's d_out.  All frames use max_iters.
+  void run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map, hipStream_t stream);
 
   // map_colors_mps (DivQuantMapColors.cpp:243-539) on device buffers.
   void map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
@@ -84,22 +94,38 @@ class Engine {
   int device() const { return device_; }
   std::mutex& mutex() { return mu_; }
 
-  // Diagnostics of the last cluster() call.
+  // Diagnostics of the last frame of the last run().
   std::vector<double> last_means;     // K*3 centroid doubles per cluster index
   std::vector<int64_t> last_sizes;    // K sizes
   std::vector<int64_t> last_trace;    // (K-1)*4: new_index old_index |C| |new|
   int last_rounds = 0;
-  uint64_t last_points_swept = 0;     // sum over passes of points read
+  uint64_t last_points_swept = 0;     // sum over passes of points read (all frames)
 
   void set_timing(bool on) { timing_ = on; }
   void reset_stats();
   KernelStat stats[ST_COUNT];
 
  private:
-  void ensure_pixels(uint32_t n);
-  void ensure_round(size_t nnodes, size_t ntiles);
+  struct FrameState {
+    FrameJob* job = nullptr;
+    double s = 0.0;                   // get_double_scale
+    uint32_t base = 0;                // frame offset in P0/P1 (16-B aligned)
+    const uint32_t* in = nullptr;     // 16-B aligned input (maybe a staged copy)
+    std::vector<int> leaf;            // cluster index -> node id
+    std::priority_queue<std::pair<std::pair<double, int>, int>> heap;  // ((tse,-idx), node)
+    int new_index = 1, old_index = 0;
+    int need = -1;                    // node the replay waits for (-1: done)
+    std::vector<int64_t> trace;
+  };
+
+  void ensure_pixels(size_t total);
+  void ensure_round(size_t nnodes, size_t ntiles, size_t nshards);
   void run_round(const std::vector<int>& active, bool root_round, int max_iters,
-                 double s, hipStream_t stream);
+                 hipStream_t stream);
+  void replay(FrameState& f);
+  void next_active(FrameState& f, std::vector<int>* active);
+  void finish_frame(FrameState& f, bool last);
+  const uint32_t* buf_ptr(int buf, const FrameState& f) const;
   void timed_begin(hipStream_t stream);
   void timed_end(int kind, double bytes, hipStream_t stream);
   void collect_timing();
@@ -109,32 +135,37 @@ class Engine {
   std::mutex mu_;
   bool timing_ = false;
 
-  // pixel working buffers (segments of the split tree)
+  // pixel working buffers (segments of the split trees of all frames)
   uint32_t* d_p0_ = nullptr;
   uint32_t* d_p1_ = nullptr;
   size_t cap_px_ = 0;
   uint32_t* d_stage_in_ = nullptr;
   uint32_t* d_stage_out_ = nullptr;
   size_t cap_stage_ = 0;
+  uint32_t* d_align_ = nullptr;       // aligned copies of misaligned inputs
+  size_t cap_align_ = 0;
+  uint32_t* d_map_align_ = nullptr;   // map staging for misaligned in/out
+  size_t cap_map_align_ = 0;
 
-  // per-round node/tile tables
+  // per-round node/tile/accumulator tables
   DevNode* d_nodes_ = nullptr;
   Tile* d_tiles_ = nullptr;
-  TilePartial* d_parts_ = nullptr;
+  uint64_t* d_acc_ = nullptr;
+  uint32_t* d_tile_cnt_ = nullptr;
   DevNode* h_nodes_ = nullptr;   // pinned
   Tile* h_tiles_ = nullptr;      // pinned
-  size_t cap_nodes_ = 0, cap_tiles_ = 0;
+  size_t cap_nodes_ = 0, cap_tiles_ = 0, cap_shards_ = 0;
 
   // map tables
   uint32_t* d_pal_ = nullptr;
   uint16_t* d_lut_ = nullptr;
-  uint16_t* d_cell_cnt_ = nullptr;
+  uint4* d_cell_rec_ = nullptr;
   uint16_t* d_cell_idx_ = nullptr;
   uint32_t* h_pal_ = nullptr;    // pinned
   uint16_t* h_lut_ = nullptr;    // pinned
 
   std::vector<Node> nodes_;
-  const uint32_t* staged_root_ = nullptr;   // the caller's input (root segment)
+  std::vector<FrameState> frames_;
   struct PendingEvent { hipEvent_t a, b; int kind; double bytes; };
   std::vector<PendingEvent> pending_;
   std::vector<hipEvent_t> event_pool_;

@@ -10,16 +10,12 @@
 //                      iteration (:613-811);
 //   segment         -- the contiguous range [off, off+len) of a working pixel
 //                      buffer that holds one node's points;
-//   tile            -- the part of a segment one workgroup sweeps in a pass.
+//   tile            -- the part of a segment one workgroup sweeps in a pass;
+//   frame           -- one quant_recurse input; a round may mix frames.
 #pragma once
 #include <stdint.h>
 
 namespace dq {
-
-// Pixel buffers a segment can live in.  The root lives in the caller's input;
-// children of a node in buffer b are written to the "other" working buffer.
-enum BufId : int32_t { BUF_IN = 0, BUF_P0 = 1, BUF_P1 = 2 };
-inline int child_buf(int b) { return b == BUF_P0 ? BUF_P1 : BUF_P0; }
 
 // Pass kinds (kernel template parameter).
 enum PassKind : int32_t {
@@ -29,43 +25,45 @@ enum PassKind : int32_t {
   PASS_KLAST = 3,    // last 2-means iteration: also sums of squares (:726-748)
 };
 
-// Per-node state for one round.  All FP64 fields follow the reference's
-// variable of the same role; the device epilogue updates them between passes.
+// Statistics of one accumulator shard: exact integer sums of the new side
+// (all points in PASS_INIT).  One 128-B line per shard.
+enum AccField : int32_t { F_CNT = 0, F_SR, F_SG, F_SB, F_QR, F_QG, F_QB, F_NUM };
+constexpr int kAccStride = 16;          // u64 per shard (128 B)
+constexpr int kAccSets = 3;             // pass p writes set p%3, reads (p-1)%3, zeroes (p+1)%3
+constexpr int kMaxShards = 64;          // shards per node (one per lane of wave 0)
+
+// Per-node state for one round.
 struct alignas(16) DevNode {
   // --- set by the host when the round starts
-  uint32_t off, len;        // segment of this node's points
-  int32_t buf;              // BufId the points live in
+  const uint32_t* src;      // element 0 of the frame in the buffer holding the node
+  uint32_t* dst;            // element 0 of the frame in the child buffer
+  uint32_t off, len;        // segment, relative to src / dst
   int32_t tile_begin;       // this node's tiles are [tile_begin, tile_end)
   int32_t tile_end;
+  int32_t shard_base;       // accumulator shards [shard_base, shard_base+nshard)
+  int32_t nshard;
+  int32_t root;             // 1: tm/tv/axis/cut come from the device INIT pass
+  int32_t thr;              // split pass: new iff v_axis >= thr  (== cut_pos < v)
   int32_t axis;             // split pass: cut axis (0=R,1=G,2=B) (:388-403)
-  double cut;               // split pass: cut position
+  int32_t pad0;
+  double s;                 // data_weight of the frame (get_double_scale)
   double tw;                // total_weight = weight[old_index]  (:353)
   double tm[3], tv[3];      // total_mean / total_var           (:357-374)
-  // --- current 2-means decision parameters (written by the epilogues)
-  double lhs, rr, rg, rb;   // (:616-623)
-  double om[3], nm[3];      // old_mean / new_mean
-  // --- decision of the LAST 2-means pass (kept for the partition sweep)
-  double plhs, prr, prg, prb;
-  // --- results of the node's split (read back by the host)
-  uint64_t n_new;           // new_size (:820-821)
-  double nw, ow;            // new_weight / old_weight
+  // --- results of the node's split (written by the partition kernel)
+  double plhs, prr, prg, prb;   // decision of the last 2-means pass
+  double om[3], nm[3];      // old_mean / new_mean after the last pass
   double nv[3], ov[3];      // new_var / old_var (:836-855)
+  double nw, ow;            // new_weight / old_weight
   double tse_old, tse_new;  // (:870-871)
+  uint64_t n_new;           // new_size (:820-821)
+  uint64_t pad1;
 };
 
 // One workgroup's share of a pass.
 struct alignas(16) Tile {
   int32_t node;             // index into the round's DevNode array
-  uint32_t start, end;      // absolute pixel range in the node's buffer
-  uint32_t old_base;        // partition: rank of this tile's first old point
-};
-
-// Per-tile partial statistics of the new side (or of all points in PASS_INIT).
-struct alignas(16) TilePartial {
-  uint64_t cnt;
-  uint64_t s[3];            // sum R, G, B
-  uint64_t q[3];            // sum R^2, G^2, B^2 (PASS_INIT / PASS_KLAST)
-  uint64_t pad;
+  uint32_t start, end;      // pixel range relative to the node's src
+  uint32_t local;           // tile index inside its node (shard = local % nshard)
 };
 
 }  // namespace dq

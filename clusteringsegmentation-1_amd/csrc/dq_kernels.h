@@ -10,43 +10,41 @@
 
 namespace dq {
 
-constexpr int kBlock = 256;                 // 4 wave64 per workgroup
-constexpr int kPxPerThread = 16;            // points per lane per sweep step
-constexpr int kSweep = kBlock * kPxPerThread;   // 4096 points per step
-constexpr uint32_t kMaxTilePx = 16 * kSweep;    // keeps per-wave u32 sums exact
+constexpr int kBlock = 256;                     // 4 wave64 per workgroup
+constexpr int kVecPerThread = 4;                // uint4 loads per lane per sweep
+constexpr int kSweep = kBlock * kVecPerThread * 4;   // 4096 points per sweep
+constexpr uint32_t kMaxTilePx = 16 * kSweep;    // keeps packed 16-bit lane sums exact
 
 // Map (nearest palette entry) cell grid: 32 cells of 8 values per channel.
 constexpr int kCellBits = 5;
 constexpr int kCells = 1 << (3 * kCellBits);
-constexpr int kCellCap = 32;                // candidates stored per cell
-constexpr uint16_t kCellOverflow = 0xFFFF;  // count marker: scan whole palette
+constexpr int kCellInline = 7;                  // candidates stored in the 16-B record
+constexpr int kCellCap = 32;                    // candidates in the overflow list
+constexpr uint32_t kCellBrute = 0xFFFF;         // count marker: scan the whole palette
 
-struct PixelBufs {
-  const uint32_t* in;
-  uint32_t* p0;
-  uint32_t* p1;
+// Accumulator sets for one round: kAccSets x total_shards x kAccStride u64.
+struct RoundArgs {
+  const Tile* tiles;
+  DevNode* nodes;
+  uint64_t* acc;
+  uint32_t* tile_cnt;       // PASS_KLAST: new-side count per tile
+  int32_t total_shards;
+  int32_t pass;             // pass index inside the round (selects the sets)
 };
 
-// One statistics pass over every tile of the round.
-void launch_pass(int kind, const Tile* tiles, int ntiles, const DevNode* nodes,
-                 PixelBufs bufs, TilePartial* parts, hipStream_t stream);
+void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
+// Reduces the last two passes' sums per node, writes the split results into
+// DevNode, and writes every node's points into its two children's segments
+// (old half first, then new half), in index order, in the child buffer.
+void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream);
 
-// FP64 epilogue of a pass, one workgroup per node (reduces that node's tiles).
-void launch_epilogue(int kind, DevNode* nodes, int nnodes, Tile* tiles,
-                     const TilePartial* parts, double s, hipStream_t stream);
-
-// Writes every node's points into its two children's segments (old half
-// first, then new half), in index order, in the other working buffer.
-void launch_partition(const Tile* tiles, int ntiles, const DevNode* nodes,
-                      PixelBufs bufs, hipStream_t stream);
-
-// Map: candidate lists per colour cell, then the per-pixel argmin over
+// Map: candidate records per colour cell, then the per-pixel argmin over
 // (squared distance, MPS visit rank).
-void launch_build_cells(const uint32_t* pal_sorted, int k, uint16_t* cell_cnt,
+void launch_build_cells(const uint32_t* pal_sorted, int k, uint4* cell_rec,
                         uint16_t* cell_idx, hipStream_t stream);
 void launch_map(const uint32_t* in, uint32_t n, uint32_t* out,
                 const uint32_t* pal_sorted, int k, const uint16_t* lut_init,
-                const uint16_t* cell_cnt, const uint16_t* cell_idx,
+                const uint4* cell_rec, const uint16_t* cell_idx,
                 hipStream_t stream);
 
 }  // namespace dq

@@ -3,24 +3,29 @@
 // MUST be compiled with -ffp-contract=off: every FP64 expression here mirrors
 // an expression of the reference (DivQuant/DivQuantCluster.cpp) operation by
 // operation, and a fused multiply-add would change its rounding.
-// tests/test_build.py checks the code object for v_fma_f64 in the pass kernels.
+// tests/test_build.py checks the code object for v_fma_f64 outside divisions.
 //
 // Kernels
-//   pass_kernel<KIND>     one sweep over the tiles of every node being split:
-//                         a per-point decision + exact integer new-side sums
-//                         (split pass :438-559, 2-means pass :613-811, root
-//                         statistics :49-104).  HBM-bound: 4 B read per point.
-//   epilogue_kernel<KIND> per node: sum the node's tile partials and run the
-//                         reference's FP64 update (:561-598, :787-871).
-//   partition_kernel      writes each node's points into its two children's
-//                         segments in index order (replaces the per-split
-//                         O(N) member[] gather, :894-1026).
-//   build_cells_kernel    map: per 8x8x8 colour cell, the palette entries that
-//                         can be nearest to some colour of the cell.
-//   map_kernel            map: per pixel argmin over (squared distance, MPS
-//                         visit rank) -- identical to map_colors_mps's pruned
-//                         walk (DivQuantMapColors.cpp:385-527), see DESIGN.md.
+//   pass_kernel<KIND>  one sweep over the tiles of every node being split
+//                      (all frames of the batch): per-point decision + exact
+//                      integer new-side sums (split pass :438-559, 2-means
+//                      pass :613-811, root statistics :49-104).  The FP64
+//                      update of the PREVIOUS pass (:561-598, :787-810) runs
+//                      in each workgroup's prologue from the sharded u64
+//                      sums, so a pass is one launch and needs no epilogue
+//                      kernel.  HBM/MALL-bound: 4 B read per point.
+//   partition_kernel   final FP64 update of the split (:787-871) and the
+//                      write of each node's points into its two children's
+//                      segments in index order (replaces the per-split O(N)
+//                      member[] gather, :894-1026).
+//   build_cells_kernel map: per 8x8x8 colour cell, the palette entries that
+//                      can be nearest to some colour of the cell.
+//   map_kernel         map: per pixel argmin over (squared distance, MPS
+//                      visit rank) -- identical to map_colors_mps's pruned
+//                      walk (DivQuantMapColors.cpp:385-527), see DESIGN.md.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "dq_kernels.h"
 
@@ -48,299 +53,375 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
-__device__ __forceinline__ const uint32_t* src_of(const PixelBufs& b, int buf) {
-  return buf == BUF_IN ? b.in : (buf == BUF_P0 ? b.p0 : b.p1);
+__device__ __forceinline__ uint64_t* acc_shard(const RoundArgs& a, int set, int shard) {
+  return a.acc + ((size_t)set * a.total_shards + shard) * kAccStride;
 }
 
-// The 2-means decision (:683): a point stays OLD iff
-//   lhs < rr*R + rg*G + rb*B    (left to right, every product rounded).
-// Ties and NaN (empty new half, :579) go NEW.
-__device__ __forceinline__ bool stays_old(uint32_t p, double lhs, double rr,
-                                          double rg, double rb) {
+// Wave-level sum of the first nf fields of a node's shards in `set`
+// (lane i reads shard i).  Valid in every lane of the calling wave.
+__device__ __forceinline__ void reduce_shards(const RoundArgs& a, const DevNode& nd, int set,
+                                              int nf, uint64_t t[F_NUM]) {
+  const int l = (int)lane_id();
+  const uint64_t* p = l < nd.nshard ? acc_shard(a, set, nd.shard_base + l) : nullptr;
+  for (int f = 0; f < F_NUM; ++f) {
+    uint64_t v = 0;
+    if (f < nf && p) v = __builtin_nontemporal_load(p + f);
+    t[f] = f < nf ? wave_sum_u64(v) : 0;
+  }
+}
+
+// Decision parameters of one pass, broadcast through LDS.
+struct Params {
+  double lhs, rr, rg, rb;   // exact FP64 decision (:616-623, :683)
+  float lhsf, rrf, rgf, rbf, eps;   // FP32 pre-filter (see stays_old)
+  int32_t thr, shift;       // split pass
+};
+
+// (:561-598 / :787-810) means and weights of both halves from the new side's
+// exact integer sums.  cnt/sums are exact in double (all < 2^53).
+__device__ __forceinline__ void means_from_sums(const uint64_t t[F_NUM], double s, double tw,
+                                                const double tm[3], double om[3], double nm[3],
+                                                double* nw_out, double* ow_out) {
+  const double nw = (double)t[F_CNT] * s;
+  const double ow = tw - nw;
+  for (int c = 0; c < 3; ++c) {
+    double m = (double)t[F_SR + c];
+    m *= s;
+    nm[c] = m / nw;
+  }
+  for (int c = 0; c < 3; ++c) om[c] = (tw * tm[c] - nw * nm[c]) / ow;
+  *nw_out = nw;
+  *ow_out = ow;
+}
+
+// (:616-623) + the FP32 filter bound.  The filter evaluates
+//   df = rr*R + rg*G + rb*B - lhs   in f32 (3 fma).
+// With M = (|rr|+|rg|+|rb|)*255 + |lhs|, its error is below 6*2^-24*M
+// (three f32 conversions, three f32 roundings) and the FP64 sum's error is
+// below 3*2^-53*M, so whenever |df| > eps = 8e-7*M the sign of df equals the
+// sign of the FP64 expression's (lhs < sum) outcome.  Non-finite or tiny M
+// (NaN/inf means of an empty half) disables the filter: eps = +inf.
+__device__ __forceinline__ void decision_from_means(const double om[3], const double nm[3],
+                                                    Params* p) {
+  p->lhs = 0.5 * (om[0] * om[0] - nm[0] * nm[0] + om[1] * om[1] - nm[1] * nm[1] +
+                  om[2] * om[2] - nm[2] * nm[2]);
+  p->rr = om[0] - nm[0];
+  p->rg = om[1] - nm[1];
+  p->rb = om[2] - nm[2];
+  const double M = (fabs(p->rr) + fabs(p->rg) + fabs(p->rb)) * 255.0 + fabs(p->lhs);
+  p->lhsf = (float)p->lhs;
+  p->rrf = (float)p->rr;
+  p->rgf = (float)p->rg;
+  p->rbf = (float)p->rb;
+  p->eps = (M > 1e-30 && M < 1e30) ? (float)(8e-7 * M) : __builtin_inff();
+}
+
+// Split pass threshold: cut_pos < v  <=>  v >= thr for integer v in [0,255].
+__device__ __forceinline__ int32_t split_threshold(double cut) {
+  if (!(cut == cut)) return 256;     // NaN: nothing moves
+  if (cut < 0.0) return 0;
+  if (cut >= 255.0) return 256;
+  return (int32_t)floor(cut) + 1;
+}
+
+// The 2-means decision (:683): a point stays OLD iff lhs < rr*R + rg*G + rb*B
+// (left to right, every product rounded).  Ties and NaN go NEW.
+__device__ __forceinline__ bool stays_old_exact(uint32_t p, const Params& q) {
   const double R = (double)((p >> 16) & 0xFF);
   const double G = (double)((p >> 8) & 0xFF);
   const double B = (double)(p & 0xFF);
-  double d = rr * R;
-  d = d + rg * G;
-  d = d + rb * B;
-  return lhs < d;
+  double d = q.rr * R;
+  d = d + q.rg * G;
+  d = d + q.rb * B;
+  return q.lhs < d;
 }
 
-// (:616-623) decision parameters from the current old/new means.
-__device__ __forceinline__ void set_decision(DevNode* n) {
-  const double* o = n->om;
-  const double* w = n->nm;
-  n->lhs = 0.5 * (o[0] * o[0] - w[0] * w[0] + o[1] * o[1] - w[1] * w[1] +
-                  o[2] * o[2] - w[2] * w[2]);
-  n->rr = o[0] - w[0];
-  n->rg = o[1] - w[1];
-  n->rb = o[2] - w[2];
-}
-
-// (:561-598 / :787-810) means and weights of both halves from the new side's
-// exact integer sums.  cnt/sum are exact in double (all < 2^53).
-__device__ __forceinline__ void update_means(DevNode* n, uint64_t cnt,
-                                             const uint64_t sum[3], double s) {
-  const double nw = (double)cnt * s;
-  const double ow = n->tw - nw;
-  for (int a = 0; a < 3; ++a) {
-    double m = (double)sum[a];
-    m *= s;
-    n->nm[a] = m / nw;
+__device__ __forceinline__ bool stays_old(uint32_t p, const Params& q) {
+  const float R = (float)((p >> 16) & 0xFF);
+  const float G = (float)((p >> 8) & 0xFF);
+  const float B = (float)(p & 0xFF);
+  const float df = __builtin_fmaf(q.rrf, R, __builtin_fmaf(q.rgf, G, __builtin_fmaf(q.rbf, B, -q.lhsf)));
+  const bool sure = __builtin_fabsf(df) > q.eps;
+  bool old = df > 0.0f;
+  if (!__all(sure)) {   // wave-uniform: only waves holding a near-boundary point pay FP64
+    const bool ex = stays_old_exact(p, q);
+    old = sure ? old : ex;
   }
-  for (int a = 0; a < 3; ++a)
-    n->om[a] = (n->tw * n->tm[a] - nw * n->nm[a]) / ow;
-  n->nw = nw;
-  n->ow = ow;
-  n->n_new = cnt;
+  return old;
+}
+
+// Load this lane's 4 uint4 of a sweep.  `vs` is the sweep's first (16-B
+// aligned) index; lanes past `end` load nothing; a partial final vector is
+// read element by element so no byte beyond `end` is touched.
+__device__ __forceinline__ void load_sweep(const uint32_t* __restrict__ src, uint32_t vs,
+                                           uint32_t end, uint4 v[kVecPerThread]) {
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    const uint32_t i = vs + 4u * (j * kBlock + threadIdx.x);
+    if (i + 4 <= end) {
+      v[j] = *reinterpret_cast<const uint4*>(src + i);
+    } else {
+      v[j] = make_uint4(0, 0, 0, 0);
+      if (i < end) v[j].x = src[i];
+      if (i + 1 < end) v[j].y = src[i + 1];
+      if (i + 2 < end) v[j].z = src[i + 2];
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t vec_elem(const uint4& v, int e) {
+  return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------
 // Statistics pass.  One workgroup per tile; a tile lies inside one node's
-// segment, so every point of the workgroup shares the node's parameters
-// (scalar loads) and the sums need no per-point binning: lane partials in
-// u32 -> wave reduction -> 4 wave totals in LDS -> one u64 partial per tile.
+// segment, so every point of the workgroup shares the node's parameters and
+// the sums need no per-point binning: packed lane partials -> wave sums ->
+// LDS -> ONE u64 atomic add per field into the node's shard (local % nshard).
 template <int KIND>
-__global__ __launch_bounds__(kBlock) void pass_kernel(
-    const Tile* __restrict__ tiles, const DevNode* __restrict__ nodes,
-    PixelBufs bufs, TilePartial* __restrict__ parts) {
-  const Tile t = tiles[blockIdx.x];
-  const DevNode* nd = nodes + t.node;
-  const uint32_t* __restrict__ src = src_of(bufs, nd->buf);
-
-  int shift = 0;
-  double cut = 0.0, lhs = 0.0, rr = 0.0, rg = 0.0, rb = 0.0;
-  if (KIND == PASS_SPLIT) {
-    shift = 16 - 8 * nd->axis;
-    cut = nd->cut;
-  }
-  if (KIND == PASS_KMEANS || KIND == PASS_KLAST) {
-    lhs = nd->lhs;
-    rr = nd->rr;
-    rg = nd->rg;
-    rb = nd->rb;
-  }
+__global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
+  const Tile t = a.tiles[blockIdx.x];
+  const DevNode& nd = a.nodes[t.node];
+  const uint32_t* __restrict__ src = nd.src;
+  const int set = a.pass % kAccSets;
   constexpr bool kSquares = (KIND == PASS_INIT || KIND == PASS_KLAST);
+  constexpr int kNF = kSquares ? 7 : 4;
 
-  uint32_t c = 0, sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
-  const uint32_t end = t.end;
-  for (uint32_t base = t.start; base < end; base += kSweep) {
-    uint32_t px[kPxPerThread];
-    bool ok[kPxPerThread];
-#pragma unroll
-    for (int j = 0; j < kPxPerThread; ++j) {
-      const uint32_t i = base + j * kBlock + threadIdx.x;
-      ok[j] = i < end;
-      px[j] = src[ok[j] ? i : t.start];
-    }
-#pragma unroll
-    for (int j = 0; j < kPxPerThread; ++j) {
-      const uint32_t p = px[j];
-      bool take;
-      if (KIND == PASS_INIT) {
-        take = ok[j];
-      } else if (KIND == PASS_SPLIT) {
-        take = ok[j] && (cut < (double)((p >> shift) & 0xFF));
-      } else {
-        take = ok[j] && !stays_old(p, lhs, rr, rg, rb);
-      }
-      const uint32_t R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
-      c += take ? 1u : 0u;
-      sr += take ? R : 0u;
-      sg += take ? G : 0u;
-      sb += take ? B : 0u;
-      if (kSquares) {
-        qr += take ? R * R : 0u;
-        qg += take ? G * G : 0u;
-        qb += take ? B * B : 0u;
-      }
-    }
-  }
-
+  __shared__ Params prm;
   __shared__ uint32_t red[kBlock / 64][8];
-  c = wave_sum_u32(c);
-  sr = wave_sum_u32(sr);
-  sg = wave_sum_u32(sg);
-  sb = wave_sum_u32(sb);
-  if (kSquares) {
-    qr = wave_sum_u32(qr);
-    qg = wave_sum_u32(qg);
-    qb = wave_sum_u32(qb);
-  }
-  if (lane_id() == 0) {
-    uint32_t* r = red[wave_id()];
-    r[0] = c; r[1] = sr; r[2] = sg; r[3] = sb;
-    r[4] = qr; r[5] = qg; r[6] = qb; r[7] = 0;
+
+  // Issue the first sweep's loads before the prologue so they overlap it.
+  const uint32_t vs0 = t.start & ~3u;
+  uint4 v[kVecPerThread];
+  load_sweep(src, vs0, t.end, v);
+
+  if (wave_id() == 0) {
+    // Zero this shard of the set the NEXT pass accumulates into.
+    if (t.local < (uint32_t)nd.nshard && lane_id() < kAccStride)
+      acc_shard(a, (a.pass + 1) % kAccSets, nd.shard_base + t.local)[lane_id()] = 0;
+    if (KIND == PASS_SPLIT) {
+      if (nd.root) {
+        // DivQuantClusterInitMeanAndVar (:90-104) from the INIT sums, then
+        // the cut (:388-403).
+        uint64_t tt[F_NUM];
+        reduce_shards(a, nd, (a.pass + kAccSets - 1) % kAccSets, 7, tt);
+        if (lane_id() == 0) {
+          double tm[3], tv[3];
+          for (int c = 0; c < 3; ++c) {
+            double m = (double)tt[F_SR + c];
+            double q = (double)tt[F_QR + c];
+            m *= nd.s;
+            q *= nd.s;
+            q -= m * m;
+            tm[c] = m;
+            tv[c] = q;
+          }
+          double maxv = tv[0], cut = tm[0];
+          int axis = 0;
+          if (maxv < tv[1]) { maxv = tv[1]; axis = 1; cut = tm[1]; }
+          if (maxv < tv[2]) { axis = 2; cut = tm[2]; }
+          prm.thr = split_threshold(cut);
+          prm.shift = 16 - 8 * axis;
+          if (t.local == 0) {   // later passes and the host read the root's tm/tv
+            DevNode& w = a.nodes[t.node];
+            for (int c = 0; c < 3; ++c) { w.tm[c] = tm[c]; w.tv[c] = tv[c]; }
+          }
+        }
+      } else if (lane_id() == 0) {
+        prm.thr = nd.thr;
+        prm.shift = 16 - 8 * nd.axis;
+      }
+    } else if (KIND == PASS_KMEANS || KIND == PASS_KLAST) {
+      uint64_t tt[F_NUM];
+      reduce_shards(a, nd, (a.pass + kAccSets - 1) % kAccSets, 4, tt);
+      if (lane_id() == 0) {
+        double om[3], nm[3], nw, ow;
+        means_from_sums(tt, nd.s, nd.tw, nd.tm, om, nm, &nw, &ow);
+        decision_from_means(om, nm, &prm);
+      }
+    }
   }
   __syncthreads();
-  if (threadIdx.x < 8) {
-    uint64_t v = 0;
+  const Params q = prm;
+
+  // Packed lane partials: rb = R<<16 | B sums, gc = cnt<<16 | G sums (each
+  // half < 2^16 because a tile gives a lane at most 256 points).
+  uint32_t rb = 0, gc = 0, qr = 0, qg = 0, qb = 0;
+  for (uint32_t vs = vs0;;) {
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) v += red[w][threadIdx.x];
-    reinterpret_cast<uint64_t*>(parts + blockIdx.x)[threadIdx.x] = v;
+    for (int j = 0; j < kVecPerThread; ++j) {
+      const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t p = vec_elem(v[j], e);
+        const uint32_t i = i0 + e;
+        const bool valid = (i >= t.start) & (i < t.end);
+        bool take;
+        if (KIND == PASS_INIT) {
+          take = valid;
+        } else if (KIND == PASS_SPLIT) {
+          take = valid && (int32_t)((p >> q.shift) & 0xFF) >= q.thr;
+        } else {
+          take = valid && !stays_old(p, q);
+        }
+        rb += take ? (p & 0x00FF00FFu) : 0u;
+        gc += take ? (((p >> 8) & 0xFFu) | 0x10000u) : 0u;
+        if (kSquares) {
+          const uint32_t R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
+          qr += take ? R * R : 0u;
+          qg += take ? G * G : 0u;
+          qb += take ? B * B : 0u;
+        }
+      }
+    }
+    vs += kSweep;
+    if (vs >= t.end) break;
+    load_sweep(src, vs, t.end, v);
+  }
+
+  uint32_t f[7] = {gc >> 16, rb >> 16, gc & 0xFFFF, rb & 0xFFFF, qr, qg, qb};
+#pragma unroll
+  for (int k = 0; k < kNF; ++k) f[k] = wave_sum_u32(f[k]);
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < kNF; ++k) red[wave_id()][k] = f[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < (uint32_t)kNF) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+    atomicAdd((unsigned long long*)acc_shard(a, set, nd.shard_base + (int)(t.local % (uint32_t)nd.nshard)) +
+                  threadIdx.x,
+              (unsigned long long)s);
+    if (KIND == PASS_KLAST && threadIdx.x == 0) a.tile_cnt[blockIdx.x] = (uint32_t)s;
   }
 }
 
 // ---------------------------------------------------------------------------
-// Per-node FP64 epilogue.  One workgroup per node: reduce the node's tile
-// partials in u64, then lane 0 applies the reference's update.
-template <int KIND>
-__global__ __launch_bounds__(kBlock) void epilogue_kernel(
-    DevNode* __restrict__ nodes, Tile* __restrict__ tiles,
-    const TilePartial* __restrict__ parts, double s) {
-  DevNode* nd = nodes + blockIdx.x;
-  const int tb = nd->tile_begin, te = nd->tile_end;
-  constexpr int kF = (KIND == PASS_INIT || KIND == PASS_KLAST) ? 7 : 4;
-  uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int i = tb + (int)threadIdx.x; i < te; i += kBlock) {
-    const uint64_t* p = reinterpret_cast<const uint64_t*>(parts + i);
-#pragma unroll
-    for (int f = 0; f < kF; ++f) acc[f] += p[f];
-  }
-  __shared__ uint64_t red[kBlock / 64][8];
-  __shared__ uint32_t scan[kBlock];
-#pragma unroll
-  for (int f = 0; f < kF; ++f) acc[f] = wave_sum_u64(acc[f]);
-  if (lane_id() == 0) {
-#pragma unroll
-    for (int f = 0; f < kF; ++f) red[wave_id()][f] = acc[f];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t tot[7] = {0, 0, 0, 0, 0, 0, 0};
-    for (int w = 0; w < kBlock / 64; ++w)
-      for (int f = 0; f < kF; ++f) tot[f] += red[w][f];
-    const uint64_t cnt = tot[0];
-    const uint64_t sum[3] = {tot[1], tot[2], tot[3]};
-    if (KIND == PASS_INIT) {
-      // DivQuantClusterInitMeanAndVar (:90-104), then the cut (:388-403).
-      for (int a = 0; a < 3; ++a) {
-        double m = (double)sum[a];
-        double v = (double)tot[4 + a];
-        m *= s;
-        v *= s;
-        v -= m * m;
-        nd->tm[a] = m;
-        nd->tv[a] = v;
-      }
-      double maxv = nd->tv[0];
-      int axis = 0;
-      double cut = nd->tm[0];
-      if (maxv < nd->tv[1]) { maxv = nd->tv[1]; axis = 1; cut = nd->tm[1]; }
-      if (maxv < nd->tv[2]) { axis = 2; cut = nd->tm[2]; }
-      nd->axis = axis;
-      nd->cut = cut;
-    } else if (KIND == PASS_SPLIT || KIND == PASS_KMEANS) {
-      update_means(nd, cnt, sum, s);
-      set_decision(nd);
-    } else {  // PASS_KLAST
-      nd->plhs = nd->lhs;
-      nd->prr = nd->rr;
-      nd->prg = nd->rg;
-      nd->prb = nd->rb;
-      update_means(nd, cnt, sum, s);
-      const double nw = nd->nw, ow = nd->ow, tw = nd->tw;
-      for (int a = 0; a < 3; ++a) {          // (:836-838)
-        double q = (double)tot[4 + a];
-        q *= s;
-        nd->nv[a] = q / nw - nd->nm[a] * nd->nm[a];
-      }
-      for (int a = 0; a < 3; ++a) {          // (:845-855)
-        const double dn = nd->nm[a] - nd->tm[a];
-        const double dox = nd->om[a] - nd->tm[a];
-        nd->ov[a] = ((tw * nd->tv[a] - nw * (nd->nv[a] + dn * dn)) / ow) - dox * dox;
-      }
-      nd->tse_old = ow * (nd->ov[0] + nd->ov[1] + nd->ov[2]);   // (:870-871)
-      nd->tse_new = nw * (nd->nv[0] + nd->nv[1] + nd->nv[2]);
-    }
-  }
-  if (KIND == PASS_KLAST) {
-    // Rank of each tile's first OLD point among the node's old points: an
-    // exclusive scan of the tiles' old counts, chunked per lane.
-    const int T = te - tb;
-    const int chunk = (T + kBlock - 1) / kBlock;
-    const int c0 = tb + (int)threadIdx.x * chunk;
-    const int c1 = min(te, c0 + chunk);
-    uint32_t local = 0;
-    for (int i = c0; i < c1; ++i)
-      local += (tiles[i].end - tiles[i].start) - (uint32_t)parts[i].cnt;
-    scan[threadIdx.x] = local;
-    __syncthreads();
-    for (int o = 1; o < kBlock; o <<= 1) {
-      const uint32_t v = threadIdx.x >= (uint32_t)o ? scan[threadIdx.x - o] : 0u;
-      __syncthreads();
-      scan[threadIdx.x] += v;
-      __syncthreads();
-    }
-    uint32_t run = scan[threadIdx.x] - local;
-    for (int i = c0; i < c1; ++i) {
-      tiles[i].old_base = run;
-      run += (tiles[i].end - tiles[i].start) - (uint32_t)parts[i].cnt;
-    }
-  }
-}
+// Partition.  Prologue: the KLAST sums (set pass-1) give the split's results
+// (:787-871, written to DevNode by the node's first tile), the sums before
+// them (set pass-2) give the KLAST decision, recomputed here bit-identically.
+// Body: OLD points to [off, off+n_old) and NEW points to [off+n_old, off+len)
+// of the child buffer, both in index order.
+__global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
+  const Tile t = a.tiles[blockIdx.x];
+  const DevNode& nd = a.nodes[t.node];
+  const uint32_t* __restrict__ src = nd.src;
+  uint32_t* __restrict__ dst = nd.dst;
 
-// ---------------------------------------------------------------------------
-// Partition sweep: recompute the last 2-means decision (identical inputs ->
-// identical result) and write OLD points to [off, off+n_old) and NEW points to
-// [off+n_old, off+len) of the child buffer, both in index order.
-__global__ __launch_bounds__(kBlock) void partition_kernel(
-    const Tile* __restrict__ tiles, const DevNode* __restrict__ nodes,
-    PixelBufs bufs) {
-  const Tile t = tiles[blockIdx.x];
-  const DevNode* nd = nodes + t.node;
-  const uint32_t* __restrict__ src = src_of(bufs, nd->buf);
-  uint32_t* __restrict__ dst = nd->buf == BUF_P0 ? bufs.p1 : bufs.p0;
-  const double lhs = nd->plhs, rr = nd->prr, rg = nd->prg, rb = nd->prb;
-  const uint32_t n_old = nd->len - (uint32_t)nd->n_new;
-  uint32_t old_cur = nd->off + t.old_base;
-  uint32_t new_cur = nd->off + n_old + ((t.start - nd->off) - t.old_base);
-
-  __shared__ uint32_t cnt[2][kPxPerThread * (kBlock / 64)];
+  __shared__ Params prm;
+  __shared__ uint32_t n_new_s;
+  __shared__ uint32_t pre[kBlock / 64];
+  __shared__ uint32_t cnt[2][kVecPerThread * 4 * (kBlock / 64)];
   __shared__ uint32_t tot[2];
+
+  const uint32_t vs0 = t.start & ~3u;
+  uint4 v[kVecPerThread];
+  load_sweep(src, vs0, t.end, v);
+
+  // Old points in this node's earlier tiles (KLAST wrote each tile's new count).
+  uint32_t older = 0;
+  for (int i = nd.tile_begin + (int)threadIdx.x; i < nd.tile_begin + (int)t.local; i += kBlock) {
+    const Tile& u = a.tiles[i];
+    older += (u.end - u.start) - a.tile_cnt[i];
+  }
+  older = wave_sum_u32(older);
+  if (lane_id() == 0) pre[wave_id()] = older;
+
+  if (wave_id() == 0) {
+    uint64_t tk[F_NUM], tp[F_NUM];
+    reduce_shards(a, nd, (a.pass + kAccSets - 1) % kAccSets, 7, tk);
+    reduce_shards(a, nd, (a.pass + kAccSets - 2) % kAccSets, 4, tp);
+    if (lane_id() == 0) {
+      double om[3], nm[3], nw, ow;
+      means_from_sums(tp, nd.s, nd.tw, nd.tm, om, nm, &nw, &ow);
+      decision_from_means(om, nm, &prm);
+      n_new_s = (uint32_t)tk[F_CNT];
+      if (t.local == 0) {
+        DevNode& w = a.nodes[t.node];
+        w.plhs = prm.lhs; w.prr = prm.rr; w.prg = prm.rg; w.prb = prm.rb;
+        means_from_sums(tk, nd.s, nd.tw, nd.tm, om, nm, &nw, &ow);
+        for (int c = 0; c < 3; ++c) {                  // (:836-838)
+          double qv = (double)tk[F_QR + c];
+          qv *= nd.s;
+          w.nv[c] = qv / nw - nm[c] * nm[c];
+        }
+        for (int c = 0; c < 3; ++c) {                  // (:845-855)
+          const double dn = nm[c] - nd.tm[c];
+          const double dox = om[c] - nd.tm[c];
+          w.ov[c] = ((nd.tw * nd.tv[c] - nw * (w.nv[c] + dn * dn)) / ow) - dox * dox;
+        }
+        w.tse_old = ow * (w.ov[0] + w.ov[1] + w.ov[2]);   // (:870-871)
+        w.tse_new = nw * (w.nv[0] + w.nv[1] + w.nv[2]);
+        for (int c = 0; c < 3; ++c) { w.om[c] = om[c]; w.nm[c] = nm[c]; }
+        w.nw = nw;
+        w.ow = ow;
+        w.n_new = tk[F_CNT];
+      }
+    }
+  }
+  __syncthreads();
+  const Params q = prm;
+  const uint32_t old_base = pre[0] + pre[1] + pre[2] + pre[3];
+  const uint32_t n_old = nd.len - n_new_s;
+  uint32_t old_cur = nd.off + old_base;
+  uint32_t new_cur = nd.off + n_old + ((t.start - nd.off) - old_base);
+
   const uint32_t w = wave_id(), l = lane_id();
-  for (uint32_t base = t.start; base < t.end; base += kSweep) {
-    uint32_t px[kPxPerThread];
-    uint32_t slot[kPxPerThread];   // bit 31: old, bit 30: new; low bits: rank in wave
+  constexpr int kSlots = kVecPerThread * 4;
+  for (uint32_t vs = vs0;;) {
+    uint32_t slot[kSlots];   // bit 31: old, bit 30: new; low bits: rank in wave
 #pragma unroll
-    for (int j = 0; j < kPxPerThread; ++j) {
-      const uint32_t i = base + j * kBlock + threadIdx.x;
-      const bool ok = i < t.end;
-      px[j] = src[ok ? i : t.start];
-      const bool old = ok && stays_old(px[j], lhs, rr, rg, rb);
-      const bool nw = ok && !old;
-      const uint64_t mo = __ballot(old), mn = __ballot(nw);
-      slot[j] = old ? (0x80000000u | mbcnt64(mo)) : (nw ? (0x40000000u | mbcnt64(mn)) : 0u);
-      if (l == 0) {
-        cnt[0][j * (kBlock / 64) + w] = (uint32_t)__popcll(mo);
-        cnt[1][j * (kBlock / 64) + w] = (uint32_t)__popcll(mn);
+    for (int j = 0; j < kVecPerThread; ++j) {
+      const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t p = vec_elem(v[j], e);
+        const uint32_t i = i0 + e;
+        const bool valid = (i >= t.start) & (i < t.end);
+        const bool old = valid && stays_old(p, q);
+        const bool nw = valid && !old;
+        const uint64_t mo = __ballot(old), mn = __ballot(nw);
+        const int sidx = j * 4 + e;
+        slot[sidx] = old ? (0x80000000u | mbcnt64(mo)) : (nw ? (0x40000000u | mbcnt64(mn)) : 0u);
+        if (l == 0) {
+          cnt[0][sidx * (kBlock / 64) + w] = (uint32_t)__popcll(mo);
+          cnt[1][sidx * (kBlock / 64) + w] = (uint32_t)__popcll(mn);
+        }
       }
     }
     __syncthreads();
-    if (w < 2) {   // wave 0 scans the old counts, wave 1 the new counts (64 entries)
-      const uint32_t v = cnt[w][l];
-      uint32_t inc = v;
+    // Points of a sweep are ranked in (slot, wave, lane) order: an exclusive
+    // scan over the 64 (slot, wave) counts by wave 0 (old) and wave 1 (new).
+    if (w < 2) {
+      const uint32_t val = cnt[w][l];
+      uint32_t inc = val;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t u = __shfl_up(inc, o, 64);
         if (l >= (uint32_t)o) inc += u;
       }
-      cnt[w][l] = inc - v;
+      cnt[w][l] = inc - val;
       if (l == 63) tot[w] = inc;
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kPxPerThread; ++j) {
-      const uint32_t sl = slot[j];
+    for (int sidx = 0; sidx < kSlots; ++sidx) {
+      const uint32_t sl = slot[sidx];
       const uint32_t r = sl & 0x3FFFFFFFu;
-      if (sl & 0x80000000u) dst[old_cur + cnt[0][j * (kBlock / 64) + w] + r] = px[j];
-      else if (sl & 0x40000000u) dst[new_cur + cnt[1][j * (kBlock / 64) + w] + r] = px[j];
+      const uint32_t p = vec_elem(v[sidx >> 2], sidx & 3);
+      if (sl & 0x80000000u) dst[old_cur + cnt[0][sidx * (kBlock / 64) + w] + r] = p;
+      else if (sl & 0x40000000u) dst[new_cur + cnt[1][sidx * (kBlock / 64) + w] + r] = p;
     }
     old_cur += tot[0];
     new_cur += tot[1];
+    vs += kSweep;
+    if (vs >= t.end) break;
     __syncthreads();
+    load_sweep(src, vs, t.end, v);
   }
 }
 
@@ -348,9 +429,12 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(
 // Map, step 1: per colour cell (8x8x8 values), the palette entries whose
 // minimum distance to the cell does not exceed the smallest maximum distance
 // of any entry to the cell.  Every exact argmin for a colour of the cell is
-// among them (ties included: <=).  One wave per cell.
+// among them (ties included: <=).  One wave per cell.  Record (16 B):
+//   x[15:0] count c; c <= 7: entries in x[31:16], y, z, w (u16 halves);
+//   7 < c <= kCellCap: entries in cell_idx[cell*kCellCap ...];
+//   c == kCellBrute: scan the whole palette.
 __global__ __launch_bounds__(kBlock) void build_cells_kernel(
-    const uint32_t* __restrict__ pal, int k, uint16_t* __restrict__ cell_cnt,
+    const uint32_t* __restrict__ pal, int k, uint4* __restrict__ cell_rec,
     uint16_t* __restrict__ cell_idx) {
   extern __shared__ uint32_t spal[];
   for (int i = threadIdx.x; i < k; i += kBlock) spal[i] = pal[i];
@@ -363,15 +447,15 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(
   lo[0] = (cell >> (2 * kCellBits)) * cw;
   lo[1] = ((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
   lo[2] = (cell & ((1 << kCellBits) - 1)) * cw;
-  for (int a = 0; a < 3; ++a) hi[a] = lo[a] + cw - 1;
+  for (int c = 0; c < 3; ++c) hi[c] = lo[c] + cw - 1;
 
   uint32_t bound = 0xFFFFFFFFu;
   for (int e = lane; e < k; e += 64) {
     const uint32_t q = spal[e];
-    const int v[3] = {(int)((q >> 16) & 0xFF), (int)((q >> 8) & 0xFF), (int)(q & 0xFF)};
+    const int vv[3] = {(int)((q >> 16) & 0xFF), (int)((q >> 8) & 0xFF), (int)(q & 0xFF)};
     uint32_t d = 0;
-    for (int a = 0; a < 3; ++a) {
-      const int x = max(v[a] - lo[a], hi[a] - v[a]);
+    for (int c = 0; c < 3; ++c) {
+      const int x = max(vv[c] - lo[c], hi[c] - vv[c]);
       d += (uint32_t)(x * x);
     }
     bound = min(bound, d);
@@ -380,27 +464,43 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(
   for (int o = 32; o >= 1; o >>= 1) bound = min(bound, (uint32_t)__shfl_xor(bound, o, 64));
 
   uint32_t count = 0;
+  uint32_t inl[kCellInline];
+  for (int c = 0; c < kCellInline; ++c) inl[c] = 0;
   for (int b = 0; b < k; b += 64) {
     const int e = b + lane;
     bool cand = false;
     if (e < k) {
       const uint32_t q = spal[e];
-      const int v[3] = {(int)((q >> 16) & 0xFF), (int)((q >> 8) & 0xFF), (int)(q & 0xFF)};
+      const int vv[3] = {(int)((q >> 16) & 0xFF), (int)((q >> 8) & 0xFF), (int)(q & 0xFF)};
       uint32_t d = 0;
-      for (int a = 0; a < 3; ++a) {
-        const int x = v[a] < lo[a] ? lo[a] - v[a] : (v[a] > hi[a] ? v[a] - hi[a] : 0);
+      for (int c = 0; c < 3; ++c) {
+        const int x = vv[c] < lo[c] ? lo[c] - vv[c] : (vv[c] > hi[c] ? vv[c] - hi[c] : 0);
         d += (uint32_t)(x * x);
       }
       cand = d <= bound;
     }
-    const uint64_t m = __ballot(cand);
+    uint64_t m = __ballot(cand);
     if (cand) {
       const uint32_t pos = count + mbcnt64(m);
       if (pos < (uint32_t)kCellCap) cell_idx[(size_t)cell * kCellCap + pos] = (uint16_t)e;
     }
-    count += (uint32_t)__popcll(m);
+    // first kCellInline candidates, known to every lane
+    while (m) {
+      const int bit = __builtin_ctzll(m);
+      if (count < (uint32_t)kCellInline) inl[count] = (uint32_t)(b + bit);
+      ++count;
+      m &= m - 1;
+    }
   }
-  if (lane == 0) cell_cnt[cell] = count > (uint32_t)kCellCap ? kCellOverflow : (uint16_t)count;
+  if (lane == 0) {
+    uint4 r;
+    const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
+    r.x = c | (inl[0] << 16);
+    r.y = inl[1] | (inl[2] << 16);
+    r.z = inl[3] | (inl[4] << 16);
+    r.w = inl[5] | (inl[6] << 16);
+    cell_rec[cell] = r;
+  }
 }
 
 // Map, step 2.  Key = (squared distance, MPS visit rank) where the walk
@@ -412,7 +512,7 @@ template <bool kWide>
 __global__ __launch_bounds__(kBlock) void map_kernel(
     const uint32_t* __restrict__ in, uint32_t n, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ pal, int k, const uint16_t* __restrict__ lut,
-    const uint16_t* __restrict__ cell_cnt, const uint16_t* __restrict__ cell_idx) {
+    const uint4* __restrict__ cell_rec, const uint16_t* __restrict__ cell_idx) {
   extern __shared__ uint32_t smem[];
   uint32_t* spal = smem;
   uint16_t* slut = reinterpret_cast<uint16_t*>(smem + k);
@@ -421,15 +521,15 @@ __global__ __launch_bounds__(kBlock) void map_kernel(
   __syncthreads();
   using Key = typename std::conditional<kWide, uint64_t, uint32_t>::type;
   constexpr int kRankBits = kWide ? 32 : 11;
-  const uint32_t stride = gridDim.x * kBlock;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
-    const uint32_t p = in[i];
+
+  auto map_one = [&](uint32_t p) -> uint32_t {
     const int R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
     const int s0 = slut[R + G + B];
     const uint32_t cell = ((uint32_t)(R >> (8 - kCellBits)) << (2 * kCellBits)) |
                           ((uint32_t)(G >> (8 - kCellBits)) << kCellBits) |
                           (uint32_t)(B >> (8 - kCellBits));
-    const uint32_t cc = cell_cnt[cell];
+    const uint4 rec = cell_rec[cell];
+    const uint32_t cc = rec.x & 0xFFFF;
     Key best = (Key)~(Key)0;
     auto eval = [&](int j) {
       const uint32_t q = spal[j];
@@ -442,71 +542,78 @@ __global__ __launch_bounds__(kBlock) void map_kernel(
       const Key key = ((Key)d << kRankBits) | (Key)rank;
       best = key < best ? key : best;
     };
-    if (cc == kCellOverflow) {
-      for (int j = 0; j < k; ++j) eval(j);
-    } else {
+    if (cc <= (uint32_t)kCellInline) {
+      const uint32_t e[kCellInline] = {rec.x >> 16, rec.y & 0xFFFF, rec.y >> 16, rec.z & 0xFFFF,
+                                       rec.z >> 16, rec.w & 0xFFFF, rec.w >> 16};
+#pragma unroll
+      for (int m = 0; m < kCellInline; ++m)
+        if ((uint32_t)m < cc) eval((int)e[m]);
+    } else if (cc != kCellBrute) {
       const uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
       for (uint32_t m = 0; m < cc; ++m) eval(lst[m]);
+    } else {
+      for (int j = 0; j < k; ++j) eval(j);
     }
     const uint32_t rank = (uint32_t)(best & (((Key)1 << kRankBits) - 1));
     const int j = (rank & 1) ? s0 + (int)((rank + 1) >> 1) : s0 - (int)(rank >> 1);
-    out[i] = spal[j];
+    return spal[j];
+  };
+
+  const uint32_t nvec = n / 4;
+  const uint32_t stride = gridDim.x * kBlock;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride) {
+    const uint4 p = reinterpret_cast<const uint4*>(in)[i];
+    uint4 o;
+    o.x = map_one(p.x);
+    o.y = map_one(p.y);
+    o.z = map_one(p.z);
+    o.w = map_one(p.w);
+    reinterpret_cast<uint4*>(out)[i] = o;
   }
+  const uint32_t tail = nvec * 4 + blockIdx.x * kBlock + threadIdx.x;
+  if (blockIdx.x == 0 && tail < n) out[tail] = map_one(in[tail]);
 }
 
 // ---------------------------------------------------------------------------
 // Launchers.
-void launch_pass(int kind, const Tile* tiles, int ntiles, const DevNode* nodes,
-                 PixelBufs bufs, TilePartial* parts, hipStream_t stream) {
+void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) {
   if (ntiles <= 0) return;
   const dim3 g(ntiles), b(kBlock);
   switch (kind) {
-    case PASS_INIT: pass_kernel<PASS_INIT><<<g, b, 0, stream>>>(tiles, nodes, bufs, parts); break;
-    case PASS_SPLIT: pass_kernel<PASS_SPLIT><<<g, b, 0, stream>>>(tiles, nodes, bufs, parts); break;
-    case PASS_KMEANS: pass_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(tiles, nodes, bufs, parts); break;
-    default: pass_kernel<PASS_KLAST><<<g, b, 0, stream>>>(tiles, nodes, bufs, parts); break;
+    case PASS_INIT: pass_kernel<PASS_INIT><<<g, b, 0, stream>>>(a); break;
+    case PASS_SPLIT: pass_kernel<PASS_SPLIT><<<g, b, 0, stream>>>(a); break;
+    case PASS_KMEANS: pass_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a); break;
+    default: pass_kernel<PASS_KLAST><<<g, b, 0, stream>>>(a); break;
   }
 }
 
-void launch_epilogue(int kind, DevNode* nodes, int nnodes, Tile* tiles,
-                     const TilePartial* parts, double s, hipStream_t stream) {
-  if (nnodes <= 0) return;
-  const dim3 g(nnodes), b(kBlock);
-  switch (kind) {
-    case PASS_INIT: epilogue_kernel<PASS_INIT><<<g, b, 0, stream>>>(nodes, tiles, parts, s); break;
-    case PASS_SPLIT: epilogue_kernel<PASS_SPLIT><<<g, b, 0, stream>>>(nodes, tiles, parts, s); break;
-    case PASS_KMEANS: epilogue_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(nodes, tiles, parts, s); break;
-    default: epilogue_kernel<PASS_KLAST><<<g, b, 0, stream>>>(nodes, tiles, parts, s); break;
-  }
-}
-
-void launch_partition(const Tile* tiles, int ntiles, const DevNode* nodes,
-                      PixelBufs bufs, hipStream_t stream) {
+void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream) {
   if (ntiles <= 0) return;
-  partition_kernel<<<dim3(ntiles), dim3(kBlock), 0, stream>>>(tiles, nodes, bufs);
+  partition_kernel<<<dim3(ntiles), dim3(kBlock), 0, stream>>>(a);
 }
 
-void launch_build_cells(const uint32_t* pal_sorted, int k, uint16_t* cell_cnt,
+void launch_build_cells(const uint32_t* pal_sorted, int k, uint4* cell_rec,
                         uint16_t* cell_idx, hipStream_t stream) {
   const int blocks = kCells / (kBlock / 64);
   build_cells_kernel<<<dim3(blocks), dim3(kBlock), (size_t)k * 4, stream>>>(
-      pal_sorted, k, cell_cnt, cell_idx);
+      pal_sorted, k, cell_rec, cell_idx);
 }
 
 void launch_map(const uint32_t* in, uint32_t n, uint32_t* out,
                 const uint32_t* pal_sorted, int k, const uint16_t* lut_init,
-                const uint16_t* cell_cnt, const uint16_t* cell_idx,
+                const uint4* cell_rec, const uint16_t* cell_idx,
                 hipStream_t stream) {
   if (n == 0) return;
   const size_t lds = (size_t)k * 4 + 768 * 2;
-  uint32_t blocks = (n + kBlock - 1) / kBlock;
-  if (blocks > 4096) blocks = 4096;
+  uint32_t blocks = (n / 4 + kBlock - 1) / kBlock;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks == 0) blocks = 1;
   if (k <= 1024)
     map_kernel<false><<<dim3(blocks), dim3(kBlock), lds, stream>>>(
-        in, n, out, pal_sorted, k, lut_init, cell_cnt, cell_idx);
+        in, n, out, pal_sorted, k, lut_init, cell_rec, cell_idx);
   else
     map_kernel<true><<<dim3(blocks), dim3(kBlock), lds, stream>>>(
-        in, n, out, pal_sorted, k, lut_init, cell_cnt, cell_idx);
+        in, n, out, pal_sorted, k, lut_init, cell_rec, cell_idx);
 }
 
 }  // namespace dq

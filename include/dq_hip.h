@@ -43,6 +43,14 @@ int dq_hip_map(const uint32_t *in, uint32_t n, uint32_t *out,
 int dq_hip_quant_dev(int device, const uint32_t *d_in, uint32_t n,
                      uint32_t *d_out, uint32_t *k, uint32_t *ct,
                      int max_iters, void *stream);
+/* A batch of frames in one call: every pass of every split round is one
+ * kernel launch over the points of all frames.  d_in/d_out/n: nframes
+ * entries; ct: nframes*k host words (frame i at ct + i*k); k_out[i] = its
+ * colour count.  Returns the total number of empty clusters or < 0. */
+int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t *const *d_in,
+                           const uint32_t *n, uint32_t *const *d_out, uint32_t k,
+                           uint32_t *ct, uint32_t *k_out, int max_iters,
+                           void *stream);
 /* Clustering only (quant_varpart_fast, DivQuantCluster.cpp:1099-1179):
  * writes the non-empty cluster colours (cluster-index order, NOT deduped). */
 int dq_hip_cluster_dev(int device, const uint32_t *d_in, uint32_t n,
