@@ -146,7 +146,7 @@ void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nshards) {
   if (nshards > cap_shards_ || !d_acc_) {
     size_t c = std::max<size_t>(nshards, 4096);
     if (d_acc_) DQ_HIP(hipFree(d_acc_));
-    DQ_HIP(hipMalloc((void**)&d_acc_, (size_t)kAccSets * c * kAccStride * sizeof(uint64_t)));
+    DQ_HIP(hipMalloc((void**)&d_acc_, c * kAccStride * sizeof(uint64_t)));
     cap_shards_ = c;
   }
 }
@@ -185,16 +185,19 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
     d.dst = (child_buf(n.buf) == BUF_P0 ? d_p0_ : d_p1_) + fs.base;
     d.off = n.off;
     d.len = n.len;
-    d.root = root_round ? 1 : 0;
     d.s = fs.s;
     d.tw = n.w;
     for (int c = 0; c < 3; ++c) { d.tm[c] = n.mean[c]; d.tv[c] = n.var[c]; }
-    // Cut axis/position (:388-403): comparisons and copies only.
-    double maxv = n.var[0], cut = n.mean[0];
-    d.axis = 0;
-    if (maxv < n.var[1]) { maxv = n.var[1]; d.axis = 1; cut = n.mean[1]; }
-    if (maxv < n.var[2]) { d.axis = 2; cut = n.mean[2]; }
-    d.thr = split_threshold(cut);
+    if (!root_round) {
+      // Cut axis/position (:388-403): comparisons and copies only.  (The
+      // root's come from its PASS_INIT on the device.)
+      double maxv = n.var[0], cut = n.mean[0];
+      int axis = 0;
+      if (maxv < n.var[1]) { maxv = n.var[1]; axis = 1; cut = n.mean[1]; }
+      if (maxv < n.var[2]) { axis = 2; cut = n.mean[2]; }
+      d.prm.thr = split_threshold(cut);
+      d.prm.shift = 16 - 8 * axis;
+    }
     d.tile_begin = t;
     uint32_t local = 0;
     for (uint64_t o = 0; o == 0 || o < n.len; o += tl) {
@@ -211,17 +214,14 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
   }
   DQ_HIP(hipMemcpyAsync(d_nodes_, h_nodes_, nn * sizeof(DevNode), hipMemcpyHostToDevice, stream));
   DQ_HIP(hipMemcpyAsync(d_tiles_, h_tiles_, ntiles * sizeof(Tile), hipMemcpyHostToDevice, stream));
-  // All sets start at zero; from then on every pass zeroes the set of the
-  // pass after it (whose previous contents were read two passes ago).
-  DQ_HIP(hipMemsetAsync(d_acc_, 0, (size_t)kAccSets * sh * kAccStride * sizeof(uint64_t), stream));
+  // Sums and tickets start at zero; each node's last arriver re-zeroes them.
+  DQ_HIP(hipMemsetAsync(d_acc_, 0, (size_t)sh * kAccStride * sizeof(uint64_t), stream));
 
   RoundArgs ra;
   ra.tiles = d_tiles_;
   ra.nodes = d_nodes_;
   ra.acc = d_acc_;
   ra.tile_cnt = d_tile_cnt_;
-  ra.total_shards = sh;
-  ra.pass = 0;
   const double bytes = 4.0 * (double)total;
   const int nt = (int)ntiles;
   auto pass = [&](int kind, int st) {
@@ -229,7 +229,6 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
     launch_pass(kind, ra, nt, stream);
     timed_end(st, bytes, stream);
     last_points_swept += total;
-    ra.pass++;
   };
   if (root_round) pass(PASS_INIT, ST_INIT);
   pass(PASS_SPLIT, ST_SPLIT);

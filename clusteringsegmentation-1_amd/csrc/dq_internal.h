@@ -25,12 +25,23 @@ enum PassKind : int32_t {
   PASS_KLAST = 3,    // last 2-means iteration: also sums of squares (:726-748)
 };
 
-// Statistics of one accumulator shard: exact integer sums of the new side
-// (all points in PASS_INIT).  One 128-B line per shard.
-enum AccField : int32_t { F_CNT = 0, F_SR, F_SG, F_SB, F_QR, F_QG, F_QB, F_NUM };
+// Accumulator shard: exact integer sums of the new side (all points in
+// PASS_INIT) of the tiles with local % nshard == shard, plus arrival tickets.
+// One 128-B line per shard; every access is a device-scope atomic, so the
+// values live at the memory side and never depend on cache state.
+enum AccField : int32_t { F_CNT = 0, F_SR, F_SG, F_SB, F_QR, F_QG, F_QB, F_NUM,
+                          F_TICKET = 8,        // tiles of this shard that arrived
+                          F_NODE_TICKET = 9 }; // (shard 0 only) shards that arrived
 constexpr int kAccStride = 16;          // u64 per shard (128 B)
-constexpr int kAccSets = 3;             // pass p writes set p%3, reads (p-1)%3, zeroes (p+1)%3
 constexpr int kMaxShards = 64;          // shards per node (one per lane of wave 0)
+
+// Decision parameters of one pass for one node (:616-623, :683).
+struct alignas(16) Params {
+  double lhs, rr, rg, rb;          // exact FP64 decision
+  float lhsf, rrf, rgf, rbf, eps;  // FP32 pre-filter (dq_kernels.hip, stays_old)
+  int32_t thr, shift;              // split pass: new iff ((p >> shift) & 0xFF) >= thr
+  int32_t pad;
+};
 
 // Per-node state for one round.
 struct alignas(16) DevNode {
@@ -42,15 +53,14 @@ struct alignas(16) DevNode {
   int32_t tile_end;
   int32_t shard_base;       // accumulator shards [shard_base, shard_base+nshard)
   int32_t nshard;
-  int32_t root;             // 1: tm/tv/axis/cut come from the device INIT pass
-  int32_t thr;              // split pass: new iff v_axis >= thr  (== cut_pos < v)
-  int32_t axis;             // split pass: cut axis (0=R,1=G,2=B) (:388-403)
-  int32_t pad0;
   double s;                 // data_weight of the frame (get_double_scale)
   double tw;                // total_weight = weight[old_index]  (:353)
-  double tm[3], tv[3];      // total_mean / total_var           (:357-374)
-  // --- results of the node's split (written by the partition kernel)
-  double plhs, prr, prg, prb;   // decision of the last 2-means pass
+  double tm[3], tv[3];      // total_mean / total_var (root: written by PASS_INIT)
+  // --- parameters of the next pass (host for the split pass of non-roots,
+  //     otherwise written by the node's last-arriving workgroup)
+  Params prm;
+  // --- results of the node's split (written by the last arriver of PASS_KLAST;
+  //     prm then still holds the last 2-means decision)
   double om[3], nm[3];      // old_mean / new_mean after the last pass
   double nv[3], ov[3];      // new_var / old_var (:836-855)
   double nw, ow;            // new_weight / old_weight

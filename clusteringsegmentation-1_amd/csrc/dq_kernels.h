@@ -22,20 +22,17 @@ constexpr int kCellInline = 7;                  // candidates stored in the 16-B
 constexpr int kCellCap = 32;                    // candidates in the overflow list
 constexpr uint32_t kCellBrute = 0xFFFF;         // count marker: scan the whole palette
 
-// Accumulator sets for one round: kAccSets x total_shards x kAccStride u64.
+// Tables of one round (device pointers).
 struct RoundArgs {
   const Tile* tiles;
   DevNode* nodes;
-  uint64_t* acc;
+  uint64_t* acc;            // total_shards x kAccStride u64, zero between passes
   uint32_t* tile_cnt;       // PASS_KLAST: new-side count per tile
-  int32_t total_shards;
-  int32_t pass;             // pass index inside the round (selects the sets)
 };
 
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
-// Reduces the last two passes' sums per node, writes the split results into
-// DevNode, and writes every node's points into its two children's segments
-// (old half first, then new half), in index order, in the child buffer.
+// Writes every node's points into its two children's segments (old half
+// first, then new half) of the child buffer, using the last 2-means decision.
 void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream);
 
 // Map: candidate records per colour cell, then the per-pixel argmin over

@@ -9,15 +9,15 @@
 //   pass_kernel<KIND>  one sweep over the tiles of every node being split
 //                      (all frames of the batch): per-point decision + exact
 //                      integer new-side sums (split pass :438-559, 2-means
-//                      pass :613-811, root statistics :49-104).  The FP64
-//                      update of the PREVIOUS pass (:561-598, :787-810) runs
-//                      in each workgroup's prologue from the sharded u64
-//                      sums, so a pass is one launch and needs no epilogue
-//                      kernel.  HBM/MALL-bound: 4 B read per point.
-//   partition_kernel   final FP64 update of the split (:787-871) and the
-//                      write of each node's points into its two children's
-//                      segments in index order (replaces the per-split O(N)
-//                      member[] gather, :894-1026).
+//                      pass :613-811, root statistics :49-104).  The node's
+//                      LAST-ARRIVING workgroup runs the reference's FP64
+//                      update (:561-598, :787-871) once and publishes the
+//                      next pass's decision in DevNode, so a pass is one
+//                      launch with no epilogue kernel and no per-workgroup
+//                      prologue.  HBM/MALL-bound: 4 B read per point.
+//   partition_kernel   writes each node's points into its two children's
+//                      segments (replaces the per-split O(N) member[]
+//                      gather, :894-1026).
 //   build_cells_kernel map: per 8x8x8 colour cell, the palette entries that
 //                      can be nearest to some colour of the cell.
 //   map_kernel         map: per pixel argmin over (squared distance, MPS
@@ -53,29 +53,27 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
-__device__ __forceinline__ uint64_t* acc_shard(const RoundArgs& a, int set, int shard) {
-  return a.acc + ((size_t)set * a.total_shards + shard) * kAccStride;
+__device__ __forceinline__ uint64_t* acc_shard(const RoundArgs& a, int shard) {
+  return a.acc + (size_t)shard * kAccStride;
 }
 
-// Wave-level sum of the first nf fields of a node's shards in `set`
-// (lane i reads shard i).  Valid in every lane of the calling wave.
-__device__ __forceinline__ void reduce_shards(const RoundArgs& a, const DevNode& nd, int set,
-                                              int nf, uint64_t t[F_NUM]) {
-  const int l = (int)lane_id();
-  const uint64_t* p = l < nd.nshard ? acc_shard(a, set, nd.shard_base + l) : nullptr;
-  for (int f = 0; f < F_NUM; ++f) {
-    uint64_t v = 0;
-    if (f < nf && p) v = __builtin_nontemporal_load(p + f);
-    t[f] = f < nf ? wave_sum_u64(v) : 0;
-  }
+// All accumulator / ticket traffic is device-scope atomic: it is performed at
+// the memory side, so it is coherent across the 8 XCDs whatever the caches hold.
+__device__ __forceinline__ uint64_t atomic_take(uint64_t* p) {   // read and reset
+  return __hip_atomic_exchange(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
-// Decision parameters of one pass, broadcast through LDS.
-struct Params {
-  double lhs, rr, rg, rb;   // exact FP64 decision (:616-623, :683)
-  float lhsf, rrf, rgf, rbf, eps;   // FP32 pre-filter (see stays_old)
-  int32_t thr, shift;       // split pass
-};
+__device__ __forceinline__ uint64_t atomic_inc(uint64_t* p) {    // returns the old value
+  return __hip_atomic_fetch_add(p, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void atomic_add(uint64_t* p, uint64_t v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Orders this wave's earlier atomics before its later ones at agent scope
+// (explicit vmcnt(0) after the fence: MI355X_MICROARCH.md, compiler hazard).
+__device__ __forceinline__ void release_agent() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // (:561-598 / :787-810) means and weights of both halves from the new side's
 // exact integer sums.  cnt/sums are exact in double (all < 2^53).
@@ -96,10 +94,10 @@ __device__ __forceinline__ void means_from_sums(const uint64_t t[F_NUM], double 
 
 // (:616-623) + the FP32 filter bound.  The filter evaluates
 //   df = rr*R + rg*G + rb*B - lhs   in f32 (3 fma).
-// With M = (|rr|+|rg|+|rb|)*255 + |lhs|, its error is below 6*2^-24*M
-// (three f32 conversions, three f32 roundings) and the FP64 sum's error is
-// below 3*2^-53*M, so whenever |df| > eps = 8e-7*M the sign of df equals the
-// sign of the FP64 expression's (lhs < sum) outcome.  Non-finite or tiny M
+// With M = (|rr|+|rg|+|rb|)*255 + |lhs|, its error is below 7*2^-24*M (four
+// f32 conversions, three f32 roundings) and the FP64 sum's error is below
+// 4*2^-53*M, so whenever |df| > eps = 8e-7*M the sign of df equals the sign
+// of the FP64 expression's (lhs < sum) outcome.  Non-finite or tiny M
 // (NaN/inf means of an empty half) disables the filter: eps = +inf.
 __device__ __forceinline__ void decision_from_means(const double om[3], const double nm[3],
                                                     Params* p) {
@@ -173,78 +171,94 @@ __device__ __forceinline__ uint32_t vec_elem(const uint4& v, int e) {
   return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
 }
 
+// The FP64 update a node's last arriver runs after pass KIND, from the
+// node's total sums t[] (exact integers).  Publishes the next pass's Params
+// (or, after PASS_KLAST, the split's results) in DevNode.
+template <int KIND>
+__device__ void node_update(DevNode* w, const uint64_t t[F_NUM]) {
+  const double s = w->s, tw = w->tw;
+  if (KIND == PASS_INIT) {
+    // DivQuantClusterInitMeanAndVar (:90-104), then the cut (:388-403).
+    double tm[3], tv[3];
+    for (int c = 0; c < 3; ++c) {
+      double m = (double)t[F_SR + c];
+      double q = (double)t[F_QR + c];
+      m *= s;
+      q *= s;
+      q -= m * m;
+      tm[c] = m;
+      tv[c] = q;
+      w->tm[c] = m;
+      w->tv[c] = q;
+    }
+    double maxv = tv[0], cut = tm[0];
+    int axis = 0;
+    if (maxv < tv[1]) { maxv = tv[1]; axis = 1; cut = tm[1]; }
+    if (maxv < tv[2]) { axis = 2; cut = tm[2]; }
+    w->prm.thr = split_threshold(cut);
+    w->prm.shift = 16 - 8 * axis;
+    return;
+  }
+  double tm[3];
+  for (int c = 0; c < 3; ++c) tm[c] = w->tm[c];
+  double om[3], nm[3], nw, ow;
+  means_from_sums(t, s, tw, tm, om, nm, &nw, &ow);
+  if (KIND == PASS_SPLIT || KIND == PASS_KMEANS) {
+    Params p = w->prm;
+    decision_from_means(om, nm, &p);
+    w->prm = p;
+    return;
+  }
+  // PASS_KLAST: the split's results (:787-871).  prm keeps the last decision
+  // (the partition replays it).
+  double nv[3], ov[3];
+  for (int c = 0; c < 3; ++c) {                  // (:836-838)
+    double q = (double)t[F_QR + c];
+    q *= s;
+    nv[c] = q / nw - nm[c] * nm[c];
+  }
+  for (int c = 0; c < 3; ++c) {                  // (:845-855)
+    const double dn = nm[c] - tm[c];
+    const double dox = om[c] - tm[c];
+    ov[c] = ((tw * w->tv[c] - nw * (nv[c] + dn * dn)) / ow) - dox * dox;
+  }
+  for (int c = 0; c < 3; ++c) {
+    w->om[c] = om[c];
+    w->nm[c] = nm[c];
+    w->nv[c] = nv[c];
+    w->ov[c] = ov[c];
+  }
+  w->nw = nw;
+  w->ow = ow;
+  w->tse_old = ow * (ov[0] + ov[1] + ov[2]);   // (:870-871)
+  w->tse_new = nw * (nv[0] + nv[1] + nv[2]);
+  w->n_new = t[F_CNT];
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
 // Statistics pass.  One workgroup per tile; a tile lies inside one node's
 // segment, so every point of the workgroup shares the node's parameters and
 // the sums need no per-point binning: packed lane partials -> wave sums ->
-// LDS -> ONE u64 atomic add per field into the node's shard (local % nshard).
+// LDS -> one u64 atomic add per field into the node's shard (local % nshard).
+// Then two-level arrival tickets (shard, then node) elect the node's last
+// workgroup, which takes (reads and zeroes) the node's sums and runs
+// node_update<KIND>.
 template <int KIND>
 __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const DevNode& nd = a.nodes[t.node];
   const uint32_t* __restrict__ src = nd.src;
-  const int set = a.pass % kAccSets;
   constexpr bool kSquares = (KIND == PASS_INIT || KIND == PASS_KLAST);
   constexpr int kNF = kSquares ? 7 : 4;
 
-  __shared__ Params prm;
   __shared__ uint32_t red[kBlock / 64][8];
 
-  // Issue the first sweep's loads before the prologue so they overlap it.
   const uint32_t vs0 = t.start & ~3u;
   uint4 v[kVecPerThread];
   load_sweep(src, vs0, t.end, v);
-
-  if (wave_id() == 0) {
-    // Zero this shard of the set the NEXT pass accumulates into.
-    if (t.local < (uint32_t)nd.nshard && lane_id() < kAccStride)
-      acc_shard(a, (a.pass + 1) % kAccSets, nd.shard_base + t.local)[lane_id()] = 0;
-    if (KIND == PASS_SPLIT) {
-      if (nd.root) {
-        // DivQuantClusterInitMeanAndVar (:90-104) from the INIT sums, then
-        // the cut (:388-403).
-        uint64_t tt[F_NUM];
-        reduce_shards(a, nd, (a.pass + kAccSets - 1) % kAccSets, 7, tt);
-        if (lane_id() == 0) {
-          double tm[3], tv[3];
-          for (int c = 0; c < 3; ++c) {
-            double m = (double)tt[F_SR + c];
-            double q = (double)tt[F_QR + c];
-            m *= nd.s;
-            q *= nd.s;
-            q -= m * m;
-            tm[c] = m;
-            tv[c] = q;
-          }
-          double maxv = tv[0], cut = tm[0];
-          int axis = 0;
-          if (maxv < tv[1]) { maxv = tv[1]; axis = 1; cut = tm[1]; }
-          if (maxv < tv[2]) { axis = 2; cut = tm[2]; }
-          prm.thr = split_threshold(cut);
-          prm.shift = 16 - 8 * axis;
-          if (t.local == 0) {   // later passes and the host read the root's tm/tv
-            DevNode& w = a.nodes[t.node];
-            for (int c = 0; c < 3; ++c) { w.tm[c] = tm[c]; w.tv[c] = tv[c]; }
-          }
-        }
-      } else if (lane_id() == 0) {
-        prm.thr = nd.thr;
-        prm.shift = 16 - 8 * nd.axis;
-      }
-    } else if (KIND == PASS_KMEANS || KIND == PASS_KLAST) {
-      uint64_t tt[F_NUM];
-      reduce_shards(a, nd, (a.pass + kAccSets - 1) % kAccSets, 4, tt);
-      if (lane_id() == 0) {
-        double om[3], nm[3], nw, ow;
-        means_from_sums(tt, nd.s, nd.tw, nd.tm, om, nm, &nw, &ow);
-        decision_from_means(om, nm, &prm);
-      }
-    }
-  }
-  __syncthreads();
-  const Params q = prm;
+  const Params q = nd.prm;
 
   // Packed lane partials: rb = R<<16 | B sums, gc = cnt<<16 | G sums (each
   // half < 2^16 because a tile gives a lane at most 256 points).
@@ -289,31 +303,60 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
     for (int k = 0; k < kNF; ++k) red[wave_id()][k] = f[k];
   }
   __syncthreads();
-  if (threadIdx.x < (uint32_t)kNF) {
+  if (wave_id() != 0) return;
+
+  const uint32_t l = lane_id();
+  const int T = nd.tile_end - nd.tile_begin;
+  const int nsh = nd.nshard;
+  const int shard = (int)(t.local % (uint32_t)nsh);
+  uint64_t* sh = acc_shard(a, nd.shard_base + shard);
+  if (l < (uint32_t)kNF) {
     uint64_t s = 0;
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-    atomicAdd((unsigned long long*)acc_shard(a, set, nd.shard_base + (int)(t.local % (uint32_t)nd.nshard)) +
-                  threadIdx.x,
-              (unsigned long long)s);
-    if (KIND == PASS_KLAST && threadIdx.x == 0) a.tile_cnt[blockIdx.x] = (uint32_t)s;
+    for (int w = 0; w < kBlock / 64; ++w) s += red[w][l];
+    atomic_add(sh + l, s);
+    if (KIND == PASS_KLAST && l == 0) a.tile_cnt[blockIdx.x] = (uint32_t)s;
+  }
+  release_agent();   // this tile's sums are performed before its ticket
+  // Tiles of this shard: local = shard, shard + nsh, ... < T.
+  const uint64_t shard_tiles = (uint64_t)((T - 1 - shard) / nsh + 1);
+  uint64_t old = 0;
+  if (l == 0) old = atomic_inc(sh + F_TICKET);
+  old = __shfl(old, 0, 64);
+  if (old != shard_tiles - 1) return;            // not the shard's last tile
+  uint64_t* sh0 = acc_shard(a, nd.shard_base);
+  if (l == 0) {
+    atomic_take(sh + F_TICKET);
+    old = atomic_inc(sh0 + F_NODE_TICKET);
+  }
+  old = __shfl(old, 0, 64);
+  if (old != (uint64_t)nsh - 1) return;          // not the node's last shard
+  // Last arriver of the node: take every shard's sums (read + zero).
+  uint64_t tot[F_NUM];
+#pragma unroll
+  for (int k = 0; k < F_NUM; ++k) {
+    uint64_t x = 0;
+    if (k < kNF && l < (uint32_t)nsh) x = atomic_take(acc_shard(a, nd.shard_base + (int)l) + k);
+    tot[k] = k < kNF ? wave_sum_u64(x) : 0;
+  }
+  if (l == 0) {
+    atomic_take(sh0 + F_NODE_TICKET);
+    node_update<KIND>(a.nodes + t.node, tot);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Partition.  Prologue: the KLAST sums (set pass-1) give the split's results
-// (:787-871, written to DevNode by the node's first tile), the sums before
-// them (set pass-2) give the KLAST decision, recomputed here bit-identically.
-// Body: OLD points to [off, off+n_old) and NEW points to [off+n_old, off+len)
-// of the child buffer, both in index order.
+// Partition: replay the last 2-means decision (DevNode.prm, bit-identical
+// inputs -> bit-identical outcome) and write OLD points to [off, off+n_old)
+// and NEW points to [off+n_old, off+len) of the child buffer.  Within a sweep
+// points are ranked in (slot, wave, lane) order; tiles follow each other, so
+// each half is a fixed permutation of the parent's order.
 __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const DevNode& nd = a.nodes[t.node];
   const uint32_t* __restrict__ src = nd.src;
   uint32_t* __restrict__ dst = nd.dst;
 
-  __shared__ Params prm;
-  __shared__ uint32_t n_new_s;
   __shared__ uint32_t pre[kBlock / 64];
   __shared__ uint32_t cnt[2][kVecPerThread * 4 * (kBlock / 64)];
   __shared__ uint32_t tot[2];
@@ -321,8 +364,9 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
   const uint32_t vs0 = t.start & ~3u;
   uint4 v[kVecPerThread];
   load_sweep(src, vs0, t.end, v);
+  const Params q = nd.prm;
 
-  // Old points in this node's earlier tiles (KLAST wrote each tile's new count).
+  // Old points in this node's earlier tiles (PASS_KLAST stored each tile's new count).
   uint32_t older = 0;
   for (int i = nd.tile_begin + (int)threadIdx.x; i < nd.tile_begin + (int)t.local; i += kBlock) {
     const Tile& u = a.tiles[i];
@@ -330,43 +374,9 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
   }
   older = wave_sum_u32(older);
   if (lane_id() == 0) pre[wave_id()] = older;
-
-  if (wave_id() == 0) {
-    uint64_t tk[F_NUM], tp[F_NUM];
-    reduce_shards(a, nd, (a.pass + kAccSets - 1) % kAccSets, 7, tk);
-    reduce_shards(a, nd, (a.pass + kAccSets - 2) % kAccSets, 4, tp);
-    if (lane_id() == 0) {
-      double om[3], nm[3], nw, ow;
-      means_from_sums(tp, nd.s, nd.tw, nd.tm, om, nm, &nw, &ow);
-      decision_from_means(om, nm, &prm);
-      n_new_s = (uint32_t)tk[F_CNT];
-      if (t.local == 0) {
-        DevNode& w = a.nodes[t.node];
-        w.plhs = prm.lhs; w.prr = prm.rr; w.prg = prm.rg; w.prb = prm.rb;
-        means_from_sums(tk, nd.s, nd.tw, nd.tm, om, nm, &nw, &ow);
-        for (int c = 0; c < 3; ++c) {                  // (:836-838)
-          double qv = (double)tk[F_QR + c];
-          qv *= nd.s;
-          w.nv[c] = qv / nw - nm[c] * nm[c];
-        }
-        for (int c = 0; c < 3; ++c) {                  // (:845-855)
-          const double dn = nm[c] - nd.tm[c];
-          const double dox = om[c] - nd.tm[c];
-          w.ov[c] = ((nd.tw * nd.tv[c] - nw * (w.nv[c] + dn * dn)) / ow) - dox * dox;
-        }
-        w.tse_old = ow * (w.ov[0] + w.ov[1] + w.ov[2]);   // (:870-871)
-        w.tse_new = nw * (w.nv[0] + w.nv[1] + w.nv[2]);
-        for (int c = 0; c < 3; ++c) { w.om[c] = om[c]; w.nm[c] = nm[c]; }
-        w.nw = nw;
-        w.ow = ow;
-        w.n_new = tk[F_CNT];
-      }
-    }
-  }
   __syncthreads();
-  const Params q = prm;
   const uint32_t old_base = pre[0] + pre[1] + pre[2] + pre[3];
-  const uint32_t n_old = nd.len - n_new_s;
+  const uint32_t n_old = nd.len - (uint32_t)nd.n_new;
   uint32_t old_cur = nd.off + old_base;
   uint32_t new_cur = nd.off + n_old + ((t.start - nd.off) - old_base);
 
@@ -394,8 +404,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
       }
     }
     __syncthreads();
-    // Points of a sweep are ranked in (slot, wave, lane) order: an exclusive
-    // scan over the 64 (slot, wave) counts by wave 0 (old) and wave 1 (new).
+    // Exclusive scan over the 64 (slot, wave) counts: wave 0 old, wave 1 new.
     if (w < 2) {
       const uint32_t val = cnt[w][l];
       uint32_t inc = val;
@@ -425,7 +434,6 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
 // Map, step 1: per colour cell (8x8x8 values), the palette entries whose
 // minimum distance to the cell does not exceed the smallest maximum distance
 // of any entry to the cell.  Every exact argmin for a colour of the cell is
@@ -493,6 +501,9 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(
     }
   }
   if (lane == 0) {
+    // unused inline slots repeat the first candidate: evaluating a duplicate
+    // never changes the argmin, so the map evaluates all slots branch-free
+    for (int c = (int)count; c < kCellInline; ++c) inl[c] = inl[0];
     uint4 r;
     const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
     r.x = c | (inl[0] << 16);
@@ -542,17 +553,19 @@ __global__ __launch_bounds__(kBlock) void map_kernel(
       const Key key = ((Key)d << kRankBits) | (Key)rank;
       best = key < best ? key : best;
     };
-    if (cc <= (uint32_t)kCellInline) {
-      const uint32_t e[kCellInline] = {rec.x >> 16, rec.y & 0xFFFF, rec.y >> 16, rec.z & 0xFFFF,
-                                       rec.z >> 16, rec.w & 0xFFFF, rec.w >> 16};
+    // Inline candidates (padded with duplicates): branch-free for every lane.
+    const uint32_t e[kCellInline] = {rec.x >> 16, rec.y & 0xFFFF, rec.y >> 16, rec.z & 0xFFFF,
+                                     rec.z >> 16, rec.w & 0xFFFF, rec.w >> 16};
 #pragma unroll
-      for (int m = 0; m < kCellInline; ++m)
-        if ((uint32_t)m < cc) eval((int)e[m]);
-    } else if (cc != kCellBrute) {
-      const uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
-      for (uint32_t m = 0; m < cc; ++m) eval(lst[m]);
-    } else {
-      for (int j = 0; j < k; ++j) eval(j);
+    for (int m = 0; m < kCellInline; ++m) eval((int)e[m]);
+    // Rare cells with more candidates: a wave-uniform slow path.
+    if (__any(cc > (uint32_t)kCellInline)) {
+      if (cc == kCellBrute) {
+        for (int j = 0; j < k; ++j) eval(j);
+      } else if (cc > (uint32_t)kCellInline) {
+        const uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
+        for (uint32_t m = kCellInline; m < cc; ++m) eval(lst[m]);
+      }
     }
     const uint32_t rank = (uint32_t)(best & (((Key)1 << kRankBits) - 1));
     const int j = (rank & 1) ? s0 + (int)((rank + 1) >> 1) : s0 - (int)(rank >> 1);
