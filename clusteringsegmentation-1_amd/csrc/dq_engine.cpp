@@ -124,7 +124,7 @@ void Engine::stage_in(const uint32_t* h_in, uint32_t n, hipStream_t stream) {
                         hipMemcpyHostToDevice, stream));
 }
 
-void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nshards) {
+void Engine::ensure_round(size_t nnodes, size_t ntiles) {
   if (nnodes > cap_nodes_ || !d_nodes_) {
     size_t c = std::max<size_t>(nnodes, 256);
     if (d_nodes_) DQ_HIP(hipFree(d_nodes_));
@@ -136,18 +136,12 @@ void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nshards) {
   if (ntiles > cap_tiles_ || !d_tiles_) {
     size_t c = std::max<size_t>(ntiles, 4096);
     if (d_tiles_) DQ_HIP(hipFree(d_tiles_));
-    if (d_tile_cnt_) DQ_HIP(hipFree(d_tile_cnt_));
+    if (d_parts_) DQ_HIP(hipFree(d_parts_));
     if (h_tiles_) DQ_HIP(hipHostFree(h_tiles_));
     DQ_HIP(hipMalloc((void**)&d_tiles_, c * sizeof(Tile)));
-    DQ_HIP(hipMalloc((void**)&d_tile_cnt_, c * sizeof(uint32_t)));
+    DQ_HIP(hipMalloc((void**)&d_parts_, c * sizeof(TilePartial)));
     DQ_HIP(hipHostMalloc((void**)&h_tiles_, c * sizeof(Tile), hipHostMallocDefault));
     cap_tiles_ = c;
-  }
-  if (nshards > cap_shards_ || !d_acc_) {
-    size_t c = std::max<size_t>(nshards, 4096);
-    if (d_acc_) DQ_HIP(hipFree(d_acc_));
-    DQ_HIP(hipMalloc((void**)&d_acc_, c * kAccStride * sizeof(uint64_t)));
-    cap_shards_ = c;
   }
 }
 
@@ -163,19 +157,17 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
   const int nn = (int)active.size();
   uint64_t total = 0;
   for (int id : active) total += nodes_[id].len;
-  // Tile length: whole 4096-point sweeps, ~2048 tiles for big rounds.
-  uint64_t tl = (total + 2047) / 2048;
+  // Tile length: whole 4096-point sweeps, ~1024 tiles for big rounds (4 per
+  // CU: measured best for one 4K frame and for 8-frame batches, microbench).
+  uint64_t tl = (total + 1023) / 1024;
   tl = ((tl + kSweep - 1) / kSweep) * kSweep;
   tl = std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, kMaxTilePx));
-  size_t ntiles = 0, nshards = 0;
-  for (int id : active) {
-    const size_t t = std::max<size_t>(1, (nodes_[id].len + tl - 1) / tl);   // empty nodes get one empty tile
-    ntiles += t;
-    nshards += std::max<size_t>(1, std::min<size_t>(t, kMaxShards));
-  }
-  ensure_round(nn, ntiles, nshards);
+  size_t ntiles = 0;
+  for (int id : active)   // empty nodes get one empty tile (their epilogue still runs)
+    ntiles += std::max<size_t>(1, (nodes_[id].len + tl - 1) / tl);
+  ensure_round(nn, ntiles);
 
-  int t = 0, sh = 0;
+  int t = 0;
   for (int a = 0; a < nn; ++a) {
     const Node& n = nodes_[active[a]];
     const FrameState& fs = frames_[n.frame];
@@ -190,7 +182,7 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
     for (int c = 0; c < 3; ++c) { d.tm[c] = n.mean[c]; d.tv[c] = n.var[c]; }
     if (!root_round) {
       // Cut axis/position (:388-403): comparisons and copies only.  (The
-      // root's come from its PASS_INIT on the device.)
+      // root's come from its PASS_INIT epilogue on the device.)
       double maxv = n.var[0], cut = n.mean[0];
       int axis = 0;
       if (maxv < n.var[1]) { maxv = n.var[1]; axis = 1; cut = n.mean[1]; }
@@ -199,35 +191,31 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
       d.prm.shift = 16 - 8 * axis;
     }
     d.tile_begin = t;
-    uint32_t local = 0;
     for (uint64_t o = 0; o == 0 || o < n.len; o += tl) {
       Tile& tt = h_tiles_[t++];
       tt.node = a;
       tt.start = n.off + (uint32_t)o;
       tt.end = n.off + (uint32_t)std::min<uint64_t>(n.len, o + tl);
-      tt.local = local++;
+      tt.old_base = 0;
     }
     d.tile_end = t;
-    d.shard_base = sh;
-    d.nshard = (int32_t)std::max<uint32_t>(1, std::min<uint32_t>(local, kMaxShards));
-    sh += d.nshard;
   }
   DQ_HIP(hipMemcpyAsync(d_nodes_, h_nodes_, nn * sizeof(DevNode), hipMemcpyHostToDevice, stream));
   DQ_HIP(hipMemcpyAsync(d_tiles_, h_tiles_, ntiles * sizeof(Tile), hipMemcpyHostToDevice, stream));
-  // Sums and tickets start at zero; each node's last arriver re-zeroes them.
-  DQ_HIP(hipMemsetAsync(d_acc_, 0, (size_t)sh * kAccStride * sizeof(uint64_t), stream));
 
   RoundArgs ra;
   ra.tiles = d_tiles_;
   ra.nodes = d_nodes_;
-  ra.acc = d_acc_;
-  ra.tile_cnt = d_tile_cnt_;
+  ra.parts = d_parts_;
   const double bytes = 4.0 * (double)total;
   const int nt = (int)ntiles;
   auto pass = [&](int kind, int st) {
     timed_begin(stream);
     launch_pass(kind, ra, nt, stream);
     timed_end(st, bytes, stream);
+    timed_begin(stream);
+    launch_epilogue(kind, ra, nn, stream);
+    timed_end(ST_EPILOGUE, 0.0, stream);
     last_points_swept += total;
   };
   if (root_round) pass(PASS_INIT, ST_INIT);
@@ -383,7 +371,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     frames_[i].job = &j;
     frames_[i].base = (uint32_t)total;
     total += align4(j.n) + 4;
-    if (((uintptr_t)j.d_in & 15) != 0) align_need += align4(j.n) + 4;
+    if (((uintptr_t)j.d_in & 15) != 0 || (j.n & 3) != 0) align_need += align4(j.n) + 4;
   }
   DQ_CHECK(total < (1ull << 32), "batch larger than 2^32 points");
   ensure_pixels(total);
@@ -400,7 +388,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     // get_double_scale (DivQuantMapColors.cpp:205-220)
     f.s = 1.0 / (std::ceil(1 / 1.0) * std::ceil(j.n / 1.0));
     f.in = j.d_in;
-    if (((uintptr_t)j.d_in & 15) != 0) {   // the sweeps use 16-B loads
+    if (((uintptr_t)j.d_in & 15) != 0 || (j.n & 3) != 0) {   // 16-B loads may read up to align4(n)
       DQ_HIP(hipMemcpyAsync(d_align_ + aoff, j.d_in, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
       f.in = d_align_ + aoff;
       aoff += align4(j.n) + 4;

@@ -119,7 +119,7 @@ class Engine {
   };
 
   void ensure_pixels(size_t total);
-  void ensure_round(size_t nnodes, size_t ntiles, size_t nshards);
+  void ensure_round(size_t nnodes, size_t ntiles);
   void run_round(const std::vector<int>& active, bool root_round, int max_iters,
                  hipStream_t stream);
   void replay(FrameState& f);
@@ -150,11 +150,10 @@ class Engine {
   // per-round node/tile/accumulator tables
   DevNode* d_nodes_ = nullptr;
   Tile* d_tiles_ = nullptr;
-  uint64_t* d_acc_ = nullptr;
-  uint32_t* d_tile_cnt_ = nullptr;
+  TilePartial* d_parts_ = nullptr;
   DevNode* h_nodes_ = nullptr;   // pinned
   Tile* h_tiles_ = nullptr;      // pinned
-  size_t cap_nodes_ = 0, cap_tiles_ = 0, cap_shards_ = 0;
+  size_t cap_nodes_ = 0, cap_tiles_ = 0;
 
   // map tables
   uint32_t* d_pal_ = nullptr;

@@ -25,15 +25,13 @@ enum PassKind : int32_t {
   PASS_KLAST = 3,    // last 2-means iteration: also sums of squares (:726-748)
 };
 
-// Accumulator shard: exact integer sums of the new side (all points in
-// PASS_INIT) of the tiles with local % nshard == shard, plus arrival tickets.
-// One 128-B line per shard; every access is a device-scope atomic, so the
-// values live at the memory side and never depend on cache state.
-enum AccField : int32_t { F_CNT = 0, F_SR, F_SG, F_SB, F_QR, F_QG, F_QB, F_NUM,
-                          F_TICKET = 8,        // tiles of this shard that arrived
-                          F_NODE_TICKET = 9 }; // (shard 0 only) shards that arrived
-constexpr int kAccStride = 16;          // u64 per shard (128 B)
-constexpr int kMaxShards = 64;          // shards per node (one per lane of wave 0)
+// Per-tile partial statistics of the new side (all points in PASS_INIT):
+// plain 32-B stores, exact in u32 because a tile has at most 65536 points
+// (65536 * 255^2 < 2^32).  The node's epilogue sums them in u64.
+enum PartField : int32_t { F_CNT = 0, F_SR, F_SG, F_SB, F_QR, F_QG, F_QB, F_NUM };
+struct alignas(32) TilePartial {
+  uint32_t f[8];
+};
 
 // Decision parameters of one pass for one node (:616-623, :683).
 struct alignas(16) Params {
@@ -51,15 +49,13 @@ struct alignas(16) DevNode {
   uint32_t off, len;        // segment, relative to src / dst
   int32_t tile_begin;       // this node's tiles are [tile_begin, tile_end)
   int32_t tile_end;
-  int32_t shard_base;       // accumulator shards [shard_base, shard_base+nshard)
-  int32_t nshard;
   double s;                 // data_weight of the frame (get_double_scale)
   double tw;                // total_weight = weight[old_index]  (:353)
   double tm[3], tv[3];      // total_mean / total_var (root: written by PASS_INIT)
   // --- parameters of the next pass (host for the split pass of non-roots,
-  //     otherwise written by the node's last-arriving workgroup)
+  //     otherwise written by the node's epilogue)
   Params prm;
-  // --- results of the node's split (written by the last arriver of PASS_KLAST;
+  // --- results of the node's split (written by the PASS_KLAST epilogue;
   //     prm then still holds the last 2-means decision)
   double om[3], nm[3];      // old_mean / new_mean after the last pass
   double nv[3], ov[3];      // new_var / old_var (:836-855)
@@ -73,7 +69,7 @@ struct alignas(16) DevNode {
 struct alignas(16) Tile {
   int32_t node;             // index into the round's DevNode array
   uint32_t start, end;      // pixel range relative to the node's src
-  uint32_t local;           // tile index inside its node (shard = local % nshard)
+  uint32_t old_base;        // partition: old points in the node's earlier tiles
 };
 
 }  // namespace dq

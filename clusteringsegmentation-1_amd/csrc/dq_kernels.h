@@ -24,13 +24,16 @@ constexpr uint32_t kCellBrute = 0xFFFF;         // count marker: scan the whole 
 
 // Tables of one round (device pointers).
 struct RoundArgs {
-  const Tile* tiles;
+  Tile* tiles;
   DevNode* nodes;
-  uint64_t* acc;            // total_shards x kAccStride u64, zero between passes
-  uint32_t* tile_cnt;       // PASS_KLAST: new-side count per tile
+  TilePartial* parts;       // one per tile, rewritten by every pass
 };
 
+// One statistics pass over every tile of the round (one workgroup per tile).
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
+// The FP64 update after a pass, one workgroup per node: sums the node's tile
+// partials and publishes the next pass's decision (or the split's results).
+void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream);
 // Writes every node's points into its two children's segments (old half
 // first, then new half) of the child buffer, using the last 2-means decision.
 void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream);

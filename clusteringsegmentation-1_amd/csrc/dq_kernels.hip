@@ -6,23 +6,23 @@
 // tests/test_build.py checks the code object for v_fma_f64 outside divisions.
 //
 // Kernels
-//   pass_kernel<KIND>  one sweep over the tiles of every node being split
-//                      (all frames of the batch): per-point decision + exact
-//                      integer new-side sums (split pass :438-559, 2-means
-//                      pass :613-811, root statistics :49-104).  The node's
-//                      LAST-ARRIVING workgroup runs the reference's FP64
-//                      update (:561-598, :787-871) once and publishes the
-//                      next pass's decision in DevNode, so a pass is one
-//                      launch with no epilogue kernel and no per-workgroup
-//                      prologue.  HBM/MALL-bound: 4 B read per point.
-//   partition_kernel   writes each node's points into its two children's
-//                      segments (replaces the per-split O(N) member[]
-//                      gather, :894-1026).
-//   build_cells_kernel map: per 8x8x8 colour cell, the palette entries that
-//                      can be nearest to some colour of the cell.
-//   map_kernel         map: per pixel argmin over (squared distance, MPS
-//                      visit rank) -- identical to map_colors_mps's pruned
-//                      walk (DivQuantMapColors.cpp:385-527), see DESIGN.md.
+//   pass_kernel<KIND>     one sweep over the tiles of every node being split
+//                         (all frames of the batch): per-point decision +
+//                         exact integer new-side sums (split pass :438-559,
+//                         2-means pass :613-811, root statistics :49-104),
+//                         one plain 32-B partial per tile.  HBM/MALL-bound:
+//                         4 B read per point.
+//   epilogue_kernel<KIND> per node: sum its tile partials in u64 and run the
+//                         reference's FP64 update (:561-598, :787-871),
+//                         publishing the next pass's decision in DevNode.
+//   partition_kernel      writes each node's points into its two children's
+//                         segments (replaces the per-split O(N) member[]
+//                         gather, :894-1026).  Reads 4 B, writes 4 B per point.
+//   build_cells_kernel    map: per 8x8x8 colour cell, the palette entries that
+//                         can be nearest to some colour of the cell.
+//   map_kernel            map: per pixel argmin over (squared distance, MPS
+//                         visit rank) -- identical to map_colors_mps's pruned
+//                         walk (DivQuantMapColors.cpp:385-527), see DESIGN.md.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -32,6 +32,17 @@
 namespace dq {
 
 namespace {
+
+// Global-address-space views: pointers read from DevNode are generic, and
+// generic (flat_*) loads make the compiler wait vmcnt(0)+lgkmcnt(0) around
+// them; these casts give global_load/store with an SGPR base.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) uint32_t g_cu32;
+typedef const __attribute__((address_space(1))) u32x4 g_cu4;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+__device__ __forceinline__ g_cu4* as_g4(const uint32_t* p) { return (g_cu4*)p; }
+__device__ __forceinline__ g_cu32* as_g(const uint32_t* p) { return (g_cu32*)p; }
+__device__ __forceinline__ g_u32* as_gw(uint32_t* p) { return (g_u32*)p; }
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ uint32_t wave_id() { return threadIdx.x >> 6; }
@@ -51,28 +62,6 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
-}
-
-__device__ __forceinline__ uint64_t* acc_shard(const RoundArgs& a, int shard) {
-  return a.acc + (size_t)shard * kAccStride;
-}
-
-// All accumulator / ticket traffic is device-scope atomic: it is performed at
-// the memory side, so it is coherent across the 8 XCDs whatever the caches hold.
-__device__ __forceinline__ uint64_t atomic_take(uint64_t* p) {   // read and reset
-  return __hip_atomic_exchange(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t atomic_inc(uint64_t* p) {    // returns the old value
-  return __hip_atomic_fetch_add(p, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void atomic_add(uint64_t* p, uint64_t v) {
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Orders this wave's earlier atomics before its later ones at agent scope
-// (explicit vmcnt(0) after the fence: MI355X_MICROARCH.md, compiler hazard).
-__device__ __forceinline__ void release_agent() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // (:561-598 / :787-810) means and weights of both halves from the new side's
@@ -148,32 +137,65 @@ __device__ __forceinline__ bool stays_old(uint32_t p, const Params& q) {
   return old;
 }
 
-// Load this lane's 4 uint4 of a sweep.  `vs` is the sweep's first (16-B
-// aligned) index; lanes past `end` load nothing; a partial final vector is
-// read element by element so no byte beyond `end` is touched.
-__device__ __forceinline__ void load_sweep(const uint32_t* __restrict__ src, uint32_t vs,
-                                           uint32_t end, uint4 v[kVecPerThread]) {
+__device__ __forceinline__ uint32_t vec_elem(const u32x4& v, int e) { return v[e]; }
+
+// This lane's kVecPerThread uint4 of the sweep starting at vs (16-B aligned).
+// FULL: the whole sweep lies inside the tile.  Otherwise vectors starting at
+// or past `end` are not loaded; a vector straddling `end` is loaded whole --
+// every working buffer keeps >= 3 readable words of slack past each frame.
+template <bool FULL>
+__device__ __forceinline__ void load_sweep(g_cu4* src4, uint32_t vs, uint32_t end,
+                                           u32x4 v[kVecPerThread]) {
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
     const uint32_t i = vs + 4u * (j * kBlock + threadIdx.x);
-    if (i + 4 <= end) {
-      v[j] = *reinterpret_cast<const uint4*>(src + i);
-    } else {
-      v[j] = make_uint4(0, 0, 0, 0);
-      if (i < end) v[j].x = src[i];
-      if (i + 1 < end) v[j].y = src[i + 1];
-      if (i + 2 < end) v[j].z = src[i + 2];
+    if (FULL || i < end) v[j] = src4[i >> 2];
+    else v[j] = (u32x4){0u, 0u, 0u, 0u};
+  }
+}
+
+// Decision for one point of a pass (KIND) -- true: the point goes NEW.
+template <int KIND>
+__device__ __forceinline__ bool goes_new(uint32_t p, const Params& q) {
+  if (KIND == PASS_INIT) return true;
+  if (KIND == PASS_SPLIT) return (int32_t)((p >> q.shift) & 0xFF) >= q.thr;
+  return !stays_old(p, q);
+}
+
+// Lane partial sums.  rb = R<<16 | B sums, gc = cnt<<16 | G sums: each half
+// stays < 2^16 because a tile gives a lane at most 256 points.
+struct LaneSums {
+  uint32_t rb = 0, gc = 0, qr = 0, qg = 0, qb = 0;
+};
+
+template <int KIND, bool FULL>
+__device__ __forceinline__ void sweep_sums(const u32x4 v[kVecPerThread], uint32_t vs,
+                                           uint32_t start, uint32_t end, const Params& q,
+                                           LaneSums& s) {
+  constexpr bool kSquares = (KIND == PASS_INIT || KIND == PASS_KLAST);
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t p = vec_elem(v[j], e);
+      bool take = goes_new<KIND>(p, q);
+      if (!FULL) take = take && (i0 + e >= start) && (i0 + e < end);
+      s.rb += take ? (p & 0x00FF00FFu) : 0u;
+      s.gc += take ? (((p >> 8) & 0xFFu) | 0x10000u) : 0u;
+      if (kSquares) {
+        const uint32_t R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
+        s.qr += take ? R * R : 0u;
+        s.qg += take ? G * G : 0u;
+        s.qb += take ? B * B : 0u;
+      }
     }
   }
 }
 
-__device__ __forceinline__ uint32_t vec_elem(const uint4& v, int e) {
-  return e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w));
-}
-
-// The FP64 update a node's last arriver runs after pass KIND, from the
-// node's total sums t[] (exact integers).  Publishes the next pass's Params
-// (or, after PASS_KLAST, the split's results) in DevNode.
+// The FP64 update after pass KIND from the node's total sums t[] (exact
+// integers).  Publishes the next pass's Params, or after PASS_KLAST the
+// split's results, in DevNode.
 template <int KIND>
 __device__ void node_update(DevNode* w, const uint64_t t[F_NUM]) {
   const double s = w->s, tw = w->tw;
@@ -241,107 +263,120 @@ __device__ void node_update(DevNode* w, const uint64_t t[F_NUM]) {
 // Statistics pass.  One workgroup per tile; a tile lies inside one node's
 // segment, so every point of the workgroup shares the node's parameters and
 // the sums need no per-point binning: packed lane partials -> wave sums ->
-// LDS -> one u64 atomic add per field into the node's shard (local % nshard).
-// Then two-level arrival tickets (shard, then node) elect the node's last
-// workgroup, which takes (reads and zeroes) the node's sums and runs
-// node_update<KIND>.
+// LDS -> one 32-B partial per tile.
 template <int KIND>
 __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const DevNode& nd = a.nodes[t.node];
-  const uint32_t* __restrict__ src = nd.src;
+  g_cu4* src4 = as_g4(nd.src);
+  const Params q = nd.prm;
   constexpr bool kSquares = (KIND == PASS_INIT || KIND == PASS_KLAST);
   constexpr int kNF = kSquares ? 7 : 4;
 
   __shared__ uint32_t red[kBlock / 64][8];
-
-  const uint32_t vs0 = t.start & ~3u;
-  uint4 v[kVecPerThread];
-  load_sweep(src, vs0, t.end, v);
-  const Params q = nd.prm;
-
-  // Packed lane partials: rb = R<<16 | B sums, gc = cnt<<16 | G sums (each
-  // half < 2^16 because a tile gives a lane at most 256 points).
-  uint32_t rb = 0, gc = 0, qr = 0, qg = 0, qb = 0;
-  for (uint32_t vs = vs0;;) {
-#pragma unroll
-    for (int j = 0; j < kVecPerThread; ++j) {
-      const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t p = vec_elem(v[j], e);
-        const uint32_t i = i0 + e;
-        const bool valid = (i >= t.start) & (i < t.end);
-        bool take;
-        if (KIND == PASS_INIT) {
-          take = valid;
-        } else if (KIND == PASS_SPLIT) {
-          take = valid && (int32_t)((p >> q.shift) & 0xFF) >= q.thr;
-        } else {
-          take = valid && !stays_old(p, q);
-        }
-        rb += take ? (p & 0x00FF00FFu) : 0u;
-        gc += take ? (((p >> 8) & 0xFFu) | 0x10000u) : 0u;
-        if (kSquares) {
-          const uint32_t R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
-          qr += take ? R * R : 0u;
-          qg += take ? G * G : 0u;
-          qb += take ? B * B : 0u;
-        }
-      }
+  LaneSums s;
+  u32x4 v[kVecPerThread];
+  for (uint32_t vs = t.start & ~3u; vs < t.end; vs += kSweep) {
+    if (vs >= t.start && vs + kSweep <= t.end) {   // wave-uniform
+      load_sweep<true>(src4, vs, t.end, v);
+      sweep_sums<KIND, true>(v, vs, t.start, t.end, q, s);
+    } else {
+      load_sweep<false>(src4, vs, t.end, v);
+      sweep_sums<KIND, false>(v, vs, t.start, t.end, q, s);
     }
-    vs += kSweep;
-    if (vs >= t.end) break;
-    load_sweep(src, vs, t.end, v);
   }
 
-  uint32_t f[7] = {gc >> 16, rb >> 16, gc & 0xFFFF, rb & 0xFFFF, qr, qg, qb};
+  uint32_t f[8] = {s.gc >> 16, s.rb >> 16, s.gc & 0xFFFF, s.rb & 0xFFFF, s.qr, s.qg, s.qb, 0};
 #pragma unroll
   for (int k = 0; k < kNF; ++k) f[k] = wave_sum_u32(f[k]);
   if (lane_id() == 0) {
 #pragma unroll
-    for (int k = 0; k < kNF; ++k) red[wave_id()][k] = f[k];
+    for (int k = 0; k < 8; ++k) red[wave_id()][k] = k < kNF ? f[k] : 0u;
   }
   __syncthreads();
-  if (wave_id() != 0) return;
+  if (threadIdx.x < 8) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) x += red[w][threadIdx.x];
+    as_gw(a.parts[blockIdx.x].f)[threadIdx.x] = x;
+  }
+}
 
-  const uint32_t l = lane_id();
-  const int T = nd.tile_end - nd.tile_begin;
-  const int nsh = nd.nshard;
-  const int shard = (int)(t.local % (uint32_t)nsh);
-  uint64_t* sh = acc_shard(a, nd.shard_base + shard);
-  if (l < (uint32_t)kNF) {
-    uint64_t s = 0;
+// ---------------------------------------------------------------------------
+// Epilogue: one workgroup per node.
+template <int KIND>
+__global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
+  DevNode* w = a.nodes + blockIdx.x;
+  const int tb = w->tile_begin, te = w->tile_end;
+  constexpr bool kSquares = (KIND == PASS_INIT || KIND == PASS_KLAST);
+  constexpr int kNF = kSquares ? 7 : 4;
+  const g_cu4* parts4 = (const g_cu4*)a.parts;
+
+  uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (int base = tb; base < te; base += 4 * kBlock) {
+    u32x4 x[4], y[4];
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; ++w) s += red[w][l];
-    atomic_add(sh + l, s);
-    if (KIND == PASS_KLAST && l == 0) a.tile_cnt[blockIdx.x] = (uint32_t)s;
-  }
-  release_agent();   // this tile's sums are performed before its ticket
-  // Tiles of this shard: local = shard, shard + nsh, ... < T.
-  const uint64_t shard_tiles = (uint64_t)((T - 1 - shard) / nsh + 1);
-  uint64_t old = 0;
-  if (l == 0) old = atomic_inc(sh + F_TICKET);
-  old = __shfl(old, 0, 64);
-  if (old != shard_tiles - 1) return;            // not the shard's last tile
-  uint64_t* sh0 = acc_shard(a, nd.shard_base);
-  if (l == 0) {
-    atomic_take(sh + F_TICKET);
-    old = atomic_inc(sh0 + F_NODE_TICKET);
-  }
-  old = __shfl(old, 0, 64);
-  if (old != (uint64_t)nsh - 1) return;          // not the node's last shard
-  // Last arriver of the node: take every shard's sums (read + zero).
-  uint64_t tot[F_NUM];
+    for (int u = 0; u < 4; ++u) {   // issue every load of the chunk first
+      const int i = base + u * kBlock + (int)threadIdx.x;
+      if (i < te) {
+        x[u] = parts4[2 * i];
+        if (kSquares) y[u] = parts4[2 * i + 1];
+      } else {
+        x[u] = (u32x4){0u, 0u, 0u, 0u};
+        y[u] = (u32x4){0u, 0u, 0u, 0u};
+      }
+    }
 #pragma unroll
-  for (int k = 0; k < F_NUM; ++k) {
-    uint64_t x = 0;
-    if (k < kNF && l < (uint32_t)nsh) x = atomic_take(acc_shard(a, nd.shard_base + (int)l) + k);
-    tot[k] = k < kNF ? wave_sum_u64(x) : 0;
+    for (int u = 0; u < 4; ++u) {
+      acc[0] += x[u][0];
+      acc[1] += x[u][1];
+      acc[2] += x[u][2];
+      acc[3] += x[u][3];
+      if (kSquares) {
+        acc[4] += y[u][0];
+        acc[5] += y[u][1];
+        acc[6] += y[u][2];
+      }
+    }
   }
-  if (l == 0) {
-    atomic_take(sh0 + F_NODE_TICKET);
-    node_update<KIND>(a.nodes + t.node, tot);
+  __shared__ uint64_t red[kBlock / 64][8];
+#pragma unroll
+  for (int k = 0; k < kNF; ++k) acc[k] = wave_sum_u64(acc[k]);
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < kNF; ++k) red[wave_id()][k] = acc[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t tot[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < kNF; ++k)
+      for (int v = 0; v < kBlock / 64; ++v) tot[k] += red[v][k];
+    node_update<KIND>(w, tot);
+  }
+  if (KIND == PASS_KLAST) {
+    // Each tile's first OLD point's rank among the node's old points: an
+    // exclusive scan of the tiles' old counts, chunked per lane.
+    __shared__ uint32_t scan[kBlock];
+    const int T = te - tb;
+    const int chunk = (T + kBlock - 1) / kBlock;
+    const int c0 = tb + (int)threadIdx.x * chunk;
+    const int c1 = min(te, c0 + chunk);
+    uint32_t local = 0;
+    for (int i = c0; i < c1; ++i)
+      local += (a.tiles[i].end - a.tiles[i].start) - a.parts[i].f[F_CNT];
+    scan[threadIdx.x] = local;
+    __syncthreads();
+    for (int o = 1; o < kBlock; o <<= 1) {
+      const uint32_t v = threadIdx.x >= (uint32_t)o ? scan[threadIdx.x - o] : 0u;
+      __syncthreads();
+      scan[threadIdx.x] += v;
+      __syncthreads();
+    }
+    uint32_t run = scan[threadIdx.x] - local;
+    for (int i = c0; i < c1; ++i) {
+      a.tiles[i].old_base = run;
+      run += (a.tiles[i].end - a.tiles[i].start) - a.parts[i].f[F_CNT];
+    }
   }
 }
 
@@ -349,40 +384,29 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
 // Partition: replay the last 2-means decision (DevNode.prm, bit-identical
 // inputs -> bit-identical outcome) and write OLD points to [off, off+n_old)
 // and NEW points to [off+n_old, off+len) of the child buffer.  Within a sweep
-// points are ranked in (slot, wave, lane) order; tiles follow each other, so
-// each half is a fixed permutation of the parent's order.
+// points are ranked in (slot, wave, lane) order and tiles follow each other,
+// so each half is a fixed permutation of the parent's points.
 __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const DevNode& nd = a.nodes[t.node];
-  const uint32_t* __restrict__ src = nd.src;
-  uint32_t* __restrict__ dst = nd.dst;
+  g_cu4* src4 = as_g4(nd.src);
+  g_u32* dst = as_gw(nd.dst);
+  const Params q = nd.prm;
 
-  __shared__ uint32_t pre[kBlock / 64];
   __shared__ uint32_t cnt[2][kVecPerThread * 4 * (kBlock / 64)];
   __shared__ uint32_t tot[2];
 
-  const uint32_t vs0 = t.start & ~3u;
-  uint4 v[kVecPerThread];
-  load_sweep(src, vs0, t.end, v);
-  const Params q = nd.prm;
-
-  // Old points in this node's earlier tiles (PASS_KLAST stored each tile's new count).
-  uint32_t older = 0;
-  for (int i = nd.tile_begin + (int)threadIdx.x; i < nd.tile_begin + (int)t.local; i += kBlock) {
-    const Tile& u = a.tiles[i];
-    older += (u.end - u.start) - a.tile_cnt[i];
-  }
-  older = wave_sum_u32(older);
-  if (lane_id() == 0) pre[wave_id()] = older;
-  __syncthreads();
-  const uint32_t old_base = pre[0] + pre[1] + pre[2] + pre[3];
   const uint32_t n_old = nd.len - (uint32_t)nd.n_new;
-  uint32_t old_cur = nd.off + old_base;
-  uint32_t new_cur = nd.off + n_old + ((t.start - nd.off) - old_base);
+  uint32_t old_cur = nd.off + t.old_base;
+  uint32_t new_cur = nd.off + n_old + ((t.start - nd.off) - t.old_base);
 
   const uint32_t w = wave_id(), l = lane_id();
   constexpr int kSlots = kVecPerThread * 4;
-  for (uint32_t vs = vs0;;) {
+  u32x4 v[kVecPerThread];
+  for (uint32_t vs = t.start & ~3u; vs < t.end; vs += kSweep) {
+    const bool full = vs >= t.start && vs + kSweep <= t.end;
+    if (full) load_sweep<true>(src4, vs, t.end, v);
+    else load_sweep<false>(src4, vs, t.end, v);
     uint32_t slot[kSlots];   // bit 31: old, bit 30: new; low bits: rank in wave
 #pragma unroll
     for (int j = 0; j < kVecPerThread; ++j) {
@@ -391,7 +415,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
       for (int e = 0; e < 4; ++e) {
         const uint32_t p = vec_elem(v[j], e);
         const uint32_t i = i0 + e;
-        const bool valid = (i >= t.start) & (i < t.end);
+        const bool valid = full || ((i >= t.start) & (i < t.end));
         const bool old = valid && stays_old(p, q);
         const bool nw = valid && !old;
         const uint64_t mo = __ballot(old), mn = __ballot(nw);
@@ -427,10 +451,7 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
     }
     old_cur += tot[0];
     new_cur += tot[1];
-    vs += kSweep;
-    if (vs >= t.end) break;
     __syncthreads();
-    load_sweep(src, vs, t.end, v);
   }
 }
 
@@ -597,6 +618,17 @@ void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) {
     case PASS_SPLIT: pass_kernel<PASS_SPLIT><<<g, b, 0, stream>>>(a); break;
     case PASS_KMEANS: pass_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a); break;
     default: pass_kernel<PASS_KLAST><<<g, b, 0, stream>>>(a); break;
+  }
+}
+
+void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream) {
+  if (nnodes <= 0) return;
+  const dim3 g(nnodes), b(kBlock);
+  switch (kind) {
+    case PASS_INIT: epilogue_kernel<PASS_INIT><<<g, b, 0, stream>>>(a); break;
+    case PASS_SPLIT: epilogue_kernel<PASS_SPLIT><<<g, b, 0, stream>>>(a); break;
+    case PASS_KMEANS: epilogue_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a); break;
+    default: epilogue_kernel<PASS_KLAST><<<g, b, 0, stream>>>(a); break;
   }
 }
 
