@@ -40,7 +40,7 @@ Engine::Engine(int device) : device_(device) {
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   DQ_HIP(hipMalloc((void**)&d_pal_, 16384 * sizeof(uint32_t)));
   DQ_HIP(hipMalloc((void**)&d_lut_, 768 * sizeof(uint16_t)));
-  DQ_HIP(hipMalloc((void**)&d_cell_rec_, kCells * sizeof(uint4)));
+  DQ_HIP(hipMalloc((void**)&d_cell_rec_, (size_t)kCells * kCellRecWords * sizeof(uint32_t)));
   DQ_HIP(hipMalloc((void**)&d_cell_idx_, (size_t)kCells * kCellCap * sizeof(uint16_t)));
   DQ_HIP(hipHostMalloc((void**)&h_pal_, 16384 * sizeof(uint32_t), hipHostMallocDefault));
   DQ_HIP(hipHostMalloc((void**)&h_lut_, 768 * sizeof(uint16_t), hipHostMallocDefault));

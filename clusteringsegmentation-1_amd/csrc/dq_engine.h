@@ -158,7 +158,7 @@ class Engine {
   // map tables
   uint32_t* d_pal_ = nullptr;
   uint16_t* d_lut_ = nullptr;
-  uint4* d_cell_rec_ = nullptr;
+  uint32_t* d_cell_rec_ = nullptr;
   uint16_t* d_cell_idx_ = nullptr;
   uint32_t* h_pal_ = nullptr;    // pinned
   uint16_t* h_lut_ = nullptr;    // pinned

@@ -18,7 +18,8 @@ constexpr uint32_t kMaxTilePx = 16 * kSweep;    // keeps packed 16-bit lane sums
 // Map (nearest palette entry) cell grid: 32 cells of 8 values per channel.
 constexpr int kCellBits = 5;
 constexpr int kCells = 1 << (3 * kCellBits);
-constexpr int kCellInline = 7;                  // candidates stored in the 16-B record
+constexpr int kCellInline = 7;                  // candidates stored in the record
+constexpr int kCellRecWords = 4;                // 16-B record per cell
 constexpr int kCellCap = 32;                    // candidates in the overflow list
 constexpr uint32_t kCellBrute = 0xFFFF;         // count marker: scan the whole palette
 
@@ -40,11 +41,11 @@ void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream);
 
 // Map: candidate records per colour cell, then the per-pixel argmin over
 // (squared distance, MPS visit rank).
-void launch_build_cells(const uint32_t* pal_sorted, int k, uint4* cell_rec,
+void launch_build_cells(const uint32_t* pal_sorted, int k, uint32_t* cell_rec,
                         uint16_t* cell_idx, hipStream_t stream);
 void launch_map(const uint32_t* in, uint32_t n, uint32_t* out,
                 const uint32_t* pal_sorted, int k, const uint16_t* lut_init,
-                const uint4* cell_rec, const uint16_t* cell_idx,
+                const uint32_t* cell_rec, const uint16_t* cell_idx,
                 hipStream_t stream);
 
 }  // namespace dq

@@ -458,150 +458,144 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
 // Map, step 1: per colour cell (8x8x8 values), the palette entries whose
 // minimum distance to the cell does not exceed the smallest maximum distance
 // of any entry to the cell.  Every exact argmin for a colour of the cell is
-// among them (ties included: <=).  One wave per cell.  Record (16 B):
-//   x[15:0] count c; c <= 7: entries in x[31:16], y, z, w (u16 halves);
-//   7 < c <= kCellCap: entries in cell_idx[cell*kCellCap ...];
-//   c == kCellBrute: scan the whole palette.
+// among them (ties included: <=).  One LANE per cell: the palette is read from
+// LDS by broadcast (every lane the same entry, no bank conflicts).
+// Record (16 B): x[15:0] count c; x[31:16], y, z, w: the first kCellInline
+// candidates' sorted indices (u16), unused slots = k (a sentinel entry that is
+// farther than any real one); c > kCellInline: all c indices in
+// cell_idx[cell*kCellCap ...]; c == kCellBrute: scan the whole palette.
 __global__ __launch_bounds__(kBlock) void build_cells_kernel(
-    const uint32_t* __restrict__ pal, int k, uint4* __restrict__ cell_rec,
+    const uint32_t* __restrict__ pal, int k, uint32_t* __restrict__ cell_rec,
     uint16_t* __restrict__ cell_idx) {
   extern __shared__ uint32_t spal[];
   for (int i = threadIdx.x; i < k; i += kBlock) spal[i] = pal[i];
   __syncthreads();
-  const int cell = blockIdx.x * (kBlock / 64) + (int)wave_id();
-  if (cell >= kCells) return;
-  const int lane = (int)lane_id();
+  const uint32_t cell = blockIdx.x * kBlock + threadIdx.x;
+  if (cell >= (uint32_t)kCells) return;
   const int cw = 1 << (8 - kCellBits);
-  int lo[3], hi[3];
-  lo[0] = (cell >> (2 * kCellBits)) * cw;
-  lo[1] = ((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
-  lo[2] = (cell & ((1 << kCellBits) - 1)) * cw;
-  for (int c = 0; c < 3; ++c) hi[c] = lo[c] + cw - 1;
-
-  uint32_t bound = 0xFFFFFFFFu;
-  for (int e = lane; e < k; e += 64) {
+  const int lo0 = (int)(cell >> (2 * kCellBits)) * cw;
+  const int lo1 = (int)((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
+  const int lo2 = (int)(cell & ((1 << kCellBits) - 1)) * cw;
+  const int hi0 = lo0 + cw - 1, hi1 = lo1 + cw - 1, hi2 = lo2 + cw - 1;
+  auto far2 = [](int v, int lo, int hi) { const int x = max(v - lo, hi - v); return x * x; };
+  auto near2 = [](int v, int lo, int hi) {
+    const int x = v < lo ? lo - v : (v > hi ? v - hi : 0);
+    return x * x;
+  };
+  int bound = 0x7FFFFFFF;
+  for (int e = 0; e < k; ++e) {
     const uint32_t q = spal[e];
-    const int vv[3] = {(int)((q >> 16) & 0xFF), (int)((q >> 8) & 0xFF), (int)(q & 0xFF)};
-    uint32_t d = 0;
-    for (int c = 0; c < 3; ++c) {
-      const int x = max(vv[c] - lo[c], hi[c] - vv[c]);
-      d += (uint32_t)(x * x);
-    }
+    const int d = far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) +
+                  far2(q & 0xFF, lo2, hi2);
     bound = min(bound, d);
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) bound = min(bound, (uint32_t)__shfl_xor(bound, o, 64));
-
   uint32_t count = 0;
   uint32_t inl[kCellInline];
-  for (int c = 0; c < kCellInline; ++c) inl[c] = 0;
-  for (int b = 0; b < k; b += 64) {
-    const int e = b + lane;
-    bool cand = false;
-    if (e < k) {
-      const uint32_t q = spal[e];
-      const int vv[3] = {(int)((q >> 16) & 0xFF), (int)((q >> 8) & 0xFF), (int)(q & 0xFF)};
-      uint32_t d = 0;
-      for (int c = 0; c < 3; ++c) {
-        const int x = vv[c] < lo[c] ? lo[c] - vv[c] : (vv[c] > hi[c] ? vv[c] - hi[c] : 0);
-        d += (uint32_t)(x * x);
-      }
-      cand = d <= bound;
-    }
-    uint64_t m = __ballot(cand);
-    if (cand) {
-      const uint32_t pos = count + mbcnt64(m);
-      if (pos < (uint32_t)kCellCap) cell_idx[(size_t)cell * kCellCap + pos] = (uint16_t)e;
-    }
-    // first kCellInline candidates, known to every lane
-    while (m) {
-      const int bit = __builtin_ctzll(m);
-      if (count < (uint32_t)kCellInline) inl[count] = (uint32_t)(b + bit);
+#pragma unroll
+  for (int m = 0; m < kCellInline; ++m) inl[m] = (uint32_t)k;
+  uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
+  for (int e = 0; e < k; ++e) {
+    const uint32_t q = spal[e];
+    const int d = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
+                  near2(q & 0xFF, lo2, hi2);
+    if (d <= bound) {
+      if (count < (uint32_t)kCellCap) lst[count] = (uint16_t)e;
+#pragma unroll
+      for (int m = 0; m < kCellInline; ++m)
+        if (count == (uint32_t)m) inl[m] = (uint32_t)e;
       ++count;
-      m &= m - 1;
     }
   }
-  if (lane == 0) {
-    // unused inline slots repeat the first candidate: evaluating a duplicate
-    // never changes the argmin, so the map evaluates all slots branch-free
-    for (int c = (int)count; c < kCellInline; ++c) inl[c] = inl[0];
-    uint4 r;
-    const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
-    r.x = c | (inl[0] << 16);
-    r.y = inl[1] | (inl[2] << 16);
-    r.z = inl[3] | (inl[4] << 16);
-    r.w = inl[5] | (inl[6] << 16);
-    cell_rec[cell] = r;
-  }
+  uint4 r;
+  const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
+  r.x = c | (inl[0] << 16);
+  r.y = inl[1] | (inl[2] << 16);
+  r.z = inl[3] | (inl[4] << 16);
+  r.w = inl[5] | (inl[6] << 16);
+  reinterpret_cast<uint4*>(cell_rec)[cell] = r;
 }
 
-// Map, step 2.  Key = (squared distance, MPS visit rank) where the walk
-// starts at s = lut_init[R+G+B] and visits s, s+1, s-1, s+2, s-2, ...:
-// rank(j) = 2(j-s)-1 for j > s, 2(s-j) otherwise.  The minimum key's entry is
-// exactly what map_colors_mps returns (strict '<' keeps the first visited;
-// the floor(d^2/3) pruning never drops a strictly closer entry).
-template <bool kWide>
+// Map, step 2.  The answer is the entry minimising (squared distance, MPS
+// visit rank) where the walk starts at s = lut_init[R+G+B] and visits s,
+// s+1, s-1, s+2, s-2, ...: rank(j) = 2(j-s)-1 for j > s, 2(s-j) otherwise.
+// That entry is exactly what map_colors_mps returns (strict '<' keeps the
+// first visited; the floor(d^2/3) pruning never drops a strictly closer
+// entry).  Fast path: d = |p|^2 + |c|^2 - 2 p.c (v_dot4_u32_u8) over the
+// cell's inline candidates, palette entries (colour, |c|^2 | j<<18) in LDS;
+// the rank is only needed when the minimum distance is shared or the cell
+// overflows, which takes a wave-uniform slow path.
 __global__ __launch_bounds__(kBlock) void map_kernel(
     const uint32_t* __restrict__ in, uint32_t n, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ pal, int k, const uint16_t* __restrict__ lut,
-    const uint4* __restrict__ cell_rec, const uint16_t* __restrict__ cell_idx) {
+    const uint32_t* __restrict__ cell_rec, const uint16_t* __restrict__ cell_idx) {
   extern __shared__ uint32_t smem[];
-  uint32_t* spal = smem;
-  uint16_t* slut = reinterpret_cast<uint16_t*>(smem + k);
-  for (int i = threadIdx.x; i < k; i += kBlock) spal[i] = pal[i];
+  uint2* spal = reinterpret_cast<uint2*>(smem);              // k+1 entries
+  uint16_t* slut = reinterpret_cast<uint16_t*>(smem + 2 * (k + 1));
+  for (int i = threadIdx.x; i <= k; i += kBlock) {
+    const uint32_t q = i < k ? pal[i] : 0u;
+    const uint32_t c2 = i < k ? __builtin_amdgcn_udot4(q, q, 0u, false) : 0x3FFFFu;
+    spal[i] = make_uint2(q, c2 | ((uint32_t)i << 18));
+  }
   for (int i = threadIdx.x; i < 766; i += kBlock) slut[i] = lut[i];
   __syncthreads();
-  using Key = typename std::conditional<kWide, uint64_t, uint32_t>::type;
-  constexpr int kRankBits = kWide ? 32 : 11;
+  g_cu4* rec4 = (g_cu4*)cell_rec;
 
   auto map_one = [&](uint32_t p) -> uint32_t {
-    const int R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
-    const int s0 = slut[R + G + B];
-    const uint32_t cell = ((uint32_t)(R >> (8 - kCellBits)) << (2 * kCellBits)) |
-                          ((uint32_t)(G >> (8 - kCellBits)) << kCellBits) |
-                          (uint32_t)(B >> (8 - kCellBits));
-    const uint4 rec = cell_rec[cell];
-    const uint32_t cc = rec.x & 0xFFFF;
-    Key best = (Key)~(Key)0;
-    auto eval = [&](int j) {
-      const uint32_t q = spal[j];
-      const int dr = R - (int)((q >> 16) & 0xFF);
-      const int dg = G - (int)((q >> 8) & 0xFF);
-      const int db = B - (int)(q & 0xFF);
-      const uint32_t d = (uint32_t)(dr * dr + dg * dg + db * db);
-      const int tt = j - s0;
-      const uint32_t rank = tt > 0 ? (uint32_t)(2 * tt - 1) : (uint32_t)(-2 * tt);
-      const Key key = ((Key)d << kRankBits) | (Key)rank;
-      best = key < best ? key : best;
-    };
-    // Inline candidates (padded with duplicates): branch-free for every lane.
-    const uint32_t e[kCellInline] = {rec.x >> 16, rec.y & 0xFFFF, rec.y >> 16, rec.z & 0xFFFF,
-                                     rec.z >> 16, rec.w & 0xFFFF, rec.w >> 16};
+    p &= 0xFFFFFF;
+    const uint32_t R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
+    const uint32_t cell = ((R >> (8 - kCellBits)) << (2 * kCellBits)) |
+                          ((G >> (8 - kCellBits)) << kCellBits) | (B >> (8 - kCellBits));
+    const uint32_t pp = __builtin_amdgcn_udot4(p, p, 0u, false);
+    const u32x4 r = rec4[cell];
+    const uint32_t idx[kCellInline] = {r[0] >> 16, r[1] & 0xFFFF, r[1] >> 16, r[2] & 0xFFFF,
+                                       r[2] >> 16, r[3] & 0xFFFF, r[3] >> 16};
+    uint32_t best = 0xFFFFFFFFu, bc = 0;
+    bool tie = false;
 #pragma unroll
-    for (int m = 0; m < kCellInline; ++m) eval((int)e[m]);
-    // Rare cells with more candidates: a wave-uniform slow path.
-    if (__any(cc > (uint32_t)kCellInline)) {
-      if (cc == kCellBrute) {
-        for (int j = 0; j < k; ++j) eval(j);
-      } else if (cc > (uint32_t)kCellInline) {
-        const uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
-        for (uint32_t m = kCellInline; m < cc; ++m) eval(lst[m]);
+    for (int m = 0; m < kCellInline; ++m) {
+      const uint2 e = spal[idx[m]];
+      const uint32_t d = (e.y & 0x3FFFFu) + pp - 2u * __builtin_amdgcn_udot4(p, e.x, 0u, false);
+      const bool lt = d < best;
+      tie = lt ? false : (tie || d == best);
+      best = lt ? d : best;
+      bc = lt ? e.x : bc;
+    }
+    const uint32_t cnt = r[0] & 0xFFFF;
+    const bool slow = tie || cnt > (uint32_t)kCellInline;
+    if (__any(slow)) {
+      if (slow) {
+        // exact key (d << 32) | rank over every candidate (the list has them all)
+        const int s0 = slut[R + G + B];
+        uint64_t bkey = ~0ull;
+        auto ev = [&](int j) {
+          const uint2 e = spal[j];
+          const uint32_t d = (e.y & 0x3FFFFu) + pp - 2u * __builtin_amdgcn_udot4(p, e.x, 0u, false);
+          const int tt = j - s0;
+          const uint32_t rank = tt > 0 ? (uint32_t)(2 * tt - 1) : (uint32_t)(-2 * tt);
+          const uint64_t key = ((uint64_t)d << 32) | rank;
+          if (key < bkey) { bkey = key; bc = e.x; }
+        };
+        if (cnt == kCellBrute) {
+          for (int j = 0; j < k; ++j) ev(j);
+        } else {
+          const uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
+          for (uint32_t m = 0; m < cnt; ++m) ev(lst[m]);
+        }
       }
     }
-    const uint32_t rank = (uint32_t)(best & (((Key)1 << kRankBits) - 1));
-    const int j = (rank & 1) ? s0 + (int)((rank + 1) >> 1) : s0 - (int)(rank >> 1);
-    return spal[j];
+    return bc;
   };
 
   const uint32_t nvec = n / 4;
+  g_cu4* in4 = (g_cu4*)in;
   const uint32_t stride = gridDim.x * kBlock;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride) {
-    const uint4 p = reinterpret_cast<const uint4*>(in)[i];
+    const u32x4 p = in4[i];
     uint4 o;
-    o.x = map_one(p.x);
-    o.y = map_one(p.y);
-    o.z = map_one(p.z);
-    o.w = map_one(p.w);
+    o.x = map_one(p[0]);
+    o.y = map_one(p[1]);
+    o.z = map_one(p[2]);
+    o.w = map_one(p[3]);
     reinterpret_cast<uint4*>(out)[i] = o;
   }
   const uint32_t tail = nvec * 4 + blockIdx.x * kBlock + threadIdx.x;
@@ -637,28 +631,24 @@ void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream) {
   partition_kernel<<<dim3(ntiles), dim3(kBlock), 0, stream>>>(a);
 }
 
-void launch_build_cells(const uint32_t* pal_sorted, int k, uint4* cell_rec,
+void launch_build_cells(const uint32_t* pal_sorted, int k, uint32_t* cell_rec,
                         uint16_t* cell_idx, hipStream_t stream) {
-  const int blocks = kCells / (kBlock / 64);
+  const int blocks = kCells / kBlock;
   build_cells_kernel<<<dim3(blocks), dim3(kBlock), (size_t)k * 4, stream>>>(
       pal_sorted, k, cell_rec, cell_idx);
 }
 
 void launch_map(const uint32_t* in, uint32_t n, uint32_t* out,
                 const uint32_t* pal_sorted, int k, const uint16_t* lut_init,
-                const uint4* cell_rec, const uint16_t* cell_idx,
+                const uint32_t* cell_rec, const uint16_t* cell_idx,
                 hipStream_t stream) {
   if (n == 0) return;
-  const size_t lds = (size_t)k * 4 + 768 * 2;
+  const size_t lds = (size_t)(k + 1) * 8 + 768 * 2;
   uint32_t blocks = (n / 4 + kBlock - 1) / kBlock;
   if (blocks > 2048) blocks = 2048;
   if (blocks == 0) blocks = 1;
-  if (k <= 1024)
-    map_kernel<false><<<dim3(blocks), dim3(kBlock), lds, stream>>>(
-        in, n, out, pal_sorted, k, lut_init, cell_rec, cell_idx);
-  else
-    map_kernel<true><<<dim3(blocks), dim3(kBlock), lds, stream>>>(
-        in, n, out, pal_sorted, k, lut_init, cell_rec, cell_idx);
+  map_kernel<<<dim3(blocks), dim3(kBlock), lds, stream>>>(in, n, out, pal_sorted, k, lut_init,
+                                                         cell_rec, cell_idx);
 }
 
 }  // namespace dq

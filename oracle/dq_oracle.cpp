@@ -284,6 +284,46 @@ void dqo_map(const uint32_t* in, uint32_t n, uint32_t* out,
   }
 }
 
+// The identity the GPU map kernel relies on, evaluated by brute force: with the
+// same sorted palette and start LUT as dqo_map, the answer is the entry that
+// minimises (squared distance, MPS visit rank), rank(j) = 2(j-s)-1 for j > s
+// and 2(s-j) otherwise (s = start[R+G+B]).  Test infrastructure only.
+void dqo_map_argmin(const uint32_t* in, uint32_t n, uint32_t* out,
+                    const uint32_t* ct, int k) {
+  std::vector<PalEntry> pal(k);
+  for (int i = 0; i < k; ++i) {
+    uint32_t c[3];
+    unpack(ct[i], c);
+    pal[i] = {(int)c[0], (int)c[1], (int)c[2], (int)(c[0] + c[1] + c[2])};
+  }
+  std::sort(pal.begin(), pal.end(),
+            [](const PalEntry& a, const PalEntry& b) { return a.w < b.w; });
+  int start[766];
+  auto mid = [&](int i) { return (int)(0.5 * (pal[i].w + pal[i + 1].w) + 0.5); };
+  int lo = k >= 2 ? mid(0) : 1;
+  for (int v = 0; v < lo; ++v) start[v] = 0;
+  int hi = k >= 2 ? mid(k - 2) : 1;
+  for (int v = hi; v < 766; ++v) start[v] = k - 1;
+  for (int i = 1; i < k - 1; ++i)
+    for (int v = mid(i - 1); v < mid(i); ++v) start[v] = i;
+  for (uint32_t ip = 0; ip < n; ++ip) {
+    uint32_t c[3];
+    unpack(in[ip], c);
+    const int s0 = start[c[0] + c[1] + c[2]];
+    uint64_t best = ~0ull;
+    int bj = 0;
+    for (int j = 0; j < k; ++j) {
+      const int dr = (int)c[0] - pal[j].r, dg = (int)c[1] - pal[j].g, db = (int)c[2] - pal[j].b;
+      const uint64_t d = (uint64_t)(dr * dr + dg * dg + db * db);
+      const int t = j - s0;
+      const uint64_t rank = t > 0 ? (uint64_t)(2 * t - 1) : (uint64_t)(-2 * t);
+      const uint64_t key = (d << 32) | rank;
+      if (key < best) { best = key; bj = j; }
+    }
+    out[ip] = ((uint32_t)pal[bj].r << 16) | ((uint32_t)pal[bj].g << 8) | (uint32_t)pal[bj].b;
+  }
+}
+
 // quant_recurse restated (quant_util.cpp:20-158), UW path only, no stdout
 // timer lines: cluster -> first-seen colortable dedup (:93-118) -> map (:139).
 int dqo_quant_recurse(uint32_t n, const uint32_t* in, uint32_t* out,

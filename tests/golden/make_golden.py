@@ -233,6 +233,41 @@ def main():
             wres.append(dict(spec={"w": w, "h": h, "k": k, "kind": "xorshift"}, **rec(out, ct)))
         fx.dump_json("weighted.json", wres)
 
+    # ---- 8. host utilities of the ABI
+    if want("utils"):
+        utils_fixtures(ref)
+
+
+def utils_fixtures(ref):
+    """Host utilities of the ABI: calc_color_table, cut_bits, get_double_scale."""
+    L = ref.lib
+    cct = getattr(L, "_Z16calc_color_tablePKjjPjjjiPi")
+    cct.restype = ctypes.POINTER(ctypes.c_double)
+    cut = getattr(L, "_Z8cut_bitsPKjjPjhhh")
+    cut.restype = None
+    gds = getattr(L, "_Z16get_double_scalePKjj")
+    gds.restype = ctypes.c_double
+    res = {"calc_color_table": [], "cut_bits": [], "get_double_scale": []}
+    for spec in [{"n": 1000, "k": 0, "kind": "ties", "seed": 1}, {"n": 5000, "k": 0, "kind": "coarse", "seed": 2},
+                 {"n": 3000, "k": 0, "kind": "uniform", "seed": 3}, {"n": 777, "k": 0, "kind": "topbyte", "seed": 4}]:
+        px = fx.make_case(spec)
+        out = np.zeros(len(px), np.uint32)
+        nc = ctypes.c_int(0)
+        w = cct(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(out), ctypes.c_uint32(1), ctypes.c_uint32(len(px)),
+                ctypes.c_int(1), ctypes.byref(nc))
+        weights = [w[i] for i in range(nc.value)]
+        res["calc_color_table"].append({"spec": spec, "num_colors": nc.value,
+                                        "colors": [int(v) for v in out[:nc.value]],
+                                        "weights": [float(x).hex() for x in weights]})
+        for bits in [(8, 8, 8), (5, 5, 5), (3, 6, 2), (1, 8, 4)]:
+            o2 = np.zeros(len(px), np.uint32)
+            cut(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(o2), ctypes.c_ubyte(bits[0]),
+                ctypes.c_ubyte(bits[1]), ctypes.c_ubyte(bits[2]))
+            res["cut_bits"].append({"spec": spec, "bits": bits, "out_fnv": "%016x" % fx.fnv(o2)})
+    for n in (1, 2, 3, 10, 49, 65536, 8294400, 268435456):
+        res["get_double_scale"].append([n, float(gds(None, ctypes.c_uint32(n))).hex()])
+    fx.dump_json("utils.json", res)
+
 
 if __name__ == "__main__":
     main()

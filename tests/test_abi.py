@@ -1,0 +1,132 @@
+"""CPU: the drop-in boundary.  libdivquant_hip.so loads, exports every entry
+point include/*.h declares (C linkage by name, C++ linkage by demangled
+signature), its host-only utilities match the reference's outputs
+(tests/golden/utils.json), and compute calls fail loudly without a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import dq_fixtures as fx
+
+ROOT = fx.ROOT
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def declared_functions(header):
+    """Function names declared in a header (prototypes ending with ';')."""
+    text = open(os.path.join(INCLUDE, header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    names = set()
+    for m in re.finditer(r"([A-Za-z_][A-Za-z0-9_]*)\s*\(([^;{}]*)\)\s*;", text):
+        name = m.group(1)
+        if name not in ("if", "while", "for", "return", "sizeof"):
+            names.add(name)
+    return names
+
+
+def exported(lib_path, demangle):
+    out = subprocess.check_output(["nm", "-D", "--defined-only"] + (["-C"] if demangle else []) + [lib_path],
+                                  text=True)
+    return out
+
+
+@pytest.fixture(scope="module")
+def lib(pkg):
+    return pkg.lib()
+
+
+def test_library_loads_and_reports_abi(pkg, lib):
+    assert lib.dq_hip_abi_version() == 1
+    assert os.path.exists(pkg.LIB_PATH)
+
+
+@pytest.mark.parametrize("header", ["dq_hip.h", "quant_util.h"])
+def test_c_linkage_symbols(lib, header):
+    names = declared_functions(header)
+    assert names, header
+    for n in sorted(names):
+        assert hasattr(lib, n), n
+
+
+def test_divquantheader_symbols_cpp_linkage(pkg):
+    """DivQuantHeader.h keeps the reference's C++ linkage (DivQuantHeader.h:52-96)."""
+    names = declared_functions("DivQuantHeader.h")
+    expected = {"start_timer", "stop_timer", "check_mem", "get_double_scale", "timediff",
+                "map_colors_mps", "calc_color_table", "cut_bits", "quant_varpart_fast",
+                "validate_num_bits"}
+    assert names == expected
+    syms = exported(pkg.LIB_PATH, demangle=True)
+    for n in expected:
+        assert re.search(r"\b%s\(" % n, syms), n
+    # and the mangled names are the ones the reference's callers link against
+    raw = exported(pkg.LIB_PATH, demangle=False)
+    for mangled in ["_Z14map_colors_mpsPKjjPjS1_i", "_Z18quant_varpart_fastjPKjPjjjS1_S1_iiii",
+                    "_Z16calc_color_tablePKjjPjjjiPi", "_Z8cut_bitsPKjjPjhhh", "_Z16get_double_scalePKjj",
+                    "_Z17validate_num_bitsh", "_Z11start_timerv", "_Z10stop_timerl", "_Z8timediffll",
+                    "_Z9check_memi"]:
+        assert mangled in raw, mangled
+
+
+def _cpp(lib, mangled, restype, argtypes):
+    fn = getattr(lib, mangled)
+    fn.restype = restype
+    fn.argtypes = argtypes
+    return fn
+
+
+def test_get_double_scale(lib):
+    gds = _cpp(lib, "_Z16get_double_scalePKjj", ctypes.c_double, [ctypes.c_void_p, ctypes.c_uint32])
+    for n, hx in fx.load_json("utils.json")["get_double_scale"]:
+        assert gds(None, n) == float.fromhex(hx)
+
+
+def test_validate_num_bits(lib):
+    v = _cpp(lib, "_Z17validate_num_bitsh", ctypes.c_int, [ctypes.c_ubyte])
+    assert [v(b) for b in range(10)] == [0, 1, 1, 1, 1, 1, 1, 1, 1, 0]
+
+
+def test_cut_bits(lib):
+    cut = _cpp(lib, "_Z8cut_bitsPKjjPjhhh", None,
+               [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_ubyte, ctypes.c_ubyte, ctypes.c_ubyte])
+    for c in fx.load_json("utils.json")["cut_bits"]:
+        px = fx.make_case(c["spec"])
+        out = np.zeros(len(px), np.uint32)
+        cut(fx.vp(px), len(px), fx.vp(out), *c["bits"])
+        assert "%016x" % fx.fnv(out) == c["out_fnv"], c
+
+
+def test_calc_color_table(lib):
+    """Unique colours in the reference's hash-bucket order with count/N weights."""
+    cct = _cpp(lib, "_Z16calc_color_tablePKjjPjjjiPi", ctypes.POINTER(ctypes.c_double),
+               [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                ctypes.c_int, ctypes.POINTER(ctypes.c_int)])
+    for c in fx.load_json("utils.json")["calc_color_table"]:
+        px = fx.make_case(c["spec"])
+        out = np.zeros(len(px), np.uint32)
+        nc = ctypes.c_int(0)
+        w = cct(fx.vp(px), len(px), fx.vp(out), 1, len(px), 1, ctypes.byref(nc))
+        assert nc.value == c["num_colors"]
+        assert [int(v) for v in out[:nc.value]] == c["colors"]
+        assert [float(w[i]).hex() for i in range(nc.value)] == c["weights"]
+
+
+def test_compute_fails_loudly_without_gpu(pkg, lib):
+    if lib.dq_hip_device_count() > 0:
+        pytest.skip("a GPU is visible here")
+    with pytest.raises(pkg.DivQuantError):
+        pkg.quant_recurse(np.arange(16, dtype=np.uint32), 4)
+    with pytest.raises(pkg.DivQuantError):
+        pkg.map_colors_mps(np.arange(16, dtype=np.uint32), np.arange(4, dtype=np.uint32))
+
+
+def test_product_does_not_link_the_oracle(pkg):
+    """The shipped library must not depend on oracle/ (checker only)."""
+    deps = subprocess.check_output(["ldd", pkg.LIB_PATH], text=True)
+    assert "dqoracle" not in deps and "dqref" not in deps
+    syms = exported(pkg.LIB_PATH, demangle=False)
+    assert "dqo_" not in syms

@@ -1,0 +1,73 @@
+"""CPU: build-level guarantees of the gfx950 code object.
+
+* No FP64 contraction: the pass and partition kernels evaluate the
+  reference's decision as separate roundings; a v_fma_f64 there would change
+  results.  (Epilogue kernels contain v_fma_f64 only inside the correctly
+  rounded f64 division sequence: 5 per v_div_fixup_f64.)
+* Global (not flat) memory instructions in the streaming kernels.
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "clusteringsegmentation-1_amd")
+ASM = os.path.join(PKG, "build", "dq_kernels-gfx950.s")
+
+
+@pytest.fixture(scope="module")
+def kernels():
+    subprocess.check_call(["make", "-s", "-C", PKG, "asm"])
+    text = open(ASM).read()
+    funcs = {}
+    for m in re.finditer(r"^(_ZN2dq\w+):.*?^\.Lfunc_end", text, flags=re.S | re.M):
+        funcs[m.group(1)] = m.group(0)
+    assert funcs
+    return funcs
+
+
+def _named(funcs, part):
+    got = {k: v for k, v in funcs.items() if part in k}
+    assert got, part
+    return got
+
+
+def test_no_fp64_contraction_in_decisions(kernels):
+    for name, body in list(_named(kernels, "pass_kernel").items()) + list(_named(kernels, "partition_kernel").items()):
+        assert "v_fma_f64" not in body and "v_fmac_f64" not in body, name
+
+
+def _fma_counts(text):
+    out = {}
+    for m in re.finditer(r"^(_ZN2dq\w+):.*?^\.Lfunc_end", text, flags=re.S | re.M):
+        b = m.group(0)
+        out[m.group(1)] = (len(re.findall(r"v_fmac?_f64", b)), len(re.findall(r"v_div_fixup_f64", b)))
+    return out
+
+
+def test_epilogue_fma_only_in_divisions(kernels, tmp_path):
+    """Every v_fma_f64 of the epilogues belongs to a correctly rounded f64
+    division sequence (<= 5 per v_div_fixup_f64), and a -ffp-contract=fast
+    build of the same source has strictly more: contraction would show."""
+    prod = _fma_counts("\n".join(kernels.values()))
+    fast_s = tmp_path / "fast.s"
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                           "-ffp-contract=fast", "--cuda-device-only", "-S", "-o", str(fast_s),
+                           os.path.join(PKG, "csrc", "dq_kernels.hip")],
+                          stderr=subprocess.DEVNULL)
+    fast = _fma_counts(fast_s.read_text())
+    for name, (nfma, ndiv) in prod.items():
+        if "epilogue_kernel" not in name:
+            continue
+        assert nfma <= 5 * ndiv, (name, nfma, ndiv)
+        if ndiv:
+            assert fast[name][0] > nfma, (name, fast[name], nfma)
+
+
+def test_streaming_kernels_use_global_memory(kernels):
+    for part in ("pass_kernel", "partition_kernel", "map_kernel"):
+        for name, body in _named(kernels, part).items():
+            assert not re.search(r"\bflat_(load|store)", body), name
+            assert re.search(r"global_load_dwordx4", body), name

@@ -99,8 +99,8 @@ int main(int argc, char** argv) {
     std::sort(pal.begin(), pal.end(), [](uint32_t x, uint32_t y) { return ((x>>16)&255)+((x>>8)&255)+(x&255) < ((y>>16)&255)+((y>>8)&255)+(y&255); });
     std::vector<uint16_t> lut(766);
     for (int v = 0; v < 766; ++v) { int best = 0; for (int i = 0; i < k; ++i) { int w = ((pal[i]>>16)&255)+((pal[i]>>8)&255)+(pal[i]&255); if (w <= v) best = i; } lut[v] = best; }
-    uint32_t* d_pal; uint16_t* d_lut; uint4* d_rec; uint16_t* d_idx;
-    CK(hipMalloc(&d_pal, k * 4)); CK(hipMalloc(&d_lut, 766 * 2)); CK(hipMalloc(&d_rec, kCells * 16)); CK(hipMalloc(&d_idx, (size_t)kCells * kCellCap * 2));
+    uint32_t* d_pal; uint16_t* d_lut; uint32_t* d_rec; uint16_t* d_idx;
+    CK(hipMalloc(&d_pal, k * 4)); CK(hipMalloc(&d_lut, 766 * 2)); CK(hipMalloc(&d_rec, kCells * kCellRecWords * 4)); CK(hipMalloc(&d_idx, (size_t)kCells * kCellCap * 2));
     CK(hipMemcpy(d_pal, pal.data(), k * 4, hipMemcpyHostToDevice)); CK(hipMemcpy(d_lut, lut.data(), 766 * 2, hipMemcpyHostToDevice));
     timeit("build_cells k=256", 0, [&] { launch_build_cells(d_pal, k, d_rec, d_idx, 0); });
     timeit("map k=256", N * 8.0, [&] { launch_map(d_px, N, d_p0, d_pal, k, d_lut, d_rec, d_idx, 0); });
