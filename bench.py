@@ -87,27 +87,66 @@ def cpu_baseline(w, h, k):
                       "(host has %d cores)" % (w, h, k, dt, os.cpu_count() or 0)}
 
 
-def main():
-    a = parse()
+def init_dist():
+    """(rank, world, local_rank) from the torchrun environment; one process
+    per GPU over RCCL ("nccl"), or gloo without a GPU (CPU tests)."""
     import torch
     import torch.distributed as dist
-    from __graft_entry__ import load_package
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and not dist.is_initialized():
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    return rank, world, local
+
+
+def frame_seed(rank, frame):
+    """Each rank owns its own frames (weak scaling, no data-path collective)."""
+    return 0x5EED + 1000 * rank + frame
+
+
+def timed_region(step, steps, world, sync):
+    """Barrier + device sync on both sides of exactly `steps` steps."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def max_over_ranks(dt, world, device="cpu"):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return dt
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def main():
+    a = parse()
+    import torch
+    from __graft_entry__ import load_package
+
+    rank, world, local = init_dist()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pkg = load_package()
 
     w, h, k = CONFIGS[a.config]
     n = w * h
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED + 1000 * rank)
-    frames = [torch.randint(0, 1 << 24, (n,), dtype=torch.int32, device=dev, generator=g)
-              for _ in range(a.frames)]
+    frames = []
+    for f in range(a.frames):
+        g = torch.Generator(device=dev)
+        g.manual_seed(frame_seed(rank, f))
+        frames.append(torch.randint(0, 1 << 24, (n,), dtype=torch.int32, device=dev, generator=g))
     outs = [torch.empty_like(f) for f in frames]
     stream = torch.cuda.current_stream(dev)
 
@@ -121,16 +160,7 @@ def main():
         step()
     # --- timed region: no per-launch events (they would perturb the timing)
     pkg.set_timing(False, device=local)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
+    dt = timed_region(step, a.steps, world, lambda: torch.cuda.synchronize(dev))
     # --- roofline region: the same steps again with HIP events around every
     # launch (on the library's launch stream) for per-kernel durations
     timing = not a.no_timing
@@ -146,10 +176,7 @@ def main():
     rounds = pkg.last_rounds(device=local)
     swept = pkg.last_points_swept(device=local)
 
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = max_over_ranks(dt, world, dev)
     total_px = n * a.frames * a.steps * world
     value = total_px / dt / 1e6
 
@@ -191,6 +218,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(w, h, k)
         print(json.dumps(res), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 
