@@ -67,6 +67,8 @@ def lib():
         "dq_hip_last_trace": ([c.c_int, vp, c.c_int], c.c_int),
         "dq_hip_last_rounds": ([c.c_int], c.c_int),
         "dq_hip_last_points_swept": ([c.c_int], c.c_uint64),
+        "dq_hip_last_points_full": ([c.c_int], c.c_uint64),
+        "dq_hip_set_fixed_point": ([c.c_int, c.c_int], None),
         "dq_hip_set_timing": ([c.c_int, c.c_int], None),
         "dq_hip_reset_stats": ([c.c_int], None),
         "dq_hip_get_stat": ([c.c_int, c.c_int, c.POINTER(c.c_uint64), c.POINTER(c.c_double),
@@ -224,6 +226,16 @@ def last_rounds(device=0):
 
 def last_points_swept(device=0):
     return int(lib().dq_hip_last_points_swept(device))
+
+
+def last_points_full(device=0):
+    """Points the last run would have swept with all max_iters iterations."""
+    return int(lib().dq_hip_last_points_full(device))
+
+
+def set_fixed_point(on, device=0):
+    """Fixed-point finalisation of 2-means splits (identical outputs)."""
+    lib().dq_hip_set_fixed_point(device, 1 if on else 0)
 
 
 def set_timing(on, device=0):

@@ -191,6 +191,8 @@ int dq_hip_last_trace(int device, int64_t* trace, int k) {
 int dq_hip_last_rounds(int device) { return engine_for(device).last_rounds; }
 
 uint64_t dq_hip_last_points_swept(int device) { return engine_for(device).last_points_swept; }
+uint64_t dq_hip_last_points_full(int device) { return engine_for(device).last_points_full; }
+void dq_hip_set_fixed_point(int device, int on) { engine_for(device).set_fixed_point(on != 0); }
 
 void dq_hip_set_timing(int device, int on) { engine_for(device).set_timing(on != 0); }
 

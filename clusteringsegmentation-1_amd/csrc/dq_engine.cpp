@@ -36,6 +36,8 @@ int32_t split_threshold(double cut) {
 }  // namespace
 
 Engine::Engine(int device) : device_(device) {
+  const char* full = getenv("DQ_HIP_FULL_ITERS");
+  fixed_point_ = !(full && full[0] == '1');
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   DQ_HIP(hipMalloc((void**)&d_pal_, 16384 * sizeof(uint32_t)));
@@ -207,22 +209,26 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
   ra.tiles = d_tiles_;
   ra.nodes = d_nodes_;
   ra.parts = d_parts_;
+  ra.fixed_point = fixed_point_ ? 1 : 0;
   const double bytes = 4.0 * (double)total;
   const int nt = (int)ntiles;
-  auto pass = [&](int kind, int st) {
+  // 2-means passes (iteration index) whose timing entry gets its swept bytes
+  // once the nodes' done_it are known
+  std::vector<std::pair<size_t, int>> km_events;
+  auto pass = [&](int kind, int st, int it) {
     timed_begin(stream);
     launch_pass(kind, ra, nt, stream);
     timed_end(st, bytes, stream);
+    if (timing_ && it >= 0) km_events.push_back({pending_.size() - 1, it});
     timed_begin(stream);
     launch_epilogue(kind, ra, nn, stream);
     timed_end(ST_EPILOGUE, 0.0, stream);
-    last_points_swept += total;
   };
-  if (root_round) pass(PASS_INIT, ST_INIT);
-  pass(PASS_SPLIT, ST_SPLIT);
+  if (root_round) pass(PASS_INIT, ST_INIT, -1);
+  pass(PASS_SPLIT, ST_SPLIT, -1);
   for (int it = 0; it < max_iters; ++it) {
     const bool last = (it == max_iters - 1);
-    pass(last ? PASS_KLAST : PASS_KMEANS, last ? ST_KLAST : ST_KMEANS);
+    pass(last ? PASS_KLAST : PASS_KMEANS, last ? ST_KLAST : ST_KMEANS, it);
   }
   timed_begin(stream);
   launch_partition(ra, nt, stream);
@@ -230,6 +236,20 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
 
   DQ_HIP(hipMemcpyAsync(h_nodes_, d_nodes_, nn * sizeof(DevNode), hipMemcpyDeviceToHost, stream));
   DQ_HIP(hipStreamSynchronize(stream));
+  // points actually swept: iteration `it` reads a node iff it is not final
+  // before it (done_it == 0, or it < done_it)
+  auto swept_in = [&](int it) {
+    uint64_t px = 0;
+    for (int a = 0; a < nn; ++a) {
+      const DevNode& d = h_nodes_[a];
+      if (d.done_it == 0 || it < d.done_it) px += d.len;
+    }
+    return px;
+  };
+  last_points_full += total * (uint64_t)((root_round ? 2 : 1) + max_iters);
+  last_points_swept += total * (uint64_t)(root_round ? 2 : 1);
+  for (int it = 0; it < max_iters; ++it) last_points_swept += swept_in(it);
+  for (auto& e : km_events) pending_[e.first].bytes = 4.0 * (double)swept_in(e.second);
   collect_timing();
 
   for (int a = 0; a < nn; ++a) {
@@ -362,6 +382,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   nodes_.clear();
   last_rounds = 0;
   last_points_swept = 0;
+  last_points_full = 0;
   size_t total = 0, align_need = 0;
   for (int i = 0; i < nframes; ++i) {
     FrameJob& j = jobs[i];

@@ -100,8 +100,13 @@ class Engine {
   std::vector<int64_t> last_trace;    // (K-1)*4: new_index old_index |C| |new|
   int last_rounds = 0;
   uint64_t last_points_swept = 0;     // sum over passes of points read (all frames)
+  uint64_t last_points_full = 0;      // the same without fixed-point finalisation
 
   void set_timing(bool on) { timing_ = on; }
+  // Finalise a split when its 2-means reaches an exact fixed point (default
+  // on; results are identical either way -- dq_kernels.hip, node_update).
+  void set_fixed_point(bool on) { fixed_point_ = on; }
+  bool fixed_point() const { return fixed_point_; }
   void reset_stats();
   KernelStat stats[ST_COUNT];
 
@@ -131,6 +136,7 @@ class Engine {
   void collect_timing();
 
   int device_ = 0;
+  bool fixed_point_ = true;
   hipStream_t stream_ = nullptr;
   std::mutex mu_;
   bool timing_ = false;

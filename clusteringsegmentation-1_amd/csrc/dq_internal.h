@@ -26,8 +26,9 @@ enum PassKind : int32_t {
 };
 
 // Per-tile partial statistics of the new side (all points in PASS_INIT):
-// plain 32-B stores, exact in u32 because a tile has at most 65536 points
-// (65536 * 255^2 < 2^32).  The node's epilogue sums them in u64.
+// count, sums and sums of squares in every pass; plain 32-B stores, exact in
+// u32 because a tile has at most 65536 points (65536 * 255^2 < 2^32).  The
+// node's epilogue sums them in u64.
 enum PartField : int32_t { F_CNT = 0, F_SR, F_SG, F_SB, F_QR, F_QG, F_QB, F_NUM };
 struct alignas(32) TilePartial {
   uint32_t f[8];
@@ -55,14 +56,22 @@ struct alignas(16) DevNode {
   // --- parameters of the next pass (host for the split pass of non-roots,
   //     otherwise written by the node's epilogue)
   Params prm;
-  // --- results of the node's split (written by the PASS_KLAST epilogue;
+  // --- results of the node's split (written by the PASS_KLAST epilogue, or
+  //     by the PASS_KMEANS epilogue that finds the 2-means at a fixed point;
   //     prm then still holds the last 2-means decision)
   double om[3], nm[3];      // old_mean / new_mean after the last pass
   double nv[3], ov[3];      // new_var / old_var (:836-855)
   double nw, ow;            // new_weight / old_weight
   double tse_old, tse_new;  // (:870-871)
   uint64_t n_new;           // new_size (:820-821)
-  uint64_t pad1;
+  // --- fixed-point detection.  The 2-means state after a pass is the new
+  //     side's exact integer (count, sums): when a pass reproduces the
+  //     previous pass's, every later iteration is bit-identical (same sums ->
+  //     same means -> same decision), so the results are final and the
+  //     remaining passes skip the node.
+  uint64_t prev[4];         // count, sum R, G, B of the previous pass
+  int32_t iter;             // 2-means iterations completed (epilogue count)
+  int32_t done_it;          // 0: active; else 1 + the iteration found at the fixed point
 };
 
 // One workgroup's share of a pass.

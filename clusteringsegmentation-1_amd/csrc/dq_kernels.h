@@ -28,6 +28,7 @@ struct RoundArgs {
   Tile* tiles;
   DevNode* nodes;
   TilePartial* parts;       // one per tile, rewritten by every pass
+  int32_t fixed_point;      // epilogues finalise nodes at a 2-means fixed point
 };
 
 // One statistics pass over every tile of the round (one workgroup per tile).

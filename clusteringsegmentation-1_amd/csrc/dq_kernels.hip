@@ -162,42 +162,84 @@ __device__ __forceinline__ bool goes_new(uint32_t p, const Params& q) {
   return !stays_old(p, q);
 }
 
-// Lane partial sums.  rb = R<<16 | B sums, gc = cnt<<16 | G sums: each half
-// stays < 2^16 because a tile gives a lane at most 256 points.
+// Lane partial sums of the new side: count, sums and sums of squares of the
+// three channels (a lane sees at most 256 points of a tile: all exact in u32).
+// Four masked pixels (0 when not taken) are byte-transposed with v_perm_b32
+// into one R, one G and one B word, then v_dot4_u32_u8 with 0x01010101 sums
+// them and with themselves sums their squares: 7 sums for ~5 ops per point.
 struct LaneSums {
-  uint32_t rb = 0, gc = 0, qr = 0, qg = 0, qb = 0;
+  uint32_t cnt = 0, sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
 };
+
+__device__ __forceinline__ void add4(const uint32_t m[4], LaneSums& s) {
+  const uint32_t u01 = __builtin_amdgcn_perm(m[1], m[0], 0x05010400u);  // B0 B1 G0 G1
+  const uint32_t u23 = __builtin_amdgcn_perm(m[3], m[2], 0x05010400u);  // B2 B3 G2 G3
+  const uint32_t bq = __builtin_amdgcn_perm(u23, u01, 0x05040100u);     // B0 B1 B2 B3
+  const uint32_t gq = __builtin_amdgcn_perm(u23, u01, 0x07060302u);     // G0 G1 G2 G3
+  const uint32_t rq = __builtin_amdgcn_perm(m[1], m[0], 0x0C0C0602u) |  // R0 R1 0 0
+                      __builtin_amdgcn_perm(m[3], m[2], 0x06020C0Cu);   // 0 0 R2 R3
+  s.sr = __builtin_amdgcn_udot4(rq, 0x01010101u, s.sr, false);
+  s.sg = __builtin_amdgcn_udot4(gq, 0x01010101u, s.sg, false);
+  s.sb = __builtin_amdgcn_udot4(bq, 0x01010101u, s.sb, false);
+  s.qr = __builtin_amdgcn_udot4(rq, rq, s.qr, false);
+  s.qg = __builtin_amdgcn_udot4(gq, gq, s.qg, false);
+  s.qb = __builtin_amdgcn_udot4(bq, bq, s.qb, false);
+}
 
 template <int KIND, bool FULL>
 __device__ __forceinline__ void sweep_sums(const u32x4 v[kVecPerThread], uint32_t vs,
                                            uint32_t start, uint32_t end, const Params& q,
                                            LaneSums& s) {
-  constexpr bool kSquares = (KIND == PASS_INIT || KIND == PASS_KLAST);
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
     const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
+    uint32_t m[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const uint32_t p = vec_elem(v[j], e);
       bool take = goes_new<KIND>(p, q);
       if (!FULL) take = take && (i0 + e >= start) && (i0 + e < end);
-      s.rb += take ? (p & 0x00FF00FFu) : 0u;
-      s.gc += take ? (((p >> 8) & 0xFFu) | 0x10000u) : 0u;
-      if (kSquares) {
-        const uint32_t R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
-        s.qr += take ? R * R : 0u;
-        s.qg += take ? G * G : 0u;
-        s.qb += take ? B * B : 0u;
-      }
+      m[e] = take ? p : 0u;
+      s.cnt += take ? 1u : 0u;
     }
+    add4(m, s);
   }
 }
 
+// The split's results from the final partition's sums (:787-871).
+__device__ void node_results(DevNode* w, const uint64_t t[F_NUM], const double om[3],
+                             const double nm[3], double nw, double ow) {
+  const double s = w->s, tw = w->tw;
+  double nv[3], ov[3];
+  for (int c = 0; c < 3; ++c) {                  // (:836-838)
+    double q = (double)t[F_QR + c];
+    q *= s;
+    nv[c] = q / nw - nm[c] * nm[c];
+  }
+  for (int c = 0; c < 3; ++c) {                  // (:845-855)
+    const double dn = nm[c] - w->tm[c];
+    const double dox = om[c] - w->tm[c];
+    ov[c] = ((tw * w->tv[c] - nw * (nv[c] + dn * dn)) / ow) - dox * dox;
+  }
+  for (int c = 0; c < 3; ++c) {
+    w->om[c] = om[c];
+    w->nm[c] = nm[c];
+    w->nv[c] = nv[c];
+    w->ov[c] = ov[c];
+  }
+  w->nw = nw;
+  w->ow = ow;
+  w->tse_old = ow * (ov[0] + ov[1] + ov[2]);   // (:870-871)
+  w->tse_new = nw * (nv[0] + nv[1] + nv[2]);
+  w->n_new = t[F_CNT];
+}
+
 // The FP64 update after pass KIND from the node's total sums t[] (exact
-// integers).  Publishes the next pass's Params, or after PASS_KLAST the
-// split's results, in DevNode.
+// integers).  Publishes the next pass's Params, or the split's results.
+// Returns true when the results are final (PASS_KLAST, or a PASS_KMEANS at a
+// fixed point: prm then already holds the decision that produced them).
 template <int KIND>
-__device__ void node_update(DevNode* w, const uint64_t t[F_NUM]) {
+__device__ bool node_update(DevNode* w, const uint64_t t[F_NUM], bool fixed_point) {
   const double s = w->s, tw = w->tw;
   if (KIND == PASS_INIT) {
     // DivQuantClusterInitMeanAndVar (:90-104), then the cut (:388-403).
@@ -219,42 +261,31 @@ __device__ void node_update(DevNode* w, const uint64_t t[F_NUM]) {
     if (maxv < tv[2]) { axis = 2; cut = tm[2]; }
     w->prm.thr = split_threshold(cut);
     w->prm.shift = 16 - 8 * axis;
-    return;
+    return false;
   }
   double tm[3];
   for (int c = 0; c < 3; ++c) tm[c] = w->tm[c];
   double om[3], nm[3], nw, ow;
+  if (KIND == PASS_KMEANS) {
+    w->iter += 1;
+    if (fixed_point && t[F_CNT] == w->prev[0] && t[F_SR] == w->prev[1] &&
+        t[F_SG] == w->prev[2] && t[F_SB] == w->prev[3]) {
+      means_from_sums(t, s, tw, tm, om, nm, &nw, &ow);
+      node_results(w, t, om, nm, nw, ow);
+      w->done_it = w->iter;
+      return true;
+    }
+  }
   means_from_sums(t, s, tw, tm, om, nm, &nw, &ow);
   if (KIND == PASS_SPLIT || KIND == PASS_KMEANS) {
+    for (int c = 0; c < 4; ++c) w->prev[c] = t[F_CNT + c];
     Params p = w->prm;
     decision_from_means(om, nm, &p);
     w->prm = p;
-    return;
+    return false;
   }
-  // PASS_KLAST: the split's results (:787-871).  prm keeps the last decision
-  // (the partition replays it).
-  double nv[3], ov[3];
-  for (int c = 0; c < 3; ++c) {                  // (:836-838)
-    double q = (double)t[F_QR + c];
-    q *= s;
-    nv[c] = q / nw - nm[c] * nm[c];
-  }
-  for (int c = 0; c < 3; ++c) {                  // (:845-855)
-    const double dn = nm[c] - tm[c];
-    const double dox = om[c] - tm[c];
-    ov[c] = ((tw * w->tv[c] - nw * (nv[c] + dn * dn)) / ow) - dox * dox;
-  }
-  for (int c = 0; c < 3; ++c) {
-    w->om[c] = om[c];
-    w->nm[c] = nm[c];
-    w->nv[c] = nv[c];
-    w->ov[c] = ov[c];
-  }
-  w->nw = nw;
-  w->ow = ow;
-  w->tse_old = ow * (ov[0] + ov[1] + ov[2]);   // (:870-871)
-  w->tse_new = nw * (nv[0] + nv[1] + nv[2]);
-  w->n_new = t[F_CNT];
+  node_results(w, t, om, nm, nw, ow);   // PASS_KLAST
+  return true;
 }
 
 }  // namespace
@@ -268,10 +299,10 @@ template <int KIND>
 __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const DevNode& nd = a.nodes[t.node];
+  if ((KIND == PASS_KMEANS || KIND == PASS_KLAST) && nd.done_it != 0) return;   // final
   g_cu4* src4 = as_g4(nd.src);
   const Params q = nd.prm;
-  constexpr bool kSquares = (KIND == PASS_INIT || KIND == PASS_KLAST);
-  constexpr int kNF = kSquares ? 7 : 4;
+  constexpr int kNF = F_NUM;
 
   __shared__ uint32_t red[kBlock / 64][8];
   LaneSums s;
@@ -286,7 +317,7 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
     }
   }
 
-  uint32_t f[8] = {s.gc >> 16, s.rb >> 16, s.gc & 0xFFFF, s.rb & 0xFFFF, s.qr, s.qg, s.qb, 0};
+  uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
 #pragma unroll
   for (int k = 0; k < kNF; ++k) f[k] = wave_sum_u32(f[k]);
   if (lane_id() == 0) {
@@ -307,9 +338,10 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
 template <int KIND>
 __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
   DevNode* w = a.nodes + blockIdx.x;
+  if ((KIND == PASS_KMEANS || KIND == PASS_KLAST) && w->done_it != 0) return;   // final
   const int tb = w->tile_begin, te = w->tile_end;
-  constexpr bool kSquares = (KIND == PASS_INIT || KIND == PASS_KLAST);
-  constexpr int kNF = kSquares ? 7 : 4;
+  constexpr bool kSquares = true;
+  constexpr int kNF = F_NUM;
   const g_cu4* parts4 = (const g_cu4*)a.parts;
 
   uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -346,14 +378,16 @@ __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
 #pragma unroll
     for (int k = 0; k < kNF; ++k) red[wave_id()][k] = acc[k];
   }
-  __syncthreads();
+  __shared__ int final_results;
+  __syncthreads();   // (every thread has read done_it above)
   if (threadIdx.x == 0) {
     uint64_t tot[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
     for (int k = 0; k < kNF; ++k)
       for (int v = 0; v < kBlock / 64; ++v) tot[k] += red[v][k];
-    node_update<KIND>(w, tot);
+    final_results = node_update<KIND>(w, tot, a.fixed_point != 0) ? 1 : 0;
   }
-  if (KIND == PASS_KLAST) {
+  __syncthreads();
+  if ((KIND == PASS_KMEANS || KIND == PASS_KLAST) && final_results) {
     // Each tile's first OLD point's rank among the node's old points: an
     // exclusive scan of the tiles' old counts, chunked per lane.
     __shared__ uint32_t scan[kBlock];
@@ -458,8 +492,9 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
 // Map, step 1: per colour cell (8x8x8 values), the palette entries whose
 // minimum distance to the cell does not exceed the smallest maximum distance
 // of any entry to the cell.  Every exact argmin for a colour of the cell is
-// among them (ties included: <=).  One LANE per cell: the palette is read from
-// LDS by broadcast (every lane the same entry, no bank conflicts).
+// among them (ties included: <=).  One WAVE per cell: lanes stride the palette
+// (coalesced), a wave min gives the bound, ballots compact the candidates in
+// palette order.
 // Record (16 B): x[15:0] count c; x[31:16], y, z, w: the first kCellInline
 // candidates' sorted indices (u16), unused slots = k (a sentinel entry that is
 // farther than any real one); c > kCellInline: all c indices in
@@ -467,11 +502,9 @@ __global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
 __global__ __launch_bounds__(kBlock) void build_cells_kernel(
     const uint32_t* __restrict__ pal, int k, uint32_t* __restrict__ cell_rec,
     uint16_t* __restrict__ cell_idx) {
-  extern __shared__ uint32_t spal[];
-  for (int i = threadIdx.x; i < k; i += kBlock) spal[i] = pal[i];
-  __syncthreads();
-  const uint32_t cell = blockIdx.x * kBlock + threadIdx.x;
-  if (cell >= (uint32_t)kCells) return;
+  __shared__ uint16_t srec[kBlock / 64][8];
+  const uint32_t lane = lane_id(), w = wave_id();
+  const uint32_t cell = blockIdx.x * (kBlock / 64) + w;   // grid = kCells / 4: always valid
   const int cw = 1 << (8 - kCellBits);
   const int lo0 = (int)(cell >> (2 * kCellBits)) * cw;
   const int lo1 = (int)((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
@@ -482,37 +515,43 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(
     const int x = v < lo ? lo - v : (v > hi ? v - hi : 0);
     return x * x;
   };
+  g_cu32* gp = as_g(pal);
   int bound = 0x7FFFFFFF;
-  for (int e = 0; e < k; ++e) {
-    const uint32_t q = spal[e];
-    const int d = far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) +
-                  far2(q & 0xFF, lo2, hi2);
-    bound = min(bound, d);
+  for (int e = (int)lane; e < k; e += 64) {
+    const uint32_t q = gp[e];
+    bound = min(bound, far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) +
+                           far2(q & 0xFF, lo2, hi2));
   }
-  uint32_t count = 0;
-  uint32_t inl[kCellInline];
 #pragma unroll
-  for (int m = 0; m < kCellInline; ++m) inl[m] = (uint32_t)k;
+  for (int o = 32; o >= 1; o >>= 1) bound = min(bound, __shfl_xor(bound, o, 64));
+  if (lane < 8) srec[w][lane] = (uint16_t)k;
   uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
-  for (int e = 0; e < k; ++e) {
-    const uint32_t q = spal[e];
-    const int d = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
-                  near2(q & 0xFF, lo2, hi2);
-    if (d <= bound) {
-      if (count < (uint32_t)kCellCap) lst[count] = (uint16_t)e;
-#pragma unroll
-      for (int m = 0; m < kCellInline; ++m)
-        if (count == (uint32_t)m) inl[m] = (uint32_t)e;
-      ++count;
+  uint32_t count = 0;
+  for (int base = 0; base < k; base += 64) {
+    const int e = base + (int)lane;
+    bool cand = false;
+    if (e < k) {
+      const uint32_t q = gp[e];
+      cand = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
+                 near2(q & 0xFF, lo2, hi2) <= bound;
     }
+    const uint64_t m = __ballot(cand);
+    const uint32_t pos = count + mbcnt64(m);
+    if (cand && pos < (uint32_t)kCellCap) lst[pos] = (uint16_t)e;
+    if (cand && pos < (uint32_t)kCellInline) srec[w][1 + pos] = (uint16_t)e;
+    count += (uint32_t)__popcll(m);
   }
-  uint4 r;
-  const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
-  r.x = c | (inl[0] << 16);
-  r.y = inl[1] | (inl[2] << 16);
-  r.z = inl[3] | (inl[4] << 16);
-  r.w = inl[5] | (inl[6] << 16);
-  reinterpret_cast<uint4*>(cell_rec)[cell] = r;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) {
+    const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
+    uint4 r;
+    r.x = c | ((uint32_t)srec[w][1] << 16);
+    r.y = srec[w][2] | ((uint32_t)srec[w][3] << 16);
+    r.z = srec[w][4] | ((uint32_t)srec[w][5] << 16);
+    r.w = srec[w][6] | ((uint32_t)srec[w][7] << 16);
+    reinterpret_cast<uint4*>(cell_rec)[cell] = r;
+  }
 }
 
 // Map, step 2.  The answer is the entry minimising (squared distance, MPS
@@ -520,86 +559,126 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(
 // s+1, s-1, s+2, s-2, ...: rank(j) = 2(j-s)-1 for j > s, 2(s-j) otherwise.
 // That entry is exactly what map_colors_mps returns (strict '<' keeps the
 // first visited; the floor(d^2/3) pruning never drops a strictly closer
-// entry).  Fast path: d = |p|^2 + |c|^2 - 2 p.c (v_dot4_u32_u8) over the
-// cell's inline candidates, palette entries (colour, |c|^2 | j<<18) in LDS;
-// the rank is only needed when the minimum distance is shared or the cell
-// overflows, which takes a wave-uniform slow path.
+// entry).  One 32-bit key per candidate carries both, exactly:
+//   d'  = (|c|^2 + 2^19) - 2 p.c  = d - |p|^2 + 2^19, in (0, 2^20)  (v_dot4)
+//   sad = |4j - (4s+1)| = 2 rank(j) + 1 < 2^12           (v_sad_u16; K<=1024 here)
+//   key = d' << 12 | sad;  the minimum key's j = the answer.
+// j is recovered from sad (4j = 4s+1 +- sad).  Inline candidates are
+// branch-free; only cells with more than kCellInline candidates take a
+// wave-uniform slow path over their list.
+constexpr int kMapPx = 8;   // pixels per lane per iteration (two 16-B loads)
+
+template <bool kWide>
+__device__ __forceinline__ uint32_t entry_from_sad(uint32_t S, uint32_t sad) {
+  const uint32_t x = S + sad;
+  return (x & 3u) == 0 ? (x >> 2) : ((S - sad) >> 2);
+}
+
+template <bool kWide>
 __global__ __launch_bounds__(kBlock) void map_kernel(
     const uint32_t* __restrict__ in, uint32_t n, uint32_t* __restrict__ out,
     const uint32_t* __restrict__ pal, int k, const uint16_t* __restrict__ lut,
     const uint32_t* __restrict__ cell_rec, const uint16_t* __restrict__ cell_idx) {
   extern __shared__ uint32_t smem[];
-  uint2* spal = reinterpret_cast<uint2*>(smem);              // k+1 entries
+  uint2* spal = reinterpret_cast<uint2*>(smem);              // k+1: colour, |c|^2 + 2^19
   uint16_t* slut = reinterpret_cast<uint16_t*>(smem + 2 * (k + 1));
   for (int i = threadIdx.x; i <= k; i += kBlock) {
     const uint32_t q = i < k ? pal[i] : 0u;
-    const uint32_t c2 = i < k ? __builtin_amdgcn_udot4(q, q, 0u, false) : 0x3FFFFu;
-    spal[i] = make_uint2(q, c2 | ((uint32_t)i << 18));
+    // the sentinel (index k, unused inline slots) has d' = 2^20 - 1: it never wins
+    const uint32_t c2 = i < k ? __builtin_amdgcn_udot4(q, q, 0u, false) + (1u << 19) : 0xFFFFFu;
+    spal[i] = make_uint2(q, c2);
   }
   for (int i = threadIdx.x; i < 766; i += kBlock) slut[i] = lut[i];
   __syncthreads();
   g_cu4* rec4 = (g_cu4*)cell_rec;
+  g_cu4* in4 = (g_cu4*)in;
+  typedef __attribute__((address_space(1))) u32x4 g_u4;
 
-  auto map_one = [&](uint32_t p) -> uint32_t {
-    p &= 0xFFFFFF;
-    const uint32_t R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
-    const uint32_t cell = ((R >> (8 - kCellBits)) << (2 * kCellBits)) |
-                          ((G >> (8 - kCellBits)) << kCellBits) | (B >> (8 - kCellBits));
-    const uint32_t pp = __builtin_amdgcn_udot4(p, p, 0u, false);
-    const u32x4 r = rec4[cell];
-    const uint32_t idx[kCellInline] = {r[0] >> 16, r[1] & 0xFFFF, r[1] >> 16, r[2] & 0xFFFF,
-                                       r[2] >> 16, r[3] & 0xFFFF, r[3] >> 16};
-    uint32_t best = 0xFFFFFFFFu, bc = 0;
-    bool tie = false;
-#pragma unroll
-    for (int m = 0; m < kCellInline; ++m) {
-      const uint2 e = spal[idx[m]];
-      const uint32_t d = (e.y & 0x3FFFFu) + pp - 2u * __builtin_amdgcn_udot4(p, e.x, 0u, false);
-      const bool lt = d < best;
-      tie = lt ? false : (tie || d == best);
-      best = lt ? d : best;
-      bc = lt ? e.x : bc;
-    }
-    const uint32_t cnt = r[0] & 0xFFFF;
-    const bool slow = tie || cnt > (uint32_t)kCellInline;
-    if (__any(slow)) {
-      if (slow) {
-        // exact key (d << 32) | rank over every candidate (the list has them all)
-        const int s0 = slut[R + G + B];
-        uint64_t bkey = ~0ull;
-        auto ev = [&](int j) {
-          const uint2 e = spal[j];
-          const uint32_t d = (e.y & 0x3FFFFu) + pp - 2u * __builtin_amdgcn_udot4(p, e.x, 0u, false);
-          const int tt = j - s0;
-          const uint32_t rank = tt > 0 ? (uint32_t)(2 * tt - 1) : (uint32_t)(-2 * tt);
-          const uint64_t key = ((uint64_t)d << 32) | rank;
-          if (key < bkey) { bkey = key; bc = e.x; }
-        };
-        if (cnt == kCellBrute) {
-          for (int j = 0; j < k; ++j) ev(j);
-        } else {
-          const uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
-          for (uint32_t m = 0; m < cnt; ++m) ev(lst[m]);
-        }
-      }
-    }
-    return bc;
+  // exact (d, rank) key of palette entry j for pixel p (S = 4 s + 1)
+  auto full_key = [&](uint32_t p, uint32_t S, uint32_t j) -> uint64_t {
+    const uint2 en = spal[j];
+    const uint32_t d = (uint32_t)((int32_t)en.y - 2 * (int32_t)__builtin_amdgcn_udot4(p, en.x, 0u, false));
+    const uint32_t sad = __builtin_amdgcn_sad_u16(4u * j, S, 0u);
+    return kWide ? (((uint64_t)d << 32) | sad) : (uint64_t)((d << 12) | sad);
   };
 
-  const uint32_t nvec = n / 4;
-  g_cu4* in4 = (g_cu4*)in;
+  const uint32_t ngrp = n / kMapPx;
   const uint32_t stride = gridDim.x * kBlock;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride) {
-    const u32x4 p = in4[i];
-    uint4 o;
-    o.x = map_one(p[0]);
-    o.y = map_one(p[1]);
-    o.z = map_one(p[2]);
-    o.w = map_one(p[3]);
-    reinterpret_cast<uint4*>(out)[i] = o;
+  for (uint32_t g = blockIdx.x * kBlock + threadIdx.x;; g += stride) {
+    const bool have = g < ngrp;
+    if (!__any(have)) break;
+    uint32_t px[kMapPx];
+    {
+      const u32x4 a = have ? in4[2 * g] : (u32x4){0u, 0u, 0u, 0u};
+      const u32x4 b = have ? in4[2 * g + 1] : (u32x4){0u, 0u, 0u, 0u};
+      for (int e = 0; e < 4; ++e) { px[e] = a[e] & 0xFFFFFFu; px[4 + e] = b[e] & 0xFFFFFFu; }
+    }
+    uint32_t cell[kMapPx];
+    u32x4 r[kMapPx];
+#pragma unroll
+    for (int e = 0; e < kMapPx; ++e) {   // issue every gather before using any
+      const uint32_t p = px[e];
+      cell[e] = ((p >> (24 - kCellBits)) << (2 * kCellBits)) |
+                (((p >> (16 - kCellBits)) & ((1u << kCellBits) - 1)) << kCellBits) |
+                ((p >> (8 - kCellBits)) & ((1u << kCellBits) - 1));
+      r[e] = rec4[cell[e]];
+    }
+    uint32_t res[kMapPx];
+    bool over[kMapPx];
+    uint32_t Ss[kMapPx];
+#pragma unroll
+    for (int e = 0; e < kMapPx; ++e) {
+      const uint32_t p = px[e];
+      const uint32_t S = 4u * slut[((p >> 16) & 0xFF) + ((p >> 8) & 0xFF) + (p & 0xFF)] + 1u;
+      Ss[e] = S;
+      const uint32_t idx[kCellInline] = {r[e][0] >> 16, r[e][1] & 0xFFFF, r[e][1] >> 16,
+                                         r[e][2] & 0xFFFF, r[e][2] >> 16, r[e][3] & 0xFFFF,
+                                         r[e][3] >> 16};
+      uint64_t best = ~0ull;
+#pragma unroll
+      for (int m = 0; m < kCellInline; ++m) {
+        const uint64_t key = full_key(p, S, idx[m]);
+        best = key < best ? key : best;
+      }
+      const uint32_t sad = (uint32_t)(kWide ? (best & 0xFFFFFFFFull) : (best & 0xFFFu));
+      res[e] = spal[entry_from_sad<kWide>(S, sad)].x;
+      over[e] = (r[e][0] & 0xFFFF) > (uint32_t)kCellInline;
+    }
+    bool any_over = false;
+#pragma unroll
+    for (int e = 0; e < kMapPx; ++e) any_over |= over[e];
+    if (__any(any_over)) {
+#pragma unroll
+      for (int e = 0; e < kMapPx; ++e) {
+        if (!over[e]) continue;
+        const uint32_t p = px[e], S = Ss[e];
+        const uint32_t cnt = r[e][0] & 0xFFFF;
+        uint64_t best = ~0ull;
+        if (cnt == kCellBrute) {
+          for (int j = 0; j < k; ++j) { const uint64_t key = full_key(p, S, (uint32_t)j); best = key < best ? key : best; }
+        } else {
+          const uint16_t* lst = cell_idx + (size_t)cell[e] * kCellCap;
+          for (uint32_t m = 0; m < cnt; ++m) { const uint64_t key = full_key(p, S, lst[m]); best = key < best ? key : best; }
+        }
+        const uint32_t sad = (uint32_t)(kWide ? (best & 0xFFFFFFFFull) : (best & 0xFFFu));
+        res[e] = spal[entry_from_sad<kWide>(S, sad)].x;
+      }
+    }
+    if (have) {
+      ((g_u4*)as_gw(out))[2 * g] = (u32x4){res[0], res[1], res[2], res[3]};
+      ((g_u4*)as_gw(out))[2 * g + 1] = (u32x4){res[4], res[5], res[6], res[7]};
+    }
   }
-  const uint32_t tail = nvec * 4 + blockIdx.x * kBlock + threadIdx.x;
-  if (blockIdx.x == 0 && tail < n) out[tail] = map_one(in[tail]);
+  // tail (n % kMapPx points): block 0, one point per lane, whole palette
+  const uint32_t t = ngrp * kMapPx + threadIdx.x;
+  if (blockIdx.x == 0 && t < n) {
+    const uint32_t p = in[t] & 0xFFFFFFu;
+    const uint32_t S = 4u * slut[((p >> 16) & 0xFF) + ((p >> 8) & 0xFF) + (p & 0xFF)] + 1u;
+    uint64_t best = ~0ull;
+    for (int j = 0; j < k; ++j) { const uint64_t key = full_key(p, S, (uint32_t)j); best = key < best ? key : best; }
+    const uint32_t sad = (uint32_t)(kWide ? (best & 0xFFFFFFFFull) : (best & 0xFFFu));
+    out[t] = spal[entry_from_sad<kWide>(S, sad)].x;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -633,8 +712,8 @@ void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream) {
 
 void launch_build_cells(const uint32_t* pal_sorted, int k, uint32_t* cell_rec,
                         uint16_t* cell_idx, hipStream_t stream) {
-  const int blocks = kCells / kBlock;
-  build_cells_kernel<<<dim3(blocks), dim3(kBlock), (size_t)k * 4, stream>>>(
+  static_assert(kCells % (kBlock / 64) == 0, "one wave per cell");
+  build_cells_kernel<<<dim3(kCells / (kBlock / 64)), dim3(kBlock), 0, stream>>>(
       pal_sorted, k, cell_rec, cell_idx);
 }
 
@@ -644,11 +723,15 @@ void launch_map(const uint32_t* in, uint32_t n, uint32_t* out,
                 hipStream_t stream) {
   if (n == 0) return;
   const size_t lds = (size_t)(k + 1) * 8 + 768 * 2;
-  uint32_t blocks = (n / 4 + kBlock - 1) / kBlock;
+  uint32_t blocks = (n / kMapPx + kBlock - 1) / kBlock;
   if (blocks > 2048) blocks = 2048;
   if (blocks == 0) blocks = 1;
-  map_kernel<<<dim3(blocks), dim3(kBlock), lds, stream>>>(in, n, out, pal_sorted, k, lut_init,
-                                                         cell_rec, cell_idx);
+  if (k <= 1024)   // 12-bit rank field in the 32-bit key
+    map_kernel<false><<<dim3(blocks), dim3(kBlock), lds, stream>>>(in, n, out, pal_sorted, k,
+                                                                  lut_init, cell_rec, cell_idx);
+  else
+    map_kernel<true><<<dim3(blocks), dim3(kBlock), lds, stream>>>(in, n, out, pal_sorted, k,
+                                                                 lut_init, cell_rec, cell_idx);
 }
 
 }  // namespace dq

@@ -67,6 +67,15 @@ int dq_hip_last_trace(int device, int64_t *trace, int k);
 int dq_hip_last_rounds(int device);
 /* Points read by all statistics passes of the last clustering. */
 uint64_t dq_hip_last_points_swept(int device);
+/* Points the last run would have swept without fixed-point finalisation
+ * (every split: split pass + max_iters 2-means passes, as the reference). */
+uint64_t dq_hip_last_points_full(int device);
+/* Fixed-point finalisation (default on; DQ_HIP_FULL_ITERS=1 turns the default
+ * off).  A split whose 2-means pass reproduces the previous pass's exact
+ * integer sums is final: the remaining iterations of the reference's loop
+ * (DivQuantCluster.cpp:613) would recompute the same means and decision.
+ * Outputs are identical either way; only the swept points differ. */
+void dq_hip_set_fixed_point(int device, int on);
 
 /* ---- per-kernel timing (HIP events on the launch stream) -----------------
  * kinds: 0 init pass, 1 split pass, 2 2-means pass, 3 last 2-means pass,

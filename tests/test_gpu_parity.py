@@ -199,3 +199,51 @@ def test_repeatable(gpu):
     r = [_quant_dev(gpu, px, 256) for _ in range(3)]
     for out, ct in r[1:]:
         assert np.array_equal(out, r[0][0]) and np.array_equal(ct, r[0][1])
+
+
+@pytest.mark.parametrize("max_iters", [1, 2, 3, 5, 10, 17])
+def test_max_iters_vs_oracle(gpu, max_iters):
+    """The iteration count is part of the algorithm (:613): every max_iters,
+    with fixed-point finalisation on, against the oracle's full loop."""
+    import torch
+    for seed, (n, k) in enumerate([(70001, 16), (250000, 256), (9000, 1024)]):
+        px = fx.xorshift(n, seed=1000 + seed)
+        if seed == 2:
+            px &= 0xE0E0E0
+        t = torch.from_numpy(px.view(np.int32)).to("cuda:0")
+        ct, _ = gpu.cluster_device(t, k, max_iters=max_iters)
+        ref_ct, ref_means, ref_sizes, ref_trace = _oracle_cluster(px, k, max_iters=max_iters)
+        assert np.array_equal(ct, ref_ct), (max_iters, n, k)
+        assert np.array_equal(gpu.last_trace(k), ref_trace), (max_iters, n, k)
+        means, sizes = gpu.last_centroids(k)
+        filled = sizes > 0
+        assert np.array_equal(means[filled].view(np.uint64), ref_means[filled].view(np.uint64))
+
+
+def test_fixed_point_finalisation_is_exact(gpu):
+    """Finalising a split when its 2-means pass reproduces the previous pass's
+    exact sums gives the same outputs as running every iteration, and sweeps
+    fewer points (uniform data: the axis-mean cut is already the bisector)."""
+    cases = [fx.xorshift(1 << 20, seed=21), fx.xorshift(300000, seed=22) & 0xF8FCF8]
+    for name in ("batman", "cookie"):
+        cases.append(fx.load_png_u32(fx.os.path.join(fx.GOLDEN, "png", name + ".png"))[0])
+    try:
+        for px in cases:
+            for k in (16, 256):
+                gpu.set_fixed_point(False)
+                a_out, a_ct = _quant_dev(gpu, px, k)
+                a_trace = gpu.last_trace(k)
+                a_means, _ = gpu.last_centroids(k)
+                full_swept, full = gpu.last_points_swept(), gpu.last_points_full()
+                assert full_swept == full
+                gpu.set_fixed_point(True)
+                b_out, b_ct = _quant_dev(gpu, px, k)
+                assert np.array_equal(a_out, b_out) and np.array_equal(a_ct, b_ct)
+                assert np.array_equal(gpu.last_trace(k), a_trace)
+                b_means, _ = gpu.last_centroids(k)
+                assert np.array_equal(np.nan_to_num(a_means).view(np.uint64),
+                                      np.nan_to_num(b_means).view(np.uint64))
+                assert gpu.last_points_full() == full
+                assert gpu.last_points_swept() < full
+    finally:
+        gpu.set_fixed_point(True)

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <vector>
 #include "../clusteringsegmentation-1_amd/csrc/dq_kernels.hip"
+#include <algorithm>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 using namespace dq;
@@ -23,6 +24,7 @@ __global__ void read_kernel(const uint4* __restrict__ p, size_t n4, uint32_t* ou
 int main(int argc, char** argv) {
   const size_t N = argc > 1 ? strtoull(argv[1], 0, 10) : 3840 * 2160;
   const int reps = argc > 2 ? atoi(argv[2]) : 20;
+  const char* only = argc > 3 ? argv[3] : "";
   uint32_t *d_px, *d_p0, *d_out;
   CK(hipMalloc(&d_px, N * 4 + 64));
   CK(hipMalloc(&d_p0, N * 4 + 64));
@@ -43,12 +45,12 @@ int main(int argc, char** argv) {
     double us = ms * 1e3 / reps;
     printf("%-40s %9.2f us  %8.1f GB/s\n", name, us, bytes / (us * 1e-6) / 1e9);
   };
-  for (int g : {1024, 2048, 4096, 8192}) {
+  if (!strcmp(only, "") || !strcmp(only, "read")) for (int g : {1024, 2048, 4096, 8192}) {
     char nm[64]; snprintf(nm, 64, "read uint4 grid=%d", g);
     timeit(nm, N * 4.0, [&] { read_kernel<<<g, 256>>>((const uint4*)d_px, N / 4, d_out); });
   }
   // one node covering all points, tiles of tl points
-  for (uint32_t tl : {4096u, 8192u, 16384u, 32768u, 65536u}) {
+  if (!strcmp(only, "") || !strcmp(only, "pass")) for (uint32_t tl : {4096u, 8192u, 16384u, 32768u, 65536u}) {
     const int nt = (int)((N + tl - 1) / tl);
     std::vector<Tile> tiles(nt);
     for (int i = 0; i < nt; ++i) { tiles[i].node = 0; tiles[i].start = i * tl; tiles[i].end = std::min<size_t>(N, (size_t)(i + 1) * tl); tiles[i].old_base = 0; }
@@ -91,19 +93,51 @@ int main(int argc, char** argv) {
   }
   // memcpy-only baseline for the node reset
   timeit("hipMemcpyAsync node only", 0, [&] { DevNode x; hipMemcpyAsync(d_out, &x, 16, hipMemcpyHostToDevice, 0); });
-  // map with a 256-entry random palette
-  {
-    const int k = 256;
-    std::vector<uint32_t> pal(k);
-    for (int i = 0; i < k; ++i) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; pal[i] = s & 0xFFFFFF; }
-    std::sort(pal.begin(), pal.end(), [](uint32_t x, uint32_t y) { return ((x>>16)&255)+((x>>8)&255)+(x&255) < ((y>>16)&255)+((y>>8)&255)+(y&255); });
-    std::vector<uint16_t> lut(766);
-    for (int v = 0; v < 766; ++v) { int best = 0; for (int i = 0; i < k; ++i) { int w = ((pal[i]>>16)&255)+((pal[i]>>8)&255)+(pal[i]&255); if (w <= v) best = i; } lut[v] = best; }
-    uint32_t* d_pal; uint16_t* d_lut; uint32_t* d_rec; uint16_t* d_idx;
-    CK(hipMalloc(&d_pal, k * 4)); CK(hipMalloc(&d_lut, 766 * 2)); CK(hipMalloc(&d_rec, kCells * kCellRecWords * 4)); CK(hipMalloc(&d_idx, (size_t)kCells * kCellCap * 2));
-    CK(hipMemcpy(d_pal, pal.data(), k * 4, hipMemcpyHostToDevice)); CK(hipMemcpy(d_lut, lut.data(), 766 * 2, hipMemcpyHostToDevice));
-    timeit("build_cells k=256", 0, [&] { launch_build_cells(d_pal, k, d_rec, d_idx, 0); });
-    timeit("map k=256", N * 8.0, [&] { launch_map(d_px, N, d_p0, d_pal, k, d_lut, d_rec, d_idx, 0); });
+  // map: random K=256, random K=1024, clustered K=256 palettes; output checked
+  // on a sample against the exact (distance, MPS rank) argmin on the host
+  if (!strcmp(only, "") || !strcmp(only, "map")) {
+    std::vector<uint32_t> outh(N);
+    for (int variant = 0; variant < 3; ++variant) {
+      const int k = variant == 1 ? 1024 : 256;
+      std::vector<uint32_t> pal(k);
+      for (int i = 0; i < k; ++i) {
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        pal[i] = variant == 2 ? (0x404040u + (uint32_t)(s & 0x3F3F3F)) : (uint32_t)(s & 0xFFFFFF);
+      }
+      auto sum = [](uint32_t x) { return ((x >> 16) & 255) + ((x >> 8) & 255) + (x & 255); };
+      std::stable_sort(pal.begin(), pal.end(), [&](uint32_t x, uint32_t y) { return sum(x) < sum(y); });
+      std::vector<uint16_t> lut(766);
+      for (int v = 0; v < 766; ++v) { int best = 0; for (int i = 0; i < k; ++i) if ((int)sum(pal[i]) <= v) best = i; lut[v] = best; }
+      uint32_t* d_pal; uint16_t* d_lut; uint32_t* d_rec; uint16_t* d_idx;
+      CK(hipMalloc(&d_pal, k * 4)); CK(hipMalloc(&d_lut, 766 * 2)); CK(hipMalloc(&d_rec, kCells * kCellRecWords * 4)); CK(hipMalloc(&d_idx, (size_t)kCells * kCellCap * 2));
+      CK(hipMemcpy(d_pal, pal.data(), k * 4, hipMemcpyHostToDevice)); CK(hipMemcpy(d_lut, lut.data(), 766 * 2, hipMemcpyHostToDevice));
+      char nm[80];
+      snprintf(nm, 80, "build_cells k=%d %s", k, variant == 2 ? "clustered" : "random");
+      timeit(nm, 0, [&] { launch_build_cells(d_pal, k, d_rec, d_idx, 0); });
+      snprintf(nm, 80, "map k=%d %s", k, variant == 2 ? "clustered" : "random");
+      timeit(nm, N * 8.0, [&] { launch_map(d_px, N, d_p0, d_pal, k, d_lut, d_rec, d_idx, 0); });
+      CK(hipMemcpy(outh.data(), d_p0, N * 4, hipMemcpyDeviceToHost));
+      size_t bad = 0, checked = 0;
+      for (size_t i = 0; i < N; i += (i < N - 64 ? 97 : 1)) {
+        const uint32_t p = h[i];
+        const int s0 = lut[sum(p)];
+        uint64_t best = ~0ull; uint32_t ans = 0;
+        for (int j = 0; j < k; ++j) {
+          const int dr = (int)((p >> 16) & 255) - (int)((pal[j] >> 16) & 255), dg = (int)((p >> 8) & 255) - (int)((pal[j] >> 8) & 255), db = (int)(p & 255) - (int)(pal[j] & 255);
+          const uint64_t rank = j > s0 ? 2 * (j - s0) - 1 : 2 * (s0 - j);
+          const uint64_t key = ((uint64_t)(dr * dr + dg * dg + db * db) << 32) | rank;
+          if (key < best) { best = key; ans = pal[j]; }
+        }
+        bad += outh[i] != ans; ++checked;
+      }
+      printf("  map check: %zu / %zu mismatches\n", bad, checked);
+      if (variant == 0) for (int bl : {512, 1024, 4096}) {
+        snprintf(nm, 80, "map blocks=%d", bl);
+        const size_t lds = (size_t)(k + 1) * 8 + 768 * 2;
+        timeit(nm, N * 8.0, [&] { map_kernel<false><<<bl, kBlock, lds>>>(d_px, N, d_p0, d_pal, k, d_lut, d_rec, d_idx); });
+      }
+      CK(hipFree(d_pal)); CK(hipFree(d_lut)); CK(hipFree(d_rec)); CK(hipFree(d_idx));
+    }
   }
   return 0;
 }
