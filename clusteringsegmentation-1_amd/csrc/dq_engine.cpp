@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <chrono>
 #include <unordered_set>
 
 namespace dq {
@@ -20,6 +21,11 @@ void die(const char* what, const char* file, int line, const char* detail) {
 }
 
 namespace {
+
+inline double host_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 constexpr int BUF_IN = 0, BUF_P0 = 1, BUF_P1 = 2;
 inline int child_buf(int b) { return b == BUF_P0 ? BUF_P1 : BUF_P0; }
@@ -38,14 +44,14 @@ int32_t split_threshold(double cut) {
 Engine::Engine(int device) : device_(device) {
   const char* full = getenv("DQ_HIP_FULL_ITERS");
   fixed_point_ = !(full && full[0] == '1');
+  const char* tr = getenv("DQ_HIP_TRACE");
+  trace_ = tr && tr[0] == '1';
+  const char* la = getenv("DQ_HIP_LOOKAHEAD");
+  if (la && la[0]) lookahead_ = std::max(0, std::min(8, atoi(la)));
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  DQ_HIP(hipMalloc((void**)&d_pal_, 16384 * sizeof(uint32_t)));
-  DQ_HIP(hipMalloc((void**)&d_lut_, 768 * sizeof(uint16_t)));
   DQ_HIP(hipMalloc((void**)&d_cell_rec_, (size_t)kCells * kCellRecWords * sizeof(uint32_t)));
   DQ_HIP(hipMalloc((void**)&d_cell_idx_, (size_t)kCells * kCellCap * sizeof(uint16_t)));
-  DQ_HIP(hipHostMalloc((void**)&h_pal_, 16384 * sizeof(uint32_t), hipHostMallocDefault));
-  DQ_HIP(hipHostMalloc((void**)&h_lut_, 768 * sizeof(uint16_t), hipHostMallocDefault));
 }
 
 Engine::~Engine() {
@@ -126,24 +132,102 @@ void Engine::stage_in(const uint32_t* h_in, uint32_t n, hipStream_t stream) {
                         hipMemcpyHostToDevice, stream));
 }
 
-void Engine::ensure_round(size_t nnodes, size_t ntiles) {
-  if (nnodes > cap_nodes_ || !d_nodes_) {
-    size_t c = std::max<size_t>(nnodes, 256);
-    if (d_nodes_) DQ_HIP(hipFree(d_nodes_));
-    if (h_nodes_) DQ_HIP(hipHostFree(h_nodes_));
-    DQ_HIP(hipMalloc((void**)&d_nodes_, c * sizeof(DevNode)));
-    DQ_HIP(hipHostMalloc((void**)&h_nodes_, c * sizeof(DevNode), hipHostMallocDefault));
-    cap_nodes_ = c;
+// Device arena for the per-round tables.  Chunks are kept (and reused by the
+// next run); a round's block never moves once written.
+char* Engine::arena_alloc(size_t bytes) {
+  bytes = (bytes + 255) & ~(size_t)255;
+  while (true) {
+    if (arena_chunk_ < arena_.size()) {
+      auto& c = arena_[arena_chunk_];
+      if (arena_used_ + bytes <= c.second) {
+        char* p = c.first + arena_used_;
+        arena_used_ += bytes;
+        return p;
+      }
+      ++arena_chunk_;
+      arena_used_ = 0;
+      continue;
+    }
+    const size_t sz = std::max<size_t>(bytes, (size_t)16 << 20);
+    char* p = nullptr;
+    DQ_HIP(hipMalloc((void**)&p, sz));
+    arena_.push_back({p, sz});
   }
-  if (ntiles > cap_tiles_ || !d_tiles_) {
-    size_t c = std::max<size_t>(ntiles, 4096);
-    if (d_tiles_) DQ_HIP(hipFree(d_tiles_));
-    if (d_parts_) DQ_HIP(hipFree(d_parts_));
-    if (h_tiles_) DQ_HIP(hipHostFree(h_tiles_));
-    DQ_HIP(hipMalloc((void**)&d_tiles_, c * sizeof(Tile)));
-    DQ_HIP(hipMalloc((void**)&d_parts_, c * sizeof(TilePartial)));
-    DQ_HIP(hipHostMalloc((void**)&h_tiles_, c * sizeof(Tile), hipHostMallocDefault));
-    cap_tiles_ = c;
+}
+
+template <typename T>
+static void grow_device(T** p, size_t* cap, size_t want) {
+  if (want <= *cap && *p) return;
+  if (*p) DQ_HIP(hipFree(*p));
+  const size_t c = std::max<size_t>(want, 1024);
+  DQ_HIP(hipMalloc((void**)p, c * sizeof(T)));
+  *cap = c;
+}
+
+// Host-coherent (fine-grained) pinned memory the kernels write with
+// system-scope visibility; the device view comes from hipHostGetDevicePointer.
+template <typename T>
+static void grow_coherent(T** h, T** d, size_t* cap, size_t want) {
+  if (want <= *cap && *h) return;
+  if (*h) DQ_HIP(hipHostFree(*h));
+  const size_t c = std::max<size_t>(want, 256);
+  DQ_HIP(hipHostMalloc((void**)h, c * sizeof(T), hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset(*h, 0, c * sizeof(T));
+  DQ_HIP(hipHostGetDevicePointer((void**)d, *h, 0));
+  *cap = c;
+}
+
+void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t staging_bytes,
+                          int max_iters, hipStream_t stream) {
+  // Lookahead launches of the previous round may still be queued (they may
+  // still read the part buffers and write a status word): drain the stream
+  // before any of these buffers moves.
+  const bool grow = staging_bytes > cap_stage_tab_ || nnodes > cap_res_ ||
+                    (size_t)max_iters > cap_stat_ || ntiles > cap_parts_ ||
+                    nptiles > cap_sparts_ || ntiles * kTileWaves > cap_wparts_ || !h_stage_ || !h_res_ || !h_stat_ || !d_parts_ ||
+                    !d_sparts_;
+  if (!grow) return;
+  DQ_HIP(hipStreamSynchronize(stream));
+  if (staging_bytes > cap_stage_tab_ || !h_stage_) {
+    if (h_stage_) DQ_HIP(hipHostFree(h_stage_));
+    const size_t c = std::max<size_t>(staging_bytes, (size_t)1 << 20);
+    DQ_HIP(hipHostMalloc((void**)&h_stage_, c, hipHostMallocDefault));
+    cap_stage_tab_ = c;
+  }
+  grow_coherent(&h_res_, &d_res_, &cap_res_, nnodes);
+  grow_coherent(&h_stat_, &d_stat_, &cap_stat_, (size_t)max_iters);
+  grow_device(&d_parts_, &cap_parts_, ntiles);
+  grow_device(&d_wparts_, &cap_wparts_, ntiles * kTileWaves);
+  grow_device(&d_sparts_, &cap_sparts_, std::max<size_t>(nptiles, 1));
+}
+
+// Wait for the status word of 2-means iteration `it` of round `seq`; returns
+// the number of nodes still active after it.  Bounded: once the stream has
+// drained the word must be there.
+uint32_t Engine::wait_status(int it, uint64_t seq, hipStream_t stream) {
+  const double t0 = trace_ ? host_us() : 0.0;
+  struct Acc {
+    Engine* e; double t0;
+    ~Acc() { if (e->trace_) e->tr_wait_us_ += host_us() - t0; }
+  } acc{this, t0};
+  const uint32_t want = (uint32_t)seq;
+  auto ready = [&](uint32_t* act) {
+    const uint64_t v = __atomic_load_n(h_stat_ + it, __ATOMIC_ACQUIRE);
+    if (!(v & 1) || (uint32_t)(v >> 32) != want) return false;
+    *act = (uint32_t)((v >> 1) & 0x7FFFFFFFu);
+    return true;
+  };
+  uint32_t act = 0;
+  for (uint64_t spin = 0;; ++spin) {
+    if (ready(&act)) return act;
+    if ((spin & 0x3FFF) == 0x3FFF) {
+      const hipError_t e = hipStreamQuery(stream);
+      if (e == hipSuccess) {
+        if (ready(&act)) return act;
+        die("status word", __FILE__, __LINE__, "stream drained without the 2-means status");
+      }
+      if (e != hipErrorNotReady) die("hipStreamQuery", __FILE__, __LINE__, hipGetErrorString(e));
+    }
   }
 }
 
@@ -154,33 +238,96 @@ const uint32_t* Engine::buf_ptr(int buf, const FrameState& f) const {
 
 // ---------------------------------------------------------------------------
 // One round: split every node in `active` (one launch per pass for all).
-void Engine::run_round(const std::vector<int>& active, bool root_round, int max_iters,
+//
+// A node whose parent was split in an earlier round but not yet partitioned
+// gets its points and its split-pass statistics from ONE fused launch over
+// the parent's tiles (partsplit_kernel); every other node (the roots, and
+// nodes whose sibling already forced the partition) has its own split pass.
+// Partitions are lazy: a node is partitioned only when one of its children is
+// split, so the leaves of the last round never are.
+void Engine::run_round(const std::vector<int>& active_in, bool root_round, int max_iters,
                        hipStream_t stream) {
-  const int nn = (int)active.size();
-  uint64_t total = 0;
-  for (int id : active) total += nodes_[id].len;
+  const double tb0 = trace_ ? host_us() : 0.0;
+  std::vector<int> order, parents;
+  // node id -> slot in the round / position in `parents` (-1: none)
+  slot_of_.assign(nodes_.size(), -1);
+  parent_pos_.assign(nodes_.size(), -1);
+  for (int id : active_in)
+    if (root_round || nodes_[nodes_[id].parent].partitioned) order.push_back(id);
+  const int n_own = (int)order.size();
+  for (int id : active_in) {
+    if (root_round || nodes_[nodes_[id].parent].partitioned) continue;
+    order.push_back(id);
+    const int p = nodes_[id].parent;
+    if (parent_pos_[p] < 0) {
+      parent_pos_[p] = (int)parents.size();
+      parents.push_back(p);
+    }
+  }
+  const int nn = (int)order.size();
+
+  uint64_t total = 0, own_total = 0, parent_total = 0;
+  for (int a = 0; a < nn; ++a) {
+    total += nodes_[order[a]].len;
+    if (a < n_own) own_total += nodes_[order[a]].len;
+  }
+  for (int p : parents) parent_total += nodes_[p].len;
   // Tile length: whole 4096-point sweeps, ~1024 tiles for big rounds (4 per
   // CU: measured best for one 4K frame and for 8-frame batches, microbench).
   uint64_t tl = (total + 1023) / 1024;
   tl = ((tl + kSweep - 1) / kSweep) * kSweep;
   tl = std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, kMaxTilePx));
-  size_t ntiles = 0;
-  for (int id : active)   // empty nodes get one empty tile (their epilogue still runs)
-    ntiles += std::max<size_t>(1, (nodes_[id].len + tl - 1) / tl);
-  ensure_round(nn, ntiles);
+  size_t ntiles = 0, nt_own = 0;
+  for (int a = 0; a < nn; ++a) {   // empty nodes get one empty tile (their epilogue still runs)
+    ntiles += std::max<size_t>(1, (nodes_[order[a]].len + tl - 1) / tl);
+    if (a == n_own - 1) nt_own = ntiles;
+  }
+  size_t nptiles = 0;
+  for (int p : parents) nptiles += nodes_[p].ntiles;
 
+  // the round's block: [DevNode nn | Tile ntiles | PartTile nptiles | LaunchCtr max_iters]
+  auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
+  const size_t o_tiles = al(nn * sizeof(DevNode));
+  const size_t o_pt = o_tiles + al(ntiles * sizeof(Tile));
+  const size_t o_ctr = o_pt + al(nptiles * sizeof(PartTile));
+  const size_t bytes = o_ctr + al((size_t)max_iters * sizeof(LaunchCtr));
+  ensure_round(nn, ntiles, nptiles, bytes, max_iters, stream);
+  char* dblk = arena_alloc(bytes);
+  std::memset(h_stage_, 0, bytes);
+  DevNode* hn = reinterpret_cast<DevNode*>(h_stage_);
+  Tile* ht = reinterpret_cast<Tile*>(h_stage_ + o_tiles);
+  PartTile* hp = reinterpret_cast<PartTile*>(h_stage_ + o_pt);
+  DevNode* dn = reinterpret_cast<DevNode*>(dblk);
+  Tile* dt = reinterpret_cast<Tile*>(dblk + o_tiles);
+
+  std::vector<int> slot_of_parent_pt(parents.size());   // first PartTile of each parent
+  {
+    int q = 0;
+    for (size_t i = 0; i < parents.size(); ++i) {
+      slot_of_parent_pt[i] = q;
+      q += nodes_[parents[i]].ntiles;
+    }
+  }
   int t = 0;
   for (int a = 0; a < nn; ++a) {
-    const Node& n = nodes_[active[a]];
+    const Node& n = nodes_[order[a]];
+    slot_of_[order[a]] = a;
     const FrameState& fs = frames_[n.frame];
-    DevNode& d = h_nodes_[a];
-    std::memset(&d, 0, sizeof(d));
+    DevNode& d = hn[a];
     d.src = buf_ptr(n.buf, fs);
     d.dst = (child_buf(n.buf) == BUF_P0 ? d_p0_ : d_p1_) + fs.base;
     d.off = n.off;
     d.len = n.len;
     d.s = fs.s;
     d.tw = n.w;
+    d.split_pb = -1;
+    d.split_pe = -1;
+    if (a >= n_own) {
+      const int pi = parent_pos_[n.parent];
+      d.split_pb = slot_of_parent_pt[pi];
+      d.split_pe = d.split_pb + nodes_[n.parent].ntiles;
+      d.split_side = nodes_[n.parent].child_new == order[a] ? 1 : 0;
+    }
     for (int c = 0; c < 3; ++c) { d.tm[c] = n.mean[c]; d.tv[c] = n.var[c]; }
     if (!root_round) {
       // Cut axis/position (:388-403): comparisons and copies only.  (The
@@ -194,85 +341,148 @@ void Engine::run_round(const std::vector<int>& active, bool root_round, int max_
     }
     d.tile_begin = t;
     for (uint64_t o = 0; o == 0 || o < n.len; o += tl) {
-      Tile& tt = h_tiles_[t++];
+      Tile& tt = ht[t++];
       tt.node = a;
       tt.start = n.off + (uint32_t)o;
       tt.end = n.off + (uint32_t)std::min<uint64_t>(n.len, o + tl);
-      tt.old_base = 0;
     }
     d.tile_end = t;
   }
-  DQ_HIP(hipMemcpyAsync(d_nodes_, h_nodes_, nn * sizeof(DevNode), hipMemcpyHostToDevice, stream));
-  DQ_HIP(hipMemcpyAsync(d_tiles_, h_tiles_, ntiles * sizeof(Tile), hipMemcpyHostToDevice, stream));
+  {
+    int q = 0;
+    for (int p : parents) {
+      const Node& pn = nodes_[p];
+      int32_t thr[2], shift[2];
+      const int ch[2] = {pn.child_old, pn.child_new};
+      for (int c = 0; c < 2; ++c) {
+        const int sl = slot_of_[ch[c]];
+        thr[c] = sl >= 0 ? hn[sl].prm.thr : 256;   // 256: nothing counted
+        shift[c] = sl >= 0 ? hn[sl].prm.shift : 0;
+      }
+      for (int i = 0; i < pn.ntiles; ++i) {
+        PartTile& pt = hp[q++];
+        pt.tile = pn.dtiles + i;
+        pt.parent = pn.dnode;
+        pt.thr[0] = thr[0];
+        pt.thr[1] = thr[1];
+        pt.shift[0] = shift[0];
+        pt.shift[1] = shift[1];
+      }
+    }
+  }
+  DQ_HIP(hipMemcpyAsync(dblk, h_stage_, bytes, hipMemcpyHostToDevice, stream));
+  if (trace_) tr_build_us_ += host_us() - tb0;
 
+  const uint64_t seq = ++seq_;
   RoundArgs ra;
-  ra.tiles = d_tiles_;
-  ra.nodes = d_nodes_;
+  ra.tiles = dt;
+  ra.nodes = dn;
   ra.parts = d_parts_;
+  ra.wparts = d_wparts_;
+  ra.ptiles = reinterpret_cast<const PartTile*>(dblk + o_pt);
+  ra.sparts = d_sparts_;
+  ra.hres = d_res_;
+  ra.ctr = reinterpret_cast<LaunchCtr*>(dblk + o_ctr);
+  ra.hstat = d_stat_;
+  ra.seq = seq;
   ra.fixed_point = fixed_point_ ? 1 : 0;
-  const double bytes = 4.0 * (double)total;
+  ra.it = 0;
+  ra.nn = nn;
+  const double bytes_all = 4.0 * (double)total;
   const int nt = (int)ntiles;
   // 2-means passes (iteration index) whose timing entry gets its swept bytes
   // once the nodes' done_it are known
   std::vector<std::pair<size_t, int>> km_events;
-  auto pass = [&](int kind, int st, int it) {
-    timed_begin(stream);
-    launch_pass(kind, ra, nt, stream);
-    timed_end(st, bytes, stream);
-    if (timing_ && it >= 0) km_events.push_back({pending_.size() - 1, it});
+  auto pass = [&](int kind, int st, int it, int tiles, double pbytes) {
+    ra.it = it < 0 ? 0 : it;
+    if (tiles > 0) {
+      timed_begin(stream);
+      launch_pass(kind, ra, tiles, stream);
+      timed_end(st, pbytes, stream);
+      if (timing_ && it >= 0) km_events.push_back({pending_.size() - 1, it});
+    }
+  };
+  auto epilogue = [&](int kind, int it) {
+    ra.it = it < 0 ? 0 : it;
     timed_begin(stream);
     launch_epilogue(kind, ra, nn, stream);
     timed_end(ST_EPILOGUE, 0.0, stream);
   };
-  if (root_round) pass(PASS_INIT, ST_INIT, -1);
-  pass(PASS_SPLIT, ST_SPLIT, -1);
-  for (int it = 0; it < max_iters; ++it) {
-    const bool last = (it == max_iters - 1);
-    pass(last ? PASS_KLAST : PASS_KMEANS, last ? ST_KLAST : ST_KMEANS, it);
+  if (root_round) {
+    pass(PASS_INIT, ST_INIT, -1, nt, bytes_all);
+    epilogue(PASS_INIT, -1);
   }
-  timed_begin(stream);
-  launch_partition(ra, nt, stream);
-  timed_end(ST_PARTITION, 2.0 * bytes, stream);
+  pass(PASS_SPLIT, ST_SPLIT, -1, (int)nt_own, 4.0 * (double)own_total);
+  if (nptiles > 0) {
+    timed_begin(stream);
+    launch_partsplit(ra, (int)nptiles, stream);
+    timed_end(ST_PARTITION, 8.0 * (double)parent_total, stream);
+  }
+  epilogue(PASS_SPLIT, -1);
+  // 2-means iterations, `lookahead_` launched past the one whose status the
+  // host waits for; stop as soon as every node is final.
+  int launched = 0, known = 0;
+  while (true) {
+    while (launched < max_iters && launched <= known + lookahead_) {
+      const bool last = launched == max_iters - 1;
+      pass(last ? PASS_KLAST : PASS_KMEANS, last ? ST_KLAST : ST_KMEANS, launched, nt, bytes_all);
+      epilogue(last ? PASS_KLAST : PASS_KMEANS, launched);
+      ++launched;
+    }
+    const uint32_t act = wait_status(known, seq, stream);
+    ++known;
+    if (act == 0) break;
+    DQ_CHECK(known < max_iters, "nodes still active after the last 2-means iteration");
+  }
 
-  DQ_HIP(hipMemcpyAsync(h_nodes_, d_nodes_, nn * sizeof(DevNode), hipMemcpyDeviceToHost, stream));
-  DQ_HIP(hipStreamSynchronize(stream));
   // points actually swept: iteration `it` reads a node iff it is not final
-  // before it (done_it == 0, or it < done_it)
+  // before it (done_it <= 0: final at the last iteration, or it < done_it)
   auto swept_in = [&](int it) {
     uint64_t px = 0;
     for (int a = 0; a < nn; ++a) {
-      const DevNode& d = h_nodes_[a];
-      if (d.done_it == 0 || it < d.done_it) px += d.len;
+      const int di = h_res_[a].done_it;
+      if (di <= 0 || it < di) px += nodes_[order[a]].len;
     }
     return px;
   };
   last_points_full += total * (uint64_t)((root_round ? 2 : 1) + max_iters);
   last_points_swept += total * (uint64_t)(root_round ? 2 : 1);
   for (int it = 0; it < max_iters; ++it) last_points_swept += swept_in(it);
-  for (auto& e : km_events) pending_[e.first].bytes = 4.0 * (double)swept_in(e.second);
-  collect_timing();
+  if (timing_) {
+    DQ_HIP(hipStreamSynchronize(stream));
+    for (auto& e : km_events) pending_[e.first].bytes = 4.0 * (double)swept_in(e.second);
+    collect_timing();
+  }
 
+  for (int p : parents) nodes_[p].partitioned = true;
+  int tcur = 0;
   for (int a = 0; a < nn; ++a) {
-    const int id = active[a];
-    const DevNode& d = h_nodes_[a];
+    const int id = order[a];
+    const NodeResult& r = h_res_[a];
     if (root_round) {
-      for (int c = 0; c < 3; ++c) { nodes_[id].mean[c] = d.tm[c]; nodes_[id].var[c] = d.tv[c]; }
+      for (int c = 0; c < 3; ++c) { nodes_[id].mean[c] = r.tm[c]; nodes_[id].var[c] = r.tv[c]; }
     }
+    const int ntl = hn[a].tile_end - hn[a].tile_begin;
+    nodes_[id].dnode = dn + a;
+    nodes_[id].dtiles = dt + tcur;
+    nodes_[id].ntiles = ntl;
+    tcur += ntl;
     const Node& p = nodes_[id];
-    const uint32_t n_new = (uint32_t)d.n_new;
+    const uint32_t n_new = r.n_new_local;
     const uint32_t n_old = p.len - n_new;
     Node co, cn;
     co.frame = cn.frame = p.frame;
-    co.w = d.ow;
-    cn.w = d.nw;
+    co.parent = cn.parent = id;
+    co.w = r.ow;
+    cn.w = r.nw;
     for (int c = 0; c < 3; ++c) {
-      co.mean[c] = d.om[c];
-      cn.mean[c] = d.nm[c];
-      co.var[c] = d.ov[c];
-      cn.var[c] = d.nv[c];
+      co.mean[c] = r.om[c];
+      cn.mean[c] = r.nm[c];
+      co.var[c] = r.ov[c];
+      cn.var[c] = r.nv[c];
     }
-    co.tse = d.tse_old;
-    cn.tse = d.tse_new;
+    co.tse = r.tse_old;
+    cn.tse = r.tse_new;
     co.off = p.off;
     co.len = n_old;
     cn.off = p.off + n_old;
@@ -380,6 +590,8 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
 
   frames_.assign(nframes, FrameState());
   nodes_.clear();
+  arena_chunk_ = 0;   // the previous run's tables are dead (its launches were drained)
+  arena_used_ = 0;
   last_rounds = 0;
   last_points_swept = 0;
   last_points_full = 0;
@@ -425,22 +637,28 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     if (j.k > 1) active.push_back(f.leaf[0]);
   }
 
+  const double t_run0 = trace_ ? host_us() : 0.0;
+  tr_wait_us_ = tr_build_us_ = tr_replay_us_ = 0.0;
   bool root_round = true;
   while (!active.empty()) {
     run_round(active, root_round, max_iters, stream);
     root_round = false;
     last_rounds++;
     active.clear();
+    const double tr0 = trace_ ? host_us() : 0.0;
     for (auto& f : frames_) {
       if (f.job->k <= 1 || (f.need < 0 && f.new_index >= f.job->k)) continue;
       replay(f);
       next_active(f, &active);
     }
+    if (trace_) tr_replay_us_ += host_us() - tr0;
   }
+  const double t_clu = trace_ ? host_us() : 0.0;
 
   for (int i = 0; i < nframes; ++i) finish_frame(frames_[i], i == nframes - 1);
 
   if (dedup_map) {
+    std::vector<MapJob> mj;
     for (auto& f : frames_) {
       FrameJob& j = *f.job;
       // First-occurrence colortable dedup (quant_util.cpp:93-118).
@@ -449,36 +667,30 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
       for (int i = 0; i < j.k_out; ++i)
         if (seen.insert(j.ct[i]).second) j.ct[m++] = j.ct[i];
       j.k_out = m;
-      if (j.d_out) map(f.in, j.n, j.d_out, j.ct, m, stream);
+      if (j.d_out) mj.push_back(MapJob{f.in, j.n, j.d_out, j.ct, m});
     }
+    if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream);
+  }
+  // Synchronous on return: lookahead launches of the last round may still be
+  // queued, and they read the caller's input.
+  DQ_HIP(hipStreamSynchronize(stream));
+  if (trace_) {
+    const double t_end = host_us();
+    std::fprintf(stderr,
+                 "divquant-hip trace: frames=%d rounds=%d cluster=%.1fus (build %.1f, wait %.1f, "
+                 "replay %.1f) map+sync=%.1fus total=%.1fus\n",
+                 nframes, last_rounds, t_clu - t_run0, tr_build_us_, tr_wait_us_, tr_replay_us_,
+                 t_end - t_clu, t_end - t_run0);
   }
 }
 
 // ---------------------------------------------------------------------------
-void Engine::map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
-                 const uint32_t* ct, int k, hipStream_t stream) {
-  DQ_CHECK(k > 0, "colormapSize must be > 0 (DivQuantMapColors.cpp:264)");
-  DQ_CHECK(k <= 16384, "colormapSize > 16384 is not supported by the LDS palette");
-  DQ_HIP(hipSetDevice(device_));
-  if (!stream) stream = stream_;
-  if (((uintptr_t)d_in & 15) != 0 || ((uintptr_t)d_out & 15) != 0) {
-    // the map kernel uses 16-B loads/stores: go through aligned staging
-    const size_t want = align4(n) + 4;
-    if (2 * want > cap_map_align_) {
-      if (d_map_align_) DQ_HIP(hipFree(d_map_align_));
-      DQ_HIP(hipMalloc((void**)&d_map_align_, want * 2 * sizeof(uint32_t)));
-      cap_map_align_ = want * 2;
-    }
-    uint32_t* ain = d_map_align_;
-    uint32_t* aout = d_map_align_ + want;
-    DQ_HIP(hipMemcpyAsync(ain, d_in, (size_t)n * 4, hipMemcpyDeviceToDevice, stream));
-    map(ain, n, aout, ct, k, stream);
-    DQ_HIP(hipMemcpyAsync(d_out, aout, (size_t)n * 4, hipMemcpyDeviceToDevice, stream));
-    DQ_HIP(hipStreamSynchronize(stream));
-    return;
-  }
-  // Palette sorted by R+G+B with std::sort and the reference comparator
-  // (:227-238, :314-323) -- same algorithm, same input => same tie order.
+namespace {
+// The palette sorted by R+G+B with std::sort and the reference comparator
+// (DivQuantMapColors.cpp:227-238, :314-323) -- same algorithm, same input =>
+// same tie order -- and the start-entry LUT from rounded midpoints (:331-383).
+// Writes k sorted colours to pal and 766 LUT entries to lut.
+void sorted_palette(const uint32_t* ct, int k, uint32_t* pal_out, uint16_t* lut_out) {
   struct Ent { int red, green, blue, weight; };
   std::vector<Ent> pal(k);
   for (int i = 0; i < k; ++i) {
@@ -490,7 +702,6 @@ void Engine::map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
   }
   std::sort(pal.begin(), pal.end(),
             [](const Ent& a, const Ent& b) { return a.weight < b.weight; });
-  // Start-entry LUT from rounded midpoints (:331-383).
   int lut[766];
   const int low = k >= 2 ? (int)(0.5 * (pal[0].weight + pal[1].weight) + 0.5) : 1;
   for (int v = 0; v < low; ++v) lut[v] = 0;
@@ -501,22 +712,80 @@ void Engine::map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
     const int hi = (int)(0.5 * (pal[i].weight + pal[i + 1].weight) + 0.5);
     for (int v = lo; v < hi; ++v) lut[v] = i;
   }
-  // The pinned staging below is reused by the next call: wait for the
-  // previous map's copies first.
-  DQ_HIP(hipStreamSynchronize(stream));
   for (int i = 0; i < k; ++i)
-    h_pal_[i] = ((uint32_t)pal[i].red << 16) | ((uint32_t)pal[i].green << 8) | (uint32_t)pal[i].blue;
-  for (int v = 0; v < 766; ++v) h_lut_[v] = (uint16_t)lut[v];
-  DQ_HIP(hipMemcpyAsync(d_pal_, h_pal_, k * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-  DQ_HIP(hipMemcpyAsync(d_lut_, h_lut_, 766 * sizeof(uint16_t), hipMemcpyHostToDevice, stream));
-  timed_begin(stream);
-  launch_build_cells(d_pal_, k, d_cell_rec_, d_cell_idx_, stream);
-  timed_end(ST_CELLS, 0.0, stream);
-  timed_begin(stream);
-  launch_map(d_in, n, d_out, d_pal_, k, d_lut_, d_cell_rec_, d_cell_idx_, stream);
-  timed_end(ST_MAP, 8.0 * (double)n, stream);
+    pal_out[i] = ((uint32_t)pal[i].red << 16) | ((uint32_t)pal[i].green << 8) | (uint32_t)pal[i].blue;
+  for (int v = 0; v < 766; ++v) lut_out[v] = (uint16_t)lut[v];
+}
+
+// Per-map block of the map staging: [palette: kMapPal words | LUT: 768 u16]
+constexpr size_t kMapPal = 16384;
+constexpr size_t kMapBlockWords = kMapPal + 768 / 2;
+}  // namespace
+
+void Engine::ensure_map_stage(size_t nmaps) {
+  if (nmaps <= cap_mapstage_ && h_mapstage_) return;
+  if (h_mapstage_) DQ_HIP(hipHostFree(h_mapstage_));
+  if (d_mapstage_) DQ_HIP(hipFree(d_mapstage_));
+  DQ_HIP(hipHostMalloc((void**)&h_mapstage_, nmaps * kMapBlockWords * 4, hipHostMallocDefault));
+  DQ_HIP(hipMalloc((void**)&d_mapstage_, nmaps * kMapBlockWords * 4));
+  cap_mapstage_ = nmaps;
+}
+
+// map_colors_mps (DivQuantMapColors.cpp:243-539) for several (input, output,
+// colortable) triples: host palettes for all of them, ONE upload, then per
+// map the cell build and the map kernel, ONE synchronisation at the end.
+void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
+  DQ_HIP(hipSetDevice(device_));
+  if (!stream) stream = stream_;
+  for (int i = 0; i < njobs; ++i) {
+    DQ_CHECK(jobs[i].k > 0, "colormapSize must be > 0 (DivQuantMapColors.cpp:264)");
+    DQ_CHECK(jobs[i].k <= (int)kMapPal, "colormapSize > 16384 is not supported by the LDS palette");
+  }
+  // the staging is reused: the previous map's upload must have been consumed
+  DQ_HIP(hipStreamSynchronize(stream));
+  ensure_map_stage(njobs);
+  for (int i = 0; i < njobs; ++i) {
+    uint32_t* blk = h_mapstage_ + i * kMapBlockWords;
+    sorted_palette(jobs[i].ct, jobs[i].k, blk, reinterpret_cast<uint16_t*>(blk + kMapPal));
+  }
+  DQ_HIP(hipMemcpyAsync(d_mapstage_, h_mapstage_, njobs * kMapBlockWords * 4,
+                        hipMemcpyHostToDevice, stream));
+  for (int i = 0; i < njobs; ++i) {
+    const MapJob& j = jobs[i];
+    const uint32_t* dpal = d_mapstage_ + i * kMapBlockWords;
+    const uint16_t* dlut = reinterpret_cast<const uint16_t*>(dpal + kMapPal);
+    const uint32_t* in = j.d_in;
+    uint32_t* out = j.d_out;
+    const size_t want = align4(j.n) + 4;
+    const bool staged = ((uintptr_t)in & 15) != 0 || ((uintptr_t)out & 15) != 0;
+    if (staged) {   // the map kernel uses 16-B loads/stores: go through aligned staging
+      if (2 * want > cap_map_align_) {
+        DQ_HIP(hipStreamSynchronize(stream));
+        if (d_map_align_) DQ_HIP(hipFree(d_map_align_));
+        DQ_HIP(hipMalloc((void**)&d_map_align_, want * 2 * sizeof(uint32_t)));
+        cap_map_align_ = want * 2;
+      }
+      DQ_HIP(hipMemcpyAsync(d_map_align_, in, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
+      in = d_map_align_;
+      out = d_map_align_ + want;
+    }
+    timed_begin(stream);
+    launch_build_cells(dpal, j.k, d_cell_rec_, d_cell_idx_, stream);
+    timed_end(ST_CELLS, 0.0, stream);
+    timed_begin(stream);
+    launch_map(in, j.n, out, dpal, j.k, dlut, d_cell_rec_, d_cell_idx_, stream);
+    timed_end(ST_MAP, 8.0 * (double)j.n, stream);
+    if (staged)
+      DQ_HIP(hipMemcpyAsync(j.d_out, out, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
+  }
   DQ_HIP(hipStreamSynchronize(stream));
   collect_timing();
+}
+
+void Engine::map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
+                 const uint32_t* ct, int k, hipStream_t stream) {
+  MapJob j{d_in, n, d_out, ct, k};
+  map_many(&j, 1, stream);
 }
 
 Engine& engine_for(int device) {

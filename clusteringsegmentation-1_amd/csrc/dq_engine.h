@@ -46,6 +46,13 @@ struct Node {
   double var[3] = {0, 0, 0};         // var[]      (:314)
   double tse = 0.0;                  // tse[]      (:304)
   uint32_t off = 0, len = 0;         // segment (len == size[] of the cluster)
+  int parent = -1;
+  // the round the node was split in: its record and tiles stay on the device
+  // so that a later round can partition it (fused with its children's split)
+  const DevNode* dnode = nullptr;
+  const Tile* dtiles = nullptr;
+  int ntiles = 0;
+  bool partitioned = false;          // children's points written to child_buf(buf)
 };
 
 // One quant_recurse / DivQuantCluster input.
@@ -84,6 +91,14 @@ class Engine {
   // map_colors_mps (DivQuantMapColors.cpp:243-539) on device buffers.
   void map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
            const uint32_t* ct, int k, hipStream_t stream);
+  struct MapJob {
+    const uint32_t* d_in;
+    uint32_t n;
+    uint32_t* d_out;
+    const uint32_t* ct;   // host colortable
+    int k;
+  };
+  void map_many(const MapJob* jobs, int njobs, hipStream_t stream);
 
   // Host-pointer convenience (copies in and out through the engine's buffers).
   void stage_in(const uint32_t* h_in, uint32_t n, hipStream_t stream);
@@ -124,7 +139,10 @@ class Engine {
   };
 
   void ensure_pixels(size_t total);
-  void ensure_round(size_t nnodes, size_t ntiles);
+  void ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t staging_bytes,
+                    int max_iters, hipStream_t stream);
+  char* arena_alloc(size_t bytes);
+  uint32_t wait_status(int it, uint64_t seq, hipStream_t stream);
   void run_round(const std::vector<int>& active, bool root_round, int max_iters,
                  hipStream_t stream);
   void replay(FrameState& f);
@@ -153,23 +171,42 @@ class Engine {
   uint32_t* d_map_align_ = nullptr;   // map staging for misaligned in/out
   size_t cap_map_align_ = 0;
 
-  // per-round node/tile/accumulator tables
-  DevNode* d_nodes_ = nullptr;
-  Tile* d_tiles_ = nullptr;
-  TilePartial* d_parts_ = nullptr;
-  DevNode* h_nodes_ = nullptr;   // pinned
-  Tile* h_tiles_ = nullptr;      // pinned
-  size_t cap_nodes_ = 0, cap_tiles_ = 0;
+  // Per-round tables: every round's [DevNode | Tile | PartTile | LaunchCtr]
+  // block is carved from a device arena that is only recycled by the next
+  // run (a later round partitions nodes through their records and tiles) and
+  // written with ONE copy from the pinned staging buffer.
+  std::vector<std::pair<char*, size_t>> arena_;   // chunks
+  size_t arena_chunk_ = 0, arena_used_ = 0;
+  char* h_stage_ = nullptr;           // pinned
+  size_t cap_stage_tab_ = 0;
+  TilePartial* d_parts_ = nullptr;    // per tile of the round
+  uint32_t* d_wparts_ = nullptr;      // per (tile, wave) of the round
+  size_t cap_wparts_ = 0;
+  TilePartial* d_sparts_ = nullptr;   // per PartTile of the round
+  size_t cap_parts_ = 0, cap_sparts_ = 0;
+  // host-coherent pinned memory the epilogues write (results, status words)
+  NodeResult* h_res_ = nullptr;
+  NodeResult* d_res_ = nullptr;       // device view of h_res_
+  size_t cap_res_ = 0;
+  uint64_t* h_stat_ = nullptr;
+  uint64_t* d_stat_ = nullptr;
+  size_t cap_stat_ = 0;
+  uint64_t seq_ = 0;                  // round sequence number
+  int lookahead_ = 1;                 // 2-means iterations queued past the one awaited
+  // host-side trace (DQ_HIP_TRACE=1): per-run phase times on stderr
+  bool trace_ = false;
+  double tr_wait_us_ = 0, tr_build_us_ = 0, tr_replay_us_ = 0;
 
   // map tables
-  uint32_t* d_pal_ = nullptr;
-  uint16_t* d_lut_ = nullptr;
   uint32_t* d_cell_rec_ = nullptr;
   uint16_t* d_cell_idx_ = nullptr;
-  uint32_t* h_pal_ = nullptr;    // pinned
-  uint16_t* h_lut_ = nullptr;    // pinned
+  uint32_t* h_mapstage_ = nullptr;   // pinned: per map [sorted palette | start LUT]
+  uint32_t* d_mapstage_ = nullptr;
+  size_t cap_mapstage_ = 0;
+  void ensure_map_stage(size_t nmaps);
 
   std::vector<Node> nodes_;
+  std::vector<int> slot_of_, parent_pos_;   // run_round scratch, indexed by node id
   std::vector<FrameState> frames_;
   struct PendingEvent { hipEvent_t a, b; int kind; double bytes; };
   std::vector<PendingEvent> pending_;

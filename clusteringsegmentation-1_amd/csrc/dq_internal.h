@@ -11,7 +11,10 @@
 //   segment         -- the contiguous range [off, off+len) of a working pixel
 //                      buffer that holds one node's points;
 //   tile            -- the part of a segment one workgroup sweeps in a pass;
-//   frame           -- one quant_recurse input; a round may mix frames.
+//   frame           -- one quant_recurse input; a round may mix frames;
+//   shard           -- (row-tile mode) the rows of a frame one GPU holds; every
+//                      count/sum below is then LOCAL to the shard unless it is
+//                      called global (the allreduced value).
 #pragma once
 #include <stdint.h>
 
@@ -26,9 +29,9 @@ enum PassKind : int32_t {
 };
 
 // Per-tile partial statistics of the new side (all points in PASS_INIT):
-// count, sums and sums of squares in every pass; plain 32-B stores, exact in
-// u32 because a tile has at most 65536 points (65536 * 255^2 < 2^32).  The
-// node's epilogue sums them in u64.
+// count, sums and sums of squares; plain 32-B stores, exact in u32 because a
+// tile has at most 65536 points (65536 * 255^2 < 2^32).  The node's epilogue
+// sums them in u64.
 enum PartField : int32_t { F_CNT = 0, F_SR, F_SG, F_SB, F_QR, F_QG, F_QB, F_NUM };
 struct alignas(32) TilePartial {
   uint32_t f[8];
@@ -42,43 +45,85 @@ struct alignas(16) Params {
   int32_t pad;
 };
 
-// Per-node state for one round.
+// Per-node state.  One record per node per round it is split in; the records
+// of earlier rounds stay valid for the whole run (a later round partitions a
+// node through its record and tiles, see PartTile).
 struct alignas(16) DevNode {
   // --- set by the host when the round starts
-  const uint32_t* src;      // element 0 of the frame in the buffer holding the node
-  uint32_t* dst;            // element 0 of the frame in the child buffer
-  uint32_t off, len;        // segment, relative to src / dst
-  int32_t tile_begin;       // this node's tiles are [tile_begin, tile_end)
+  const uint32_t* src;      // element 0 of the frame (shard) in the buffer holding the node
+  uint32_t* dst;            // element 0 of the frame (shard) in the child buffer
+  uint32_t off, len;        // local segment, relative to src / dst
+  int32_t tile_begin;       // this node's tiles are [tile_begin, tile_end) of the round
   int32_t tile_end;
+  int32_t split_pb, split_pe;   // fused split: the parent's PartTiles [pb, pe) of the round
+  int32_t split_side;           //   0: this node is the parent's old half, 1: the new half
+  int32_t pad0;                 //   (split_pb < 0: the node has its own split pass)
   double s;                 // data_weight of the frame (get_double_scale)
   double tw;                // total_weight = weight[old_index]  (:353)
   double tm[3], tv[3];      // total_mean / total_var (root: written by PASS_INIT)
   // --- parameters of the next pass (host for the split pass of non-roots,
-  //     otherwise written by the node's epilogue)
+  //     otherwise written by the node's epilogue); after the split is final
+  //     prm holds the 2-means decision that produced the final halves.
   Params prm;
-  // --- results of the node's split (written by the PASS_KLAST epilogue, or
-  //     by the PASS_KMEANS epilogue that finds the 2-means at a fixed point;
-  //     prm then still holds the last 2-means decision)
-  double om[3], nm[3];      // old_mean / new_mean after the last pass
-  double nv[3], ov[3];      // new_var / old_var (:836-855)
-  double nw, ow;            // new_weight / old_weight
-  double tse_old, tse_new;  // (:870-871)
-  uint64_t n_new;           // new_size (:820-821)
   // --- fixed-point detection.  The 2-means state after a pass is the new
   //     side's exact integer (count, sums): when a pass reproduces the
   //     previous pass's, every later iteration is bit-identical (same sums ->
   //     same means -> same decision), so the results are final and the
   //     remaining passes skip the node.
-  uint64_t prev[4];         // count, sum R, G, B of the previous pass
+  uint64_t prev[4];         // count, sum R, G, B of the previous pass (global)
+  uint32_t n_new_local;     // final new-half size in this shard (partition)
   int32_t iter;             // 2-means iterations completed (epilogue count)
   int32_t done_it;          // 0: active; else 1 + the iteration found at the fixed point
+  int32_t pad1;
 };
 
-// One workgroup's share of a pass.
+// The split's results, written by the finalising epilogue straight into
+// host-coherent pinned memory (the host reads them without a copy).
+struct alignas(16) NodeResult {
+  double om[3], nm[3];      // old_mean / new_mean after the last pass
+  double nv[3], ov[3];      // new_var / old_var (:836-855)
+  double tm[3], tv[3];      // the node's own mean / var (root: from PASS_INIT)
+  double nw, ow;            // new_weight / old_weight
+  double tse_old, tse_new;  // (:870-871)
+  uint64_t n_new;           // new_size (:820-821), global
+  uint32_t n_new_local;     // new half in this shard
+  int32_t done_it;          // see DevNode
+};
+
+// One workgroup's share of a pass.  Inside a tile, wave w of the workgroup
+// owns the points vs + 4*(j*kBlock + w*64 + lane) + e of every sweep vs (the
+// same in every kernel), so the final pass's per-wave counts let each wave
+// of the partition write its points with no block-level synchronisation.
+constexpr int kTileWaves = 4;
 struct alignas(16) Tile {
   int32_t node;             // index into the round's DevNode array
   uint32_t start, end;      // pixel range relative to the node's src
-  uint32_t old_base;        // partition: old points in the node's earlier tiles
+  uint32_t pad;
+  // partition cursors of each wave (set by the finalising epilogue):
+  uint32_t old_base[kTileWaves];   // OLD points of the node before this wave's share
+  uint32_t new_base[kTileWaves];   // NEW points of the node before this wave's share
 };
+
+// One workgroup's share of a fused partition + split pass: a tile of a
+// parent node split in an EARLIER round.  Its points are written to the two
+// children's segments (replaying the parent's final decision) and each
+// child's split-pass statistics (:438-559) are accumulated on the way.
+struct alignas(32) PartTile {
+  const Tile* tile;         // the parent's tile (cursors final)
+  const DevNode* parent;    // the parent's record
+  int32_t thr[2];           // children's split thresholds (256: child not split this round)
+  int32_t shift[2];
+};
+
+// Per-launch completion counters of the round's 2-means epilogues (device
+// memory, zeroed with the round's tables).
+struct alignas(16) LaunchCtr {
+  uint64_t word;            // low 32 bits: workgroups arrived; high: nodes not final
+  uint64_t pad;
+};
+
+// The last-arriving epilogue workgroup of 2-means iteration `it` publishes
+// the status word (round sequence << 32) | (active nodes << 1) | 1 to host
+// memory (RoundArgs::hstat[it]).
 
 }  // namespace dq

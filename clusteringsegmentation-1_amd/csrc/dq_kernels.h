@@ -10,7 +10,7 @@
 
 namespace dq {
 
-constexpr int kBlock = 256;                     // 4 wave64 per workgroup
+constexpr int kBlock = 64 * kTileWaves;          // 4 wave64 per workgroup
 constexpr int kVecPerThread = 4;                // uint4 loads per lane per sweep
 constexpr int kSweep = kBlock * kVecPerThread * 4;   // 4096 points per sweep
 constexpr uint32_t kMaxTilePx = 16 * kSweep;    // keeps packed 16-bit lane sums exact
@@ -23,22 +23,33 @@ constexpr int kCellRecWords = 4;                // 16-B record per cell
 constexpr int kCellCap = 32;                    // candidates in the overflow list
 constexpr uint32_t kCellBrute = 0xFFFF;         // count marker: scan the whole palette
 
-// Tables of one round (device pointers).
+// Tables of one round (device pointers unless noted).
 struct RoundArgs {
-  Tile* tiles;
-  DevNode* nodes;
+  Tile* tiles;              // the round's tiles (kept: a later round partitions through them)
+  DevNode* nodes;           // the round's node records (kept, as tiles)
   TilePartial* parts;       // one per tile, rewritten by every pass
+  uint32_t* wparts;         // per (tile, wave): old | new << 16 of the last 2-means pass
+  const PartTile* ptiles;   // fused partition + split work of this round
+  TilePartial* sparts;      // one per PartTile
+  NodeResult* hres;         // host-coherent pinned: final results per node
+  LaunchCtr* ctr;           // per 2-means iteration
+  uint64_t* hstat;          // host-coherent pinned: status word per 2-means iteration
+  uint64_t seq;             // round sequence number (tags the status words)
   int32_t fixed_point;      // epilogues finalise nodes at a 2-means fixed point
+  int32_t it;               // 2-means iteration of an epilogue launch
+  int32_t nn;               // nodes in the round
 };
 
-// One statistics pass over every tile of the round (one workgroup per tile).
+// One statistics pass over tiles [0, ntiles) of the round (one workgroup per tile).
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
 // The FP64 update after a pass, one workgroup per node: sums the node's tile
 // partials and publishes the next pass's decision (or the split's results).
 void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream);
-// Writes every node's points into its two children's segments (old half
-// first, then new half) of the child buffer, using the last 2-means decision.
-void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream);
+// Fused partition + split pass over the round's PartTiles: writes each
+// parent's points into its two children's segments (old half first, then new
+// half) of the child buffer, using the parent's final 2-means decision, and
+// accumulates the children's split-pass statistics.
+void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream);
 
 // Map: candidate records per colour cell, then the per-pixel argmin over
 // (squared distance, MPS visit rank).

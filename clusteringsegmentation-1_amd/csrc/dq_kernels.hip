@@ -14,10 +14,15 @@
 //                         4 B read per point.
 //   epilogue_kernel<KIND> per node: sum its tile partials in u64 and run the
 //                         reference's FP64 update (:561-598, :787-871),
-//                         publishing the next pass's decision in DevNode.
-//   partition_kernel      writes each node's points into its two children's
-//                         segments (replaces the per-split O(N) member[]
-//                         gather, :894-1026).  Reads 4 B, writes 4 B per point.
+//                         publishing the next pass's decision in DevNode;
+//                         a node whose split is final writes its results
+//                         straight to host memory; 2-means launches publish
+//                         a per-launch status word the host polls.
+//   partsplit_kernel      writes the points of nodes split in an earlier round
+//                         into their two children's segments (replaces the
+//                         per-split O(N) member[] gather, :894-1026) and
+//                         accumulates the children's split-pass statistics on
+//                         the way.  Reads 4 B, writes 4 B per point.
 //   build_cells_kernel    map: per 8x8x8 colour cell, the palette entries that
 //                         can be nearest to some colour of the cell.
 //   map_kernel            map: per pixel argmin over (squared distance, MPS
@@ -169,6 +174,7 @@ __device__ __forceinline__ bool goes_new(uint32_t p, const Params& q) {
 // them and with themselves sums their squares: 7 sums for ~5 ops per point.
 struct LaneSums {
   uint32_t cnt = 0, sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
+  uint32_t vcnt = 0;   // points of the lane inside the tile (partition cursors)
 };
 
 __device__ __forceinline__ void add4(const uint32_t m[4], LaneSums& s) {
@@ -186,10 +192,28 @@ __device__ __forceinline__ void add4(const uint32_t m[4], LaneSums& s) {
   s.qb = __builtin_amdgcn_udot4(bq, bq, s.qb, false);
 }
 
+// The split pass needs only the new side's count and sums (:438-559).
+struct SplitSums {
+  uint32_t cnt = 0, sr = 0, sg = 0, sb = 0;
+};
+
+__device__ __forceinline__ void add4_sums(const uint32_t m[4], SplitSums& s) {
+  const uint32_t u01 = __builtin_amdgcn_perm(m[1], m[0], 0x05010400u);  // B0 B1 G0 G1
+  const uint32_t u23 = __builtin_amdgcn_perm(m[3], m[2], 0x05010400u);  // B2 B3 G2 G3
+  const uint32_t bq = __builtin_amdgcn_perm(u23, u01, 0x05040100u);     // B0 B1 B2 B3
+  const uint32_t gq = __builtin_amdgcn_perm(u23, u01, 0x07060302u);     // G0 G1 G2 G3
+  const uint32_t rq = __builtin_amdgcn_perm(m[1], m[0], 0x0C0C0602u) |  // R0 R1 0 0
+                      __builtin_amdgcn_perm(m[3], m[2], 0x06020C0Cu);   // 0 0 R2 R3
+  s.sr = __builtin_amdgcn_udot4(rq, 0x01010101u, s.sr, false);
+  s.sg = __builtin_amdgcn_udot4(gq, 0x01010101u, s.sg, false);
+  s.sb = __builtin_amdgcn_udot4(bq, 0x01010101u, s.sb, false);
+}
+
 template <int KIND, bool FULL>
 __device__ __forceinline__ void sweep_sums(const u32x4 v[kVecPerThread], uint32_t vs,
                                            uint32_t start, uint32_t end, const Params& q,
                                            LaneSums& s) {
+  if (FULL) s.vcnt += kVecPerThread * 4;
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
     const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
@@ -198,7 +222,11 @@ __device__ __forceinline__ void sweep_sums(const u32x4 v[kVecPerThread], uint32_
     for (int e = 0; e < 4; ++e) {
       const uint32_t p = vec_elem(v[j], e);
       bool take = goes_new<KIND>(p, q);
-      if (!FULL) take = take && (i0 + e >= start) && (i0 + e < end);
+      if (!FULL) {
+        const bool valid = (i0 + e - start) < (end - start);
+        take = take && valid;
+        s.vcnt += valid ? 1u : 0u;
+      }
       m[e] = take ? p : 0u;
       s.cnt += take ? 1u : 0u;
     }
@@ -207,8 +235,8 @@ __device__ __forceinline__ void sweep_sums(const u32x4 v[kVecPerThread], uint32_
 }
 
 // The split's results from the final partition's sums (:787-871).
-__device__ void node_results(DevNode* w, const uint64_t t[F_NUM], const double om[3],
-                             const double nm[3], double nw, double ow) {
+__device__ void node_results(NodeResult* r, const DevNode* w, const uint64_t t[F_NUM],
+                             const double om[3], const double nm[3], double nw, double ow) {
   const double s = w->s, tw = w->tw;
   double nv[3], ov[3];
   for (int c = 0; c < 3; ++c) {                  // (:836-838)
@@ -222,24 +250,25 @@ __device__ void node_results(DevNode* w, const uint64_t t[F_NUM], const double o
     ov[c] = ((tw * w->tv[c] - nw * (nv[c] + dn * dn)) / ow) - dox * dox;
   }
   for (int c = 0; c < 3; ++c) {
-    w->om[c] = om[c];
-    w->nm[c] = nm[c];
-    w->nv[c] = nv[c];
-    w->ov[c] = ov[c];
+    r->om[c] = om[c];
+    r->nm[c] = nm[c];
+    r->nv[c] = nv[c];
+    r->ov[c] = ov[c];
   }
-  w->nw = nw;
-  w->ow = ow;
-  w->tse_old = ow * (ov[0] + ov[1] + ov[2]);   // (:870-871)
-  w->tse_new = nw * (nv[0] + nv[1] + nv[2]);
-  w->n_new = t[F_CNT];
+  r->nw = nw;
+  r->ow = ow;
+  r->tse_old = ow * (ov[0] + ov[1] + ov[2]);   // (:870-871)
+  r->tse_new = nw * (nv[0] + nv[1] + nv[2]);
+  r->n_new = t[F_CNT];
 }
 
 // The FP64 update after pass KIND from the node's total sums t[] (exact
-// integers).  Publishes the next pass's Params, or the split's results.
-// Returns true when the results are final (PASS_KLAST, or a PASS_KMEANS at a
-// fixed point: prm then already holds the decision that produced them).
+// integers).  Publishes the next pass's Params, or -- when the results are
+// final (PASS_KLAST, or a PASS_KMEANS at a fixed point: prm then already
+// holds the decision that produced them) -- the split's results into *r and
+// returns true.
 template <int KIND>
-__device__ bool node_update(DevNode* w, const uint64_t t[F_NUM], bool fixed_point) {
+__device__ bool node_update(DevNode* w, NodeResult* r, const uint64_t t[F_NUM], bool fixed_point) {
   const double s = w->s, tw = w->tw;
   if (KIND == PASS_INIT) {
     // DivQuantClusterInitMeanAndVar (:90-104), then the cut (:388-403).
@@ -266,26 +295,23 @@ __device__ bool node_update(DevNode* w, const uint64_t t[F_NUM], bool fixed_poin
   double tm[3];
   for (int c = 0; c < 3; ++c) tm[c] = w->tm[c];
   double om[3], nm[3], nw, ow;
+  bool final = KIND == PASS_KLAST;
   if (KIND == PASS_KMEANS) {
     w->iter += 1;
-    if (fixed_point && t[F_CNT] == w->prev[0] && t[F_SR] == w->prev[1] &&
-        t[F_SG] == w->prev[2] && t[F_SB] == w->prev[3]) {
-      means_from_sums(t, s, tw, tm, om, nm, &nw, &ow);
-      node_results(w, t, om, nm, nw, ow);
-      w->done_it = w->iter;
-      return true;
-    }
+    final = fixed_point && t[F_CNT] == w->prev[0] && t[F_SR] == w->prev[1] &&
+            t[F_SG] == w->prev[2] && t[F_SB] == w->prev[3];
   }
   means_from_sums(t, s, tw, tm, om, nm, &nw, &ow);
-  if (KIND == PASS_SPLIT || KIND == PASS_KMEANS) {
-    for (int c = 0; c < 4; ++c) w->prev[c] = t[F_CNT + c];
-    Params p = w->prm;
-    decision_from_means(om, nm, &p);
-    w->prm = p;
-    return false;
+  if (final) {
+    node_results(r, w, t, om, nm, nw, ow);
+    w->done_it = KIND == PASS_KMEANS ? w->iter : -1;
+    return true;
   }
-  node_results(w, t, om, nm, nw, ow);   // PASS_KLAST
-  return true;
+  for (int c = 0; c < 4; ++c) w->prev[c] = t[F_CNT + c];
+  Params p = w->prm;
+  decision_from_means(om, nm, &p);
+  w->prm = p;
+  return false;
 }
 
 }  // namespace
@@ -320,6 +346,11 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
   uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
 #pragma unroll
   for (int k = 0; k < kNF; ++k) f[k] = wave_sum_u32(f[k]);
+  if (KIND == PASS_KMEANS || KIND == PASS_KLAST) {
+    // this wave's (old, new) counts: the partition cursors if this pass is final
+    const uint32_t vsum = wave_sum_u32(s.vcnt);
+    if (lane_id() == 0) a.wparts[blockIdx.x * kTileWaves + wave_id()] = (vsum - f[F_CNT]) | (f[F_CNT] << 16);
+  }
   if (lane_id() == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) red[wave_id()][k] = k < kNF ? f[k] : 0u;
@@ -334,158 +365,311 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Epilogue: one workgroup per node.
+// Epilogue: one workgroup per node of the round.
+//   * sums the node's tile partials in u64 (PASS_SPLIT of a node whose
+//     parent was partitioned this round: its half of the parent's fused
+//     partition+split partials instead);
+//   * thread 0 runs the FP64 update (node_update);
+//   * a node whose split became final: each tile's first OLD point's rank
+//     among the node's old points (the partition's write cursors), and the
+//     results written straight to host memory (NodeResult);
+//   * 2-means launches: every workgroup arrives on the launch's counter; the
+//     last to arrive publishes (round seq, nodes still active) to the host,
+//     which stops launching iterations once no node is active.
 template <int KIND>
 __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
+  constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
   DevNode* w = a.nodes + blockIdx.x;
-  if ((KIND == PASS_KMEANS || KIND == PASS_KLAST) && w->done_it != 0) return;   // final
-  const int tb = w->tile_begin, te = w->tile_end;
-  constexpr bool kSquares = true;
-  constexpr int kNF = F_NUM;
-  const g_cu4* parts4 = (const g_cu4*)a.parts;
-
-  uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int base = tb; base < te; base += 4 * kBlock) {
-    u32x4 x[4], y[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {   // issue every load of the chunk first
-      const int i = base + u * kBlock + (int)threadIdx.x;
-      if (i < te) {
-        x[u] = parts4[2 * i];
-        if (kSquares) y[u] = parts4[2 * i + 1];
-      } else {
-        x[u] = (u32x4){0u, 0u, 0u, 0u};
-        y[u] = (u32x4){0u, 0u, 0u, 0u};
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      acc[0] += x[u][0];
-      acc[1] += x[u][1];
-      acc[2] += x[u][2];
-      acc[3] += x[u][3];
-      if (kSquares) {
-        acc[4] += y[u][0];
-        acc[5] += y[u][1];
-        acc[6] += y[u][2];
-      }
-    }
-  }
+  const bool skip = kMeans && w->done_it != 0;   // final in an earlier launch
   __shared__ uint64_t red[kBlock / 64][8];
-#pragma unroll
-  for (int k = 0; k < kNF; ++k) acc[k] = wave_sum_u64(acc[k]);
-  if (lane_id() == 0) {
-#pragma unroll
-    for (int k = 0; k < kNF; ++k) red[wave_id()][k] = acc[k];
-  }
   __shared__ int final_results;
-  __syncthreads();   // (every thread has read done_it above)
-  if (threadIdx.x == 0) {
-    uint64_t tot[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < kNF; ++k)
-      for (int v = 0; v < kBlock / 64; ++v) tot[k] += red[v][k];
-    final_results = node_update<KIND>(w, tot, a.fixed_point != 0) ? 1 : 0;
-  }
-  __syncthreads();
-  if ((KIND == PASS_KMEANS || KIND == PASS_KLAST) && final_results) {
-    // Each tile's first OLD point's rank among the node's old points: an
-    // exclusive scan of the tiles' old counts, chunked per lane.
-    __shared__ uint32_t scan[kBlock];
-    const int T = te - tb;
-    const int chunk = (T + kBlock - 1) / kBlock;
-    const int c0 = tb + (int)threadIdx.x * chunk;
-    const int c1 = min(te, c0 + chunk);
-    uint32_t local = 0;
-    for (int i = c0; i < c1; ++i)
-      local += (a.tiles[i].end - a.tiles[i].start) - a.parts[i].f[F_CNT];
-    scan[threadIdx.x] = local;
-    __syncthreads();
-    for (int o = 1; o < kBlock; o <<= 1) {
-      const uint32_t v = threadIdx.x >= (uint32_t)o ? scan[threadIdx.x - o] : 0u;
-      __syncthreads();
-      scan[threadIdx.x] += v;
-      __syncthreads();
+  __shared__ NodeResult sres;
+  if (threadIdx.x == 0) final_results = 0;
+  if (!skip) {
+    const int tb = w->tile_begin, te = w->tile_end;
+    const g_cu4* parts4 = (const g_cu4*)a.parts;
+    uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (KIND == PASS_SPLIT && w->split_pb >= 0) {
+      // children's (cnt, sums) of the fused pass: [0..3] old half, [4..7] new half
+      const g_cu4* sp4 = (const g_cu4*)a.sparts;
+      const int side = w->split_side;
+      for (int i = w->split_pb + (int)threadIdx.x; i < w->split_pe; i += kBlock) {
+        const u32x4 x = sp4[2 * i + side];
+        acc[0] += x[0];
+        acc[1] += x[1];
+        acc[2] += x[2];
+        acc[3] += x[3];
+      }
+    } else {
+      constexpr bool kSquares = KIND != PASS_SPLIT;
+      for (int base = tb; base < te; base += 4 * kBlock) {
+        u32x4 x[4], y[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {   // issue every load of the chunk first
+          const int i = base + u * kBlock + (int)threadIdx.x;
+          if (i < te) {
+            x[u] = parts4[2 * i];
+            if (kSquares) y[u] = parts4[2 * i + 1];
+          } else {
+            x[u] = (u32x4){0u, 0u, 0u, 0u};
+            y[u] = (u32x4){0u, 0u, 0u, 0u};
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc[0] += x[u][0];
+          acc[1] += x[u][1];
+          acc[2] += x[u][2];
+          acc[3] += x[u][3];
+          if (kSquares) {
+            acc[4] += y[u][0];
+            acc[5] += y[u][1];
+            acc[6] += y[u][2];
+          }
+        }
+      }
     }
-    uint32_t run = scan[threadIdx.x] - local;
-    for (int i = c0; i < c1; ++i) {
-      a.tiles[i].old_base = run;
-      run += (a.tiles[i].end - a.tiles[i].start) - a.parts[i].f[F_CNT];
+#pragma unroll
+    for (int k = 0; k < F_NUM; ++k) acc[k] = wave_sum_u64(acc[k]);
+    if (lane_id() == 0) {
+#pragma unroll
+      for (int k = 0; k < F_NUM; ++k) red[wave_id()][k] = acc[k];
+    }
+    __syncthreads();   // (every thread has read done_it above)
+    if (threadIdx.x == 0) {
+      uint64_t tot[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < F_NUM; ++k)
+        for (int v = 0; v < kBlock / 64; ++v) tot[k] += red[v][k];
+      const bool fin = node_update<KIND>(w, &sres, tot, a.fixed_point != 0);
+      if (fin) {
+        for (int c = 0; c < 3; ++c) { sres.tm[c] = w->tm[c]; sres.tv[c] = w->tv[c]; }
+        w->n_new_local = (uint32_t)tot[F_CNT];   // single shard: local == global
+        sres.n_new_local = (uint32_t)tot[F_CNT];
+        sres.done_it = w->done_it;
+      }
+      final_results = fin ? 1 : 0;
+    }
+    __syncthreads();
+    if (kMeans && final_results) {
+      // Partition cursors: for every (tile, wave) of the node, the OLD and
+      // NEW points of the node before its share -- an exclusive scan of the
+      // final pass's per-wave counts, chunked per lane over the tiles.
+      __shared__ uint64_t scan[kBlock];
+      const int T = te - tb;
+      const int chunk = (T + kBlock - 1) / kBlock;
+      const int c0 = tb + (int)threadIdx.x * chunk;
+      const int c1 = min(te, c0 + chunk);
+      const uint32_t* wp = a.wparts;
+      uint64_t local = 0;   // old | new << 32
+      for (int i = c0; i < c1; ++i)
+        for (int ww = 0; ww < kTileWaves; ++ww) {
+          const uint32_t x = wp[i * kTileWaves + ww];
+          local += (uint64_t)(x & 0xFFFFu) | ((uint64_t)(x >> 16) << 32);
+        }
+      scan[threadIdx.x] = local;
+      __syncthreads();
+      for (int o = 1; o < kBlock; o <<= 1) {
+        const uint64_t v = threadIdx.x >= (uint32_t)o ? scan[threadIdx.x - o] : 0ull;
+        __syncthreads();
+        scan[threadIdx.x] += v;
+        __syncthreads();
+      }
+      const uint64_t run0 = scan[threadIdx.x] - local;
+      uint32_t ro = (uint32_t)run0, rn = (uint32_t)(run0 >> 32);
+      for (int i = c0; i < c1; ++i)
+        for (int ww = 0; ww < kTileWaves; ++ww) {
+          const uint32_t x = wp[i * kTileWaves + ww];
+          a.tiles[i].old_base[ww] = ro;
+          a.tiles[i].new_base[ww] = rn;
+          ro += x & 0xFFFFu;
+          rn += x >> 16;
+        }
+    }
+  }
+  if (kMeans) {
+    __syncthreads();
+    // Final results go straight to host-coherent memory: relaxed system-scope
+    // 8-B stores, one per lane (no L2 write-back), drained before arriving.
+    constexpr int kWords = (int)(sizeof(NodeResult) / 8);
+    static_assert(kWords <= 64, "one wave stores the result");
+    if (final_results && threadIdx.x < kWords) {
+      const uint64_t v = reinterpret_cast<const uint64_t*>(&sres)[threadIdx.x];
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.hres + blockIdx.x) + threadIdx.x, v,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (threadIdx.x < 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0) {
+        // one 64-bit arrival: low word = workgroups arrived, high = still active
+        const uint64_t mine = 1ull | ((uint64_t)(!skip && !final_results) << 32);
+        const uint64_t old = __hip_atomic_fetch_add(&a.ctr[a.it].word, mine, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)old == (uint32_t)a.nn - 1) {
+          const uint64_t act = (old >> 32) + (mine >> 32);
+          __hip_atomic_store(a.hstat + a.it, (a.seq << 32) | (act << 1) | 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
     }
   }
 }
 
+// The 2-means decisions of one sweep as lane bit masks: bit s of oldm = slot
+// s stays OLD (:683), bit s of validm = slot s lies inside [start, end).
+// FP32 filter in 32-bit integer arithmetic (no 64-bit compare masks): with a
+// finite eps, df is finite, sign(df) > 0 <=> -bits(df) has bit 31 set (a -0
+// result has |df| <= eps and takes the exact path), and |df| <= eps <=>
+// bits(|df|) - bits(eps) - 1 has bit 31 set.  Points the filter cannot decide
+// (or every point, when the node's filter is off) take the exact FP64
+// expression; that branch is wave-uniform.
+template <bool FULL>
+__device__ __forceinline__ void decide_sweep(const u32x4 v[kVecPerThread], uint32_t vs,
+                                             uint32_t start, uint32_t end, const Params& q,
+                                             bool exact_all, uint32_t& oldm, uint32_t& validm) {
+  constexpr int kSlots = kVecPerThread * 4;
+  uint32_t om = 0, un = 0, vm = FULL ? 0xFFFFu : 0u;
+  const uint32_t epsb = __float_as_uint(q.eps);
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int sidx = j * 4 + e;
+      const uint32_t p = vec_elem(v[j], e);
+      const float R = (float)((p >> 16) & 0xFF);
+      const float G = (float)((p >> 8) & 0xFF);
+      const float B = (float)(p & 0xFF);
+      const float df = __builtin_fmaf(q.rrf, R, __builtin_fmaf(q.rgf, G, __builtin_fmaf(q.rbf, B, -q.lhsf)));
+      const uint32_t db = __float_as_uint(df);
+      om |= ((0u - db) >> 31) << sidx;
+      un |= (((db & 0x7FFFFFFFu) - epsb - 1u) >> 31) << sidx;
+      if (!FULL) {
+        const uint32_t i = i0 + e;
+        vm |= ((uint32_t)((i - start) < (end - start))) << sidx;
+      }
+    }
+  }
+  if (exact_all) un = 0xFFFFu;
+  if (__any(un != 0)) {
+#pragma unroll
+    for (int sidx = 0; sidx < kSlots; ++sidx) {
+      if ((un >> sidx) & 1u) {
+        const bool ex = stays_old_exact(vec_elem(v[sidx >> 2], sidx & 3), q);
+        om = (om & ~(1u << sidx)) | ((ex ? 1u : 0u) << sidx);
+      }
+    }
+  }
+  oldm = om & vm;
+  validm = vm;
+}
+
 // ---------------------------------------------------------------------------
-// Partition: replay the last 2-means decision (DevNode.prm, bit-identical
-// inputs -> bit-identical outcome) and write OLD points to [off, off+n_old)
-// and NEW points to [off+n_old, off+len) of the child buffer.  Within a sweep
-// points are ranked in (slot, wave, lane) order and tiles follow each other,
-// so each half is a fixed permutation of the parent's points.
-__global__ __launch_bounds__(kBlock) void partition_kernel(RoundArgs a) {
-  const Tile t = a.tiles[blockIdx.x];
-  const DevNode& nd = a.nodes[t.node];
+// Fused partition + split pass over the tiles of parents split in an earlier
+// round (replaces the reference's per-split O(N) member[] gather, :894-1026,
+// and the children's split pass, :438-559).  Replays the parent's final
+// 2-means decision (bit-identical inputs -> bit-identical outcome), writes
+// OLD points to [off, off+n_old) and NEW points to [off+n_old, off+len) of
+// the child buffer, and accumulates each child's split-pass statistics
+// (cut_pos < v_axis -> the child's new side) from the same registers.
+//
+// Every wave works alone: its share of the tile (the same points the final
+// 2-means pass gave it) starts at the cursors the finalising epilogue scanned
+// from that pass's per-wave counts (Tile::old_base / new_base).  Per sweep:
+// decisions into lane bit masks (FP64 only on a wave-uniform branch for
+// near-plane points), then per slot one ballot-ranked store of the wave's
+// points into the old or the new run (each store instruction covers at most
+// two contiguous runs of the child buffer), with the next sweep's loads in
+// flight.  No LDS and no barrier until the final reduction of the sums.
+// One 32-B partial per tile: [0..3] old child, [4..7] new child.
+__global__ __launch_bounds__(kBlock) void partsplit_kernel(RoundArgs a) {
+  constexpr int kSlots = kVecPerThread * 4;
+  const PartTile pt = a.ptiles[blockIdx.x];
+  const Tile* tp = pt.tile;
+  const DevNode& nd = *pt.parent;
+  const uint32_t w = wave_id(), l = lane_id();
+  const uint32_t start = tp->start, end = tp->end;
   g_cu4* src4 = as_g4(nd.src);
   g_u32* dst = as_gw(nd.dst);
   const Params q = nd.prm;
+  const uint32_t n_old = nd.len - nd.n_new_local;
+  uint32_t oc = nd.off + tp->old_base[w];
+  uint32_t nc = nd.off + n_old + tp->new_base[w];
+  const bool exact_all = !(q.eps < __builtin_inff());   // FP32 filter off for this node
+  const uint32_t sh0 = (uint32_t)pt.shift[0], sh1 = (uint32_t)pt.shift[1];
+  const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
+  SplitSums so, sn;
 
-  __shared__ uint32_t cnt[2][kVecPerThread * 4 * (kBlock / 64)];
-  __shared__ uint32_t tot[2];
-
-  const uint32_t n_old = nd.len - (uint32_t)nd.n_new;
-  uint32_t old_cur = nd.off + t.old_base;
-  uint32_t new_cur = nd.off + n_old + ((t.start - nd.off) - t.old_base);
-
-  const uint32_t w = wave_id(), l = lane_id();
-  constexpr int kSlots = kVecPerThread * 4;
   u32x4 v[kVecPerThread];
-  for (uint32_t vs = t.start & ~3u; vs < t.end; vs += kSweep) {
-    const bool full = vs >= t.start && vs + kSweep <= t.end;
-    if (full) load_sweep<true>(src4, vs, t.end, v);
-    else load_sweep<false>(src4, vs, t.end, v);
-    uint32_t slot[kSlots];   // bit 31: old, bit 30: new; low bits: rank in wave
+  uint32_t vs = start & ~3u;
+  bool full = vs >= start && vs + kSweep <= end;
+  if (vs < end) {
+    if (full) load_sweep<true>(src4, vs, end, v);
+    else load_sweep<false>(src4, vs, end, v);
+  }
+  while (vs < end) {
+    uint32_t oldm, validm;
+    if (full) decide_sweep<true>(v, vs, start, end, q, exact_all, oldm, validm);
+    else decide_sweep<false>(v, vs, start, end, q, exact_all, oldm, validm);
+    const uint32_t newm = validm & ~oldm;
+    // --- the children's split pass on the same registers: bit arithmetic,
+    //     (byte - thr) >> 31 == 0  <=>  byte >= thr  <=>  cut_pos < byte
 #pragma unroll
     for (int j = 0; j < kVecPerThread; ++j) {
-      const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
+      uint32_t mo[4], mn[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const uint32_t p = vec_elem(v[j], e);
-        const uint32_t i = i0 + e;
-        const bool valid = full || ((i >= t.start) & (i < t.end));
-        const bool old = valid && stays_old(p, q);
-        const bool nw = valid && !old;
-        const uint64_t mo = __ballot(old), mn = __ballot(nw);
         const int sidx = j * 4 + e;
-        slot[sidx] = old ? (0x80000000u | mbcnt64(mo)) : (nw ? (0x40000000u | mbcnt64(mn)) : 0u);
-        if (l == 0) {
-          cnt[0][sidx * (kBlock / 64) + w] = (uint32_t)__popcll(mo);
-          cnt[1][sidx * (kBlock / 64) + w] = (uint32_t)__popcll(mn);
-        }
+        const uint32_t p = vec_elem(v[j], e);
+        const uint32_t b0 = ((uint32_t)((int32_t)((p >> sh0) & 0xFF) - thr0) >> 31) ^ 1u;
+        const uint32_t b1 = ((uint32_t)((int32_t)((p >> sh1) & 0xFF) - thr1) >> 31) ^ 1u;
+        const uint32_t so_new = b0 & (oldm >> sidx);
+        const uint32_t sn_new = b1 & (newm >> sidx);
+        mo[e] = p & (0u - (so_new & 1u));
+        mn[e] = p & (0u - (sn_new & 1u));
+        so.cnt += so_new & 1u;
+        sn.cnt += sn_new & 1u;
       }
+      add4_sums(mo, so);
+      add4_sums(mn, sn);
     }
-    __syncthreads();
-    // Exclusive scan over the 64 (slot, wave) counts: wave 0 old, wave 1 new.
-    if (w < 2) {
-      const uint32_t val = cnt[w][l];
-      uint32_t inc = val;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(inc, o, 64);
-        if (l >= (uint32_t)o) inc += u;
-      }
-      cnt[w][l] = inc - val;
-      if (l == 63) tot[w] = inc;
+    // --- next sweep's loads in flight during the stores
+    const uint32_t nvs = vs + kSweep;
+    const bool nfull = nvs >= start && nvs + kSweep <= end;
+    u32x4 vn[kVecPerThread];
+    if (nvs < end) {
+      if (nfull) load_sweep<true>(src4, nvs, end, vn);
+      else load_sweep<false>(src4, nvs, end, vn);
     }
-    __syncthreads();
+    // --- this wave's points, slot by slot, ranked by ballot
 #pragma unroll
     for (int sidx = 0; sidx < kSlots; ++sidx) {
-      const uint32_t sl = slot[sidx];
-      const uint32_t r = sl & 0x3FFFFFFFu;
-      const uint32_t p = vec_elem(v[sidx >> 2], sidx & 3);
-      if (sl & 0x80000000u) dst[old_cur + cnt[0][sidx * (kBlock / 64) + w] + r] = p;
-      else if (sl & 0x40000000u) dst[new_cur + cnt[1][sidx * (kBlock / 64) + w] + r] = p;
+      const bool o = (oldm >> sidx) & 1u, n = (newm >> sidx) & 1u;
+      const uint64_t bo = __ballot(o), bn = __ballot(n);
+      const uint32_t idx = o ? oc + mbcnt64(bo) : nc + mbcnt64(bn);
+      if (o || n) dst[idx] = vec_elem(v[sidx >> 2], sidx & 3);
+      oc += (uint32_t)__popcll(bo);
+      nc += (uint32_t)__popcll(bn);
     }
-    old_cur += tot[0];
-    new_cur += tot[1];
-    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kVecPerThread; ++j) v[j] = vn[j];
+    vs = nvs;
+    full = nfull;
+  }
+
+  __shared__ uint32_t red[kTileWaves][8];
+  uint32_t f[8] = {so.cnt, so.sr, so.sg, so.sb, sn.cnt, sn.sr, sn.sg, sn.sb};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = wave_sum_u32(f[k]);
+  if (l == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[w][k] = f[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int ww = 0; ww < kTileWaves; ++ww) x += red[ww][threadIdx.x];
+    as_gw(a.sparts[blockIdx.x].f)[threadIdx.x] = x;
   }
 }
 
@@ -705,9 +889,9 @@ void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t strea
   }
 }
 
-void launch_partition(const RoundArgs& a, int ntiles, hipStream_t stream) {
-  if (ntiles <= 0) return;
-  partition_kernel<<<dim3(ntiles), dim3(kBlock), 0, stream>>>(a);
+void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream) {
+  if (nptiles <= 0) return;
+  partsplit_kernel<<<dim3(nptiles), dim3(kBlock), 0, stream>>>(a);
 }
 
 void launch_build_cells(const uint32_t* pal_sorted, int k, uint32_t* cell_rec,

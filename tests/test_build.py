@@ -1,6 +1,6 @@
 """CPU: build-level guarantees of the gfx950 code object.
 
-* No FP64 contraction: the pass and partition kernels evaluate the
+* No FP64 contraction: the pass and partsplit kernels evaluate the
   reference's decision as separate roundings; a v_fma_f64 there would change
   results.  (Epilogue kernels contain v_fma_f64 only inside the correctly
   rounded f64 division sequence: 5 per v_div_fixup_f64.)
@@ -35,7 +35,7 @@ def _named(funcs, part):
 
 
 def test_no_fp64_contraction_in_decisions(kernels):
-    for name, body in list(_named(kernels, "pass_kernel").items()) + list(_named(kernels, "partition_kernel").items()):
+    for name, body in list(_named(kernels, "pass_kernel").items()) + list(_named(kernels, "partsplit_kernel").items()):
         assert "v_fma_f64" not in body and "v_fmac_f64" not in body, name
 
 
@@ -67,7 +67,7 @@ def test_epilogue_fma_only_in_divisions(kernels, tmp_path):
 
 
 def test_streaming_kernels_use_global_memory(kernels):
-    for part in ("pass_kernel", "partition_kernel", "map_kernel"):
+    for part in ("pass_kernel", "partsplit_kernel", "map_kernel"):
         for name, body in _named(kernels, part).items():
             assert not re.search(r"\bflat_(load|store)", body), name
             assert re.search(r"global_load_dwordx4", body), name
