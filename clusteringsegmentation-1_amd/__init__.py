@@ -14,7 +14,9 @@ Reference-named entry points (same argument meaning, host numpy arrays):
     map_colors_mps(pixels, colortable)                       -> out
     quant_varpart_fast(pixels, num_clusters, max_iters=10)   -> colortable
 Device-resident entry points (torch tensors / raw device pointers on HBM):
-    quant_device, cluster_device, map_device
+    quant_device, quant_batch_device, cluster_device, map_device
+Row-tile sharding (one frame over shards / GPUs, RCCL allreduce per pass):
+    quant_rows_device, comm_init_torch (comm_unique_id, comm_init, comm_destroy)
 """
 import ctypes
 import os
@@ -61,6 +63,11 @@ def lib():
         "dq_hip_quant_dev": ([c.c_int, vp, c.c_uint32, vp, u32p, vp, c.c_int, vp], c.c_int),
         "dq_hip_quant_batch_dev": ([c.c_int, c.c_int, vp, vp, vp, c.c_uint32, vp, vp, c.c_int, vp],
                                    c.c_int),
+        "dq_hip_quant_rows_dev": ([c.c_int, c.c_int, vp, vp, vp, vp, c.c_int, vp, c.c_uint32, vp, vp,
+                                   c.c_int, vp], c.c_int),
+        "dq_hip_comm_unique_id": ([vp], c.c_int),
+        "dq_hip_comm_init": ([c.c_int, c.c_int, c.c_int, vp], c.c_int),
+        "dq_hip_comm_destroy": ([c.c_int], c.c_int),
         "dq_hip_cluster_dev": ([c.c_int, vp, c.c_uint32, u32p, vp, c.c_int, vp], c.c_int),
         "dq_hip_map_dev": ([c.c_int, vp, c.c_uint32, vp, vp, c.c_int, vp], c.c_int),
         "dq_hip_last_centroids": ([c.c_int, vp, vp, c.c_int], c.c_int),
@@ -182,6 +189,65 @@ def quant_batch_device(t_ins, t_outs, num_clusters, max_iters=10, device=0, stre
     if r < 0:
         raise DivQuantError("dq_hip_quant_batch_dev: bad arguments")
     return [ct[i, :kout[i]].copy() for i in range(nf)], r
+
+
+def quant_rows_device(t_ins, t_outs, num_clusters, widths=None, n_globals=None, nshard=1,
+                      max_iters=10, device=0, stream=None):
+    """Row-tile sharded quant_recurse: t_ins[i] holds THIS
+    process's rows of frame i.  nshard > 1 splits them into row ranges
+    processed as separate shards on this GPU; n_globals[i] > numel means the
+    other rows live in other processes, joined by the RCCL communicator of
+    comm_init (every pass's integer node totals are allreduced).  Returns
+    ([colortable per frame], total_empty) -- identical on every process."""
+    nf = len(t_ins)
+    ins = (ctypes.c_void_p * nf)(*[_dptr(t).value for t in t_ins])
+    outs = None
+    if t_outs is not None:
+        outs = (ctypes.c_void_p * nf)(*[_dptr(t).value for t in t_outs])
+    ns = np.array([t.numel() for t in t_ins], np.uint32)
+    ws = np.array(widths if widths is not None else [0] * nf, np.uint32)
+    ng = np.array(n_globals if n_globals is not None else [0] * nf, np.uint64)
+    ct = np.zeros((nf, num_clusters), np.uint32)
+    kout = np.zeros(nf, np.uint32)
+    r = lib().dq_hip_quant_rows_dev(device, nf, ctypes.cast(ins, ctypes.c_void_p), _ptr(ns),
+                                    _ptr(ws), _ptr(ng), nshard,
+                                    ctypes.cast(outs, ctypes.c_void_p) if outs is not None else None,
+                                    num_clusters, _ptr(ct), _ptr(kout), max_iters,
+                                    _stream_ptr(stream))
+    if r == -2:
+        raise DivQuantError("dq_hip_quant_rows_dev: n_global > n needs comm_init first")
+    if r < 0:
+        raise DivQuantError("dq_hip_quant_rows_dev: bad arguments")
+    return [ct[i, :kout[i]].copy() for i in range(nf)], r
+
+
+def comm_unique_id():
+    """128-byte RCCL id (rank 0 creates it; broadcast it to the other ranks)."""
+    buf = ctypes.create_string_buffer(128)
+    if lib().dq_hip_comm_unique_id(buf) != 0:
+        raise DivQuantError("dq_hip_comm_unique_id failed")
+    return buf.raw
+
+
+def comm_init(nranks, rank, uid, device=0):
+    """Join the engine on `device` to an RCCL communicator (one process per GPU)."""
+    buf = ctypes.create_string_buffer(bytes(uid), 128)
+    if lib().dq_hip_comm_init(device, nranks, rank, buf) != 0:
+        raise DivQuantError("dq_hip_comm_init: bad arguments")
+
+
+def comm_destroy(device=0):
+    lib().dq_hip_comm_destroy(device)
+
+
+def comm_init_torch(device=0, group=None):
+    """comm_init over an initialised torch.distributed process group: rank 0's
+    id is broadcast with the group (any backend), then every rank joins."""
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    obj = [comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    comm_init(world, rank, obj[0], device=device)
 
 
 def cluster_device(t_in, num_clusters, max_iters=10, device=0, n=None, stream=None):

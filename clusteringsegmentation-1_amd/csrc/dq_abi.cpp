@@ -127,6 +127,61 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
   return empty;
 }
 
+int dq_hip_quant_rows_dev(int device, int nframes, const uint32_t* const* d_in,
+                          const uint32_t* n, const uint32_t* width, const uint64_t* n_global,
+                          int nshard, uint32_t* const* d_out, uint32_t k, uint32_t* ct,
+                          uint32_t* k_out, int max_iters, void* stream) {
+  if (nframes <= 0 || !d_in || !n || !ct || !k_out || k == 0 || max_iters < 1) return -1;
+  if (nshard < 1 || nshard > dq::kMaxShard) return -1;
+  Engine& e = engine_for(device);
+  for (int i = 0; i < nframes; ++i) {
+    if (!d_in[i] || n[i] == 0) return -1;
+    const uint64_t ng = n_global ? n_global[i] : 0;
+    if (ng != 0 && ng < n[i]) return -1;
+    if (ng > n[i] && e.comm_ranks() < 2) return -2;   // other rows live in other processes
+  }
+  std::lock_guard<std::mutex> g(e.mutex());
+  std::vector<dq::FrameJob> jobs(nframes);
+  for (int i = 0; i < nframes; ++i) {
+    jobs[i].d_in = d_in[i];
+    jobs[i].n = n[i];
+    jobs[i].d_out = d_out ? d_out[i] : nullptr;
+    jobs[i].k = (int)k;
+    jobs[i].ct = ct + (size_t)i * k;
+    jobs[i].nshard = nshard;
+    jobs[i].width = width ? width[i] : 0;
+    jobs[i].n_global = n_global ? n_global[i] : 0;
+  }
+  e.run(jobs.data(), nframes, max_iters, true, (hipStream_t)stream);
+  int empty = 0;
+  for (int i = 0; i < nframes; ++i) {
+    k_out[i] = (uint32_t)jobs[i].k_out;
+    empty += jobs[i].num_empty;
+  }
+  return empty;
+}
+
+int dq_hip_comm_unique_id(void* id128) {
+  if (!id128) return -1;
+  Engine::comm_unique_id(static_cast<char*>(id128));
+  return 0;
+}
+
+int dq_hip_comm_init(int device, int nranks, int rank, const void* id128) {
+  if (!id128 || nranks < 1 || rank < 0 || rank >= nranks) return -1;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  e.comm_init(nranks, rank, static_cast<const char*>(id128));
+  return 0;
+}
+
+int dq_hip_comm_destroy(int device) {
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  e.comm_destroy();
+  return 0;
+}
+
 int dq_hip_quant_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out,
                      uint32_t* k, uint32_t* ct, int max_iters, void* stream) {
   if (!d_in || !d_out || !k || !ct || n == 0 || *k == 0 || max_iters < 1) return -1;

@@ -1,6 +1,8 @@
 // dq_engine.cpp -- host side of the DivQuant hot path (see dq_engine.h).
 #include "dq_engine.h"
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -231,13 +233,19 @@ uint32_t Engine::wait_status(int it, uint64_t seq, hipStream_t stream) {
   }
 }
 
-const uint32_t* Engine::buf_ptr(int buf, const FrameState& f) const {
-  if (buf == BUF_IN) return f.in;
-  return (buf == BUF_P0 ? d_p0_ : d_p1_) + f.base;
+const uint32_t* Engine::buf_ptr(int buf, const FrameState& f, int shard) const {
+  if (buf == BUF_IN) return f.in[shard];
+  return (buf == BUF_P0 ? d_p0_ : d_p1_) + f.base[shard];
 }
 
 // ---------------------------------------------------------------------------
 // One round: split every node in `active` (one launch per pass for all).
+//
+// Every logical node has one RECORD per shard (record r = node * S + shard):
+// the passes run over each record's own (local) points; the FP64 update
+// needs the node's sums over all shards and all processes -- one fused
+// epilogue when S == 1 and no communicator, else nodesum (over the records)
+// + RCCL allreduce (over the processes) + epilogue from the totals.
 //
 // A node whose parent was split in an earlier round but not yet partitioned
 // gets its points and its split-pass statistics from ONE fused launch over
@@ -248,8 +256,10 @@ const uint32_t* Engine::buf_ptr(int buf, const FrameState& f) const {
 void Engine::run_round(const std::vector<int>& active_in, bool root_round, int max_iters,
                        hipStream_t stream) {
   const double tb0 = trace_ ? host_us() : 0.0;
+  const int S = nshard_;
+  const bool sharded = S > 1 || comm_ != nullptr;
   std::vector<int> order, parents;
-  // node id -> slot in the round / position in `parents` (-1: none)
+  // node id -> logical slot in the round / position in `parents` (-1: none)
   slot_of_.assign(nodes_.size(), -1);
   parent_pos_.assign(nodes_.size(), -1);
   for (int id : active_in)
@@ -264,34 +274,45 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       parents.push_back(p);
     }
   }
-  const int nn = (int)order.size();
+  const int nl = (int)order.size();   // logical nodes
+  const int nr = nl * S;              // records
 
-  uint64_t total = 0, own_total = 0, parent_total = 0;
-  for (int a = 0; a < nn; ++a) {
-    total += nodes_[order[a]].len;
-    if (a < n_own) own_total += nodes_[order[a]].len;
-  }
-  for (int p : parents) parent_total += nodes_[p].len;
+  uint64_t total = 0, own_total = 0, parent_total = 0;   // local points
+  for (int a = 0; a < nl; ++a)
+    for (int sh = 0; sh < S; ++sh) {
+      total += nodes_[order[a]].len[sh];
+      if (a < n_own) own_total += nodes_[order[a]].len[sh];
+    }
+  for (int p : parents)
+    for (int sh = 0; sh < S; ++sh) parent_total += nodes_[p].len[sh];
   // Tile length: whole 4096-point sweeps, ~1024 tiles for big rounds (4 per
   // CU: measured best for one 4K frame and for 8-frame batches, microbench).
   uint64_t tl = (total + 1023) / 1024;
   tl = ((tl + kSweep - 1) / kSweep) * kSweep;
   tl = std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, kMaxTilePx));
   size_t ntiles = 0, nt_own = 0;
-  for (int a = 0; a < nn; ++a) {   // empty nodes get one empty tile (their epilogue still runs)
-    ntiles += std::max<size_t>(1, (nodes_[order[a]].len + tl - 1) / tl);
+  for (int a = 0; a < nl; ++a) {   // empty records get one empty tile (their epilogue still runs)
+    for (int sh = 0; sh < S; ++sh)
+      ntiles += std::max<size_t>(1, (nodes_[order[a]].len[sh] + tl - 1) / tl);
     if (a == n_own - 1) nt_own = ntiles;
   }
   size_t nptiles = 0;
-  for (int p : parents) nptiles += nodes_[p].ntiles;
+  for (int p : parents)
+    for (int sh = 0; sh < S; ++sh) nptiles += nodes_[p].ntiles[sh];
 
-  // the round's block: [DevNode nn | Tile ntiles | PartTile nptiles | LaunchCtr max_iters]
+  // the round's block: [DevNode nr | Tile ntiles | PartTile nptiles | LaunchCtr max_iters]
   auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
-  const size_t o_tiles = al(nn * sizeof(DevNode));
+  const size_t o_tiles = al(nr * sizeof(DevNode));
   const size_t o_pt = o_tiles + al(ntiles * sizeof(Tile));
   const size_t o_ctr = o_pt + al(nptiles * sizeof(PartTile));
   const size_t bytes = o_ctr + al((size_t)max_iters * sizeof(LaunchCtr));
-  ensure_round(nn, ntiles, nptiles, bytes, max_iters, stream);
+  ensure_round(nr, ntiles, nptiles, bytes, max_iters, stream);
+  if (sharded && (size_t)nl * 8 > cap_tot_) {
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (d_tot_) DQ_HIP(hipFree(d_tot_));
+    cap_tot_ = std::max<size_t>((size_t)nl * 8, 4096);
+    DQ_HIP(hipMalloc((void**)&d_tot_, cap_tot_ * sizeof(uint64_t)));
+  }
   char* dblk = arena_alloc(bytes);
   std::memset(h_stage_, 0, bytes);
   DevNode* hn = reinterpret_cast<DevNode*>(h_stage_);
@@ -300,35 +321,22 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   DevNode* dn = reinterpret_cast<DevNode*>(dblk);
   Tile* dt = reinterpret_cast<Tile*>(dblk + o_tiles);
 
-  std::vector<int> slot_of_parent_pt(parents.size());   // first PartTile of each parent
+  // first PartTile of each (parent, shard)
+  std::vector<int> pt_first(parents.size() * S);
   {
     int q = 0;
-    for (size_t i = 0; i < parents.size(); ++i) {
-      slot_of_parent_pt[i] = q;
-      q += nodes_[parents[i]].ntiles;
-    }
+    for (size_t i = 0; i < parents.size(); ++i)
+      for (int sh = 0; sh < S; ++sh) {
+        pt_first[i * S + sh] = q;
+        q += nodes_[parents[i]].ntiles[sh];
+      }
   }
   int t = 0;
-  for (int a = 0; a < nn; ++a) {
+  for (int a = 0; a < nl; ++a) {
     const Node& n = nodes_[order[a]];
     slot_of_[order[a]] = a;
     const FrameState& fs = frames_[n.frame];
-    DevNode& d = hn[a];
-    d.src = buf_ptr(n.buf, fs);
-    d.dst = (child_buf(n.buf) == BUF_P0 ? d_p0_ : d_p1_) + fs.base;
-    d.off = n.off;
-    d.len = n.len;
-    d.s = fs.s;
-    d.tw = n.w;
-    d.split_pb = -1;
-    d.split_pe = -1;
-    if (a >= n_own) {
-      const int pi = parent_pos_[n.parent];
-      d.split_pb = slot_of_parent_pt[pi];
-      d.split_pe = d.split_pb + nodes_[n.parent].ntiles;
-      d.split_side = nodes_[n.parent].child_new == order[a] ? 1 : 0;
-    }
-    for (int c = 0; c < 3; ++c) { d.tm[c] = n.mean[c]; d.tv[c] = n.var[c]; }
+    int32_t thr = 0, shift = 0;
     if (!root_round) {
       // Cut axis/position (:388-403): comparisons and copies only.  (The
       // root's come from its PASS_INIT epilogue on the device.)
@@ -336,17 +344,37 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       int axis = 0;
       if (maxv < n.var[1]) { maxv = n.var[1]; axis = 1; cut = n.mean[1]; }
       if (maxv < n.var[2]) { axis = 2; cut = n.mean[2]; }
-      d.prm.thr = split_threshold(cut);
-      d.prm.shift = 16 - 8 * axis;
+      thr = split_threshold(cut);
+      shift = 16 - 8 * axis;
     }
-    d.tile_begin = t;
-    for (uint64_t o = 0; o == 0 || o < n.len; o += tl) {
-      Tile& tt = ht[t++];
-      tt.node = a;
-      tt.start = n.off + (uint32_t)o;
-      tt.end = n.off + (uint32_t)std::min<uint64_t>(n.len, o + tl);
+    for (int sh = 0; sh < S; ++sh) {
+      DevNode& d = hn[a * S + sh];
+      d.src = buf_ptr(n.buf, fs, sh);
+      d.dst = (child_buf(n.buf) == BUF_P0 ? d_p0_ : d_p1_) + fs.base[sh];
+      d.off = n.off[sh];
+      d.len = n.len[sh];
+      d.s = fs.s;
+      d.tw = n.w;
+      d.split_pb = -1;
+      d.split_pe = -1;
+      if (a >= n_own) {
+        const int pi = parent_pos_[n.parent];
+        d.split_pb = pt_first[pi * S + sh];
+        d.split_pe = d.split_pb + nodes_[n.parent].ntiles[sh];
+        d.split_side = nodes_[n.parent].child_new == order[a] ? 1 : 0;
+      }
+      for (int c = 0; c < 3; ++c) { d.tm[c] = n.mean[c]; d.tv[c] = n.var[c]; }
+      d.prm.thr = thr;
+      d.prm.shift = shift;
+      d.tile_begin = t;
+      for (uint64_t o = 0; o == 0 || o < n.len[sh]; o += tl) {
+        Tile& tt = ht[t++];
+        tt.node = a * S + sh;
+        tt.start = n.off[sh] + (uint32_t)o;
+        tt.end = n.off[sh] + (uint32_t)std::min<uint64_t>(n.len[sh], o + tl);
+      }
+      d.tile_end = t;
     }
-    d.tile_end = t;
   }
   {
     int q = 0;
@@ -356,18 +384,19 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       const int ch[2] = {pn.child_old, pn.child_new};
       for (int c = 0; c < 2; ++c) {
         const int sl = slot_of_[ch[c]];
-        thr[c] = sl >= 0 ? hn[sl].prm.thr : 256;   // 256: nothing counted
-        shift[c] = sl >= 0 ? hn[sl].prm.shift : 0;
+        thr[c] = sl >= 0 ? hn[sl * S].prm.thr : 256;   // 256: nothing counted
+        shift[c] = sl >= 0 ? hn[sl * S].prm.shift : 0;
       }
-      for (int i = 0; i < pn.ntiles; ++i) {
-        PartTile& pt = hp[q++];
-        pt.tile = pn.dtiles + i;
-        pt.parent = pn.dnode;
-        pt.thr[0] = thr[0];
-        pt.thr[1] = thr[1];
-        pt.shift[0] = shift[0];
-        pt.shift[1] = shift[1];
-      }
+      for (int sh = 0; sh < S; ++sh)
+        for (int i = 0; i < pn.ntiles[sh]; ++i) {
+          PartTile& pt = hp[q++];
+          pt.tile = pn.dtiles[sh] + i;
+          pt.parent = pn.dnode[sh];
+          pt.thr[0] = thr[0];
+          pt.thr[1] = thr[1];
+          pt.shift[0] = shift[0];
+          pt.shift[1] = shift[1];
+        }
     }
   }
   DQ_HIP(hipMemcpyAsync(dblk, h_stage_, bytes, hipMemcpyHostToDevice, stream));
@@ -387,7 +416,10 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   ra.seq = seq;
   ra.fixed_point = fixed_point_ ? 1 : 0;
   ra.it = 0;
-  ra.nn = nn;
+  ra.nn = nr;
+  ra.tot = d_tot_;
+  ra.nshard = S;
+  ra.pad = 0;
   const double bytes_all = 4.0 * (double)total;
   const int nt = (int)ntiles;
   // 2-means passes (iteration index) whose timing entry gets its swept bytes
@@ -405,7 +437,11 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   auto epilogue = [&](int kind, int it) {
     ra.it = it < 0 ? 0 : it;
     timed_begin(stream);
-    launch_epilogue(kind, ra, nn, stream);
+    if (sharded) {
+      launch_nodesum(kind, ra, nl, stream);
+      if (comm_) allreduce_totals(nl, stream);
+    }
+    launch_epilogue(kind, ra, nr, sharded, stream);
     timed_end(ST_EPILOGUE, 0.0, stream);
   };
   if (root_round) {
@@ -439,9 +475,10 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   // before it (done_it <= 0: final at the last iteration, or it < done_it)
   auto swept_in = [&](int it) {
     uint64_t px = 0;
-    for (int a = 0; a < nn; ++a) {
-      const int di = h_res_[a].done_it;
-      if (di <= 0 || it < di) px += nodes_[order[a]].len;
+    for (int a = 0; a < nl; ++a) {
+      const int di = h_res_[a * S].done_it;
+      if (di <= 0 || it < di)
+        for (int sh = 0; sh < S; ++sh) px += nodes_[order[a]].len[sh];
     }
     return px;
   };
@@ -455,39 +492,43 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   }
 
   for (int p : parents) nodes_[p].partitioned = true;
-  int tcur = 0;
-  for (int a = 0; a < nn; ++a) {
+  for (int a = 0; a < nl; ++a) {
     const int id = order[a];
-    const NodeResult& r = h_res_[a];
+    const NodeResult& r = h_res_[a * S];   // global results: every record agrees
     if (root_round) {
       for (int c = 0; c < 3; ++c) { nodes_[id].mean[c] = r.tm[c]; nodes_[id].var[c] = r.tv[c]; }
     }
-    const int ntl = hn[a].tile_end - hn[a].tile_begin;
-    nodes_[id].dnode = dn + a;
-    nodes_[id].dtiles = dt + tcur;
-    nodes_[id].ntiles = ntl;
-    tcur += ntl;
-    const Node& p = nodes_[id];
-    const uint32_t n_new = r.n_new_local;
-    const uint32_t n_old = p.len - n_new;
     Node co, cn;
-    co.frame = cn.frame = p.frame;
-    co.parent = cn.parent = id;
-    co.w = r.ow;
-    cn.w = r.nw;
-    for (int c = 0; c < 3; ++c) {
-      co.mean[c] = r.om[c];
-      cn.mean[c] = r.nm[c];
-      co.var[c] = r.ov[c];
-      cn.var[c] = r.nv[c];
+    {
+      Node& p = nodes_[id];
+      for (int sh = 0; sh < S; ++sh) {
+        const DevNode& d = hn[a * S + sh];
+        p.dnode[sh] = dn + a * S + sh;
+        p.dtiles[sh] = dt + d.tile_begin;
+        p.ntiles[sh] = d.tile_end - d.tile_begin;
+        const uint32_t n_new = h_res_[a * S + sh].n_new_local;
+        const uint32_t n_old = p.len[sh] - n_new;
+        co.off[sh] = p.off[sh];
+        co.len[sh] = n_old;
+        cn.off[sh] = p.off[sh] + n_old;
+        cn.len[sh] = n_new;
+      }
+      co.frame = cn.frame = p.frame;
+      co.parent = cn.parent = id;
+      co.w = r.ow;
+      cn.w = r.nw;
+      for (int c = 0; c < 3; ++c) {
+        co.mean[c] = r.om[c];
+        cn.mean[c] = r.nm[c];
+        co.var[c] = r.ov[c];
+        cn.var[c] = r.nv[c];
+      }
+      co.tse = r.tse_old;
+      cn.tse = r.tse_new;
+      cn.glen = r.n_new;
+      co.glen = p.glen - r.n_new;
+      co.buf = cn.buf = child_buf(p.buf);
     }
-    co.tse = r.tse_old;
-    cn.tse = r.tse_new;
-    co.off = p.off;
-    co.len = n_old;
-    cn.off = p.off + n_old;
-    cn.len = n_new;
-    co.buf = cn.buf = child_buf(p.buf);
     const int io = (int)nodes_.size();
     nodes_.push_back(co);
     nodes_.push_back(cn);
@@ -511,8 +552,8 @@ void Engine::replay(FrameState& f) {
     const int co = nodes_[x].child_old, cn = nodes_[x].child_new;
     f.trace.push_back(f.new_index);
     f.trace.push_back(f.old_index);
-    f.trace.push_back(nodes_[x].len);
-    f.trace.push_back(nodes_[cn].len);
+    f.trace.push_back((int64_t)nodes_[x].glen);
+    f.trace.push_back((int64_t)nodes_[cn].glen);
     f.leaf[f.old_index] = co;
     f.leaf[f.new_index] = cn;
     if (f.new_index == k - 1) { ++f.new_index; return; }     // :823-832
@@ -559,15 +600,15 @@ void Engine::finish_frame(FrameState& f, bool last) {
   if (k == 1) {
     // No split happens: mean[0] keeps its zero initialisation (:309).
     job.ct[out++] = 0;
-    if (last) last_sizes[0] = job.n;
+    if (last) last_sizes[0] = (int64_t)(job.n_global ? job.n_global : job.n);
   } else {
     for (int ic = 0; ic < k; ++ic) {
       const Node& nd = nodes_[f.leaf[ic]];
       if (last) {
         for (int c = 0; c < 3; ++c) last_means[3 * ic + c] = nd.mean[c];
-        last_sizes[ic] = nd.len;
+        last_sizes[ic] = (int64_t)nd.glen;
       }
-      if (nd.len > 0) {
+      if (nd.glen > 0) {
         const uint32_t R = (uint8_t)(nd.mean[0] + 0.5);
         const uint32_t G = (uint8_t)(nd.mean[1] + 0.5);
         const uint32_t B = (uint8_t)(nd.mean[2] + 0.5);
@@ -595,16 +636,40 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   last_rounds = 0;
   last_points_swept = 0;
   last_points_full = 0;
+  nshard_ = jobs[0].nshard;
+  DQ_CHECK(nshard_ >= 1 && nshard_ <= kMaxShard, "shards per frame must be in [1, 8]");
+  const int S = nshard_;
   size_t total = 0, align_need = 0;
   for (int i = 0; i < nframes; ++i) {
     FrameJob& j = jobs[i];
     DQ_CHECK(j.n > 0, "num_points must be > 0 (DivQuantCluster.cpp:211)");
     DQ_CHECK(j.k > 0, "num_colors must be > 0 (DivQuantCluster.cpp:229)");
     DQ_CHECK(j.d_in && j.ct, "null buffer");
-    frames_[i].job = &j;
-    frames_[i].base = (uint32_t)total;
-    total += align4(j.n) + 4;
-    if (((uintptr_t)j.d_in & 15) != 0 || (j.n & 3) != 0) align_need += align4(j.n) + 4;
+    DQ_CHECK(j.nshard == S, "every frame of a batch must have the same shard count");
+    DQ_CHECK(j.n_global == 0 || j.n_global >= j.n, "n_global < n");
+    DQ_CHECK(j.n_global == 0 || j.n_global == j.n || comm_ != nullptr,
+             "n_global > n needs a communicator (dq_hip_comm_init)");
+    FrameState& f = frames_[i];
+    f.job = &j;
+    // shard boundaries: whole rows when the width is known, else 4-point multiples
+    for (int sh = 0; sh <= S; ++sh) {
+      uint64_t b;
+      if (j.width > 0 && j.n % j.width == 0) {
+        const uint64_t rows = j.n / j.width;
+        b = (rows * (uint64_t)sh / S) * j.width;
+      } else {
+        b = ((uint64_t)j.n * sh / S) & ~(uint64_t)3;
+      }
+      if (sh == S) b = j.n;
+      if (sh < S) f.first[sh] = (uint32_t)b;
+      if (sh > 0) f.n[sh - 1] = (uint32_t)b - f.first[sh - 1];
+    }
+    for (int sh = 0; sh < S; ++sh) {
+      f.base[sh] = (uint32_t)total;
+      total += align4(f.n[sh]) + 4;
+      const uint32_t* p = j.d_in + f.first[sh];
+      if (((uintptr_t)p & 15) != 0 || (f.n[sh] & 3) != 0) align_need += align4(f.n[sh]) + 4;
+    }
   }
   DQ_CHECK(total < (1ull << 32), "batch larger than 2^32 points");
   ensure_pixels(total);
@@ -618,19 +683,25 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   for (int i = 0; i < nframes; ++i) {
     FrameState& f = frames_[i];
     FrameJob& j = *f.job;
-    // get_double_scale (DivQuantMapColors.cpp:205-220)
-    f.s = 1.0 / (std::ceil(1 / 1.0) * std::ceil(j.n / 1.0));
-    f.in = j.d_in;
-    if (((uintptr_t)j.d_in & 15) != 0 || (j.n & 3) != 0) {   // 16-B loads may read up to align4(n)
-      DQ_HIP(hipMemcpyAsync(d_align_ + aoff, j.d_in, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
-      f.in = d_align_ + aoff;
-      aoff += align4(j.n) + 4;
-    }
+    const uint64_t ng = j.n_global ? j.n_global : j.n;
+    // get_double_scale (DivQuantMapColors.cpp:205-220), on the whole frame
+    f.s = 1.0 / (std::ceil(1 / 1.0) * std::ceil((double)ng / 1.0));
     Node root;
     root.frame = i;
     root.w = 1.0;          // :329
-    root.len = j.n;
+    root.glen = ng;
     root.buf = BUF_IN;
+    for (int sh = 0; sh < S; ++sh) {
+      const uint32_t* p = j.d_in + f.first[sh];
+      f.in[sh] = p;
+      if (((uintptr_t)p & 15) != 0 || (f.n[sh] & 3) != 0) {   // 16-B loads may read up to align4(n)
+        DQ_HIP(hipMemcpyAsync(d_align_ + aoff, p, (size_t)f.n[sh] * 4, hipMemcpyDeviceToDevice, stream));
+        f.in[sh] = d_align_ + aoff;
+        aoff += align4(f.n[sh]) + 4;
+      }
+      root.off[sh] = 0;
+      root.len[sh] = f.n[sh];
+    }
     f.leaf.assign(j.k, -1);
     f.leaf[0] = (int)nodes_.size();
     nodes_.push_back(root);
@@ -667,7 +738,9 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
       for (int i = 0; i < j.k_out; ++i)
         if (seen.insert(j.ct[i]).second) j.ct[m++] = j.ct[i];
       j.k_out = m;
-      if (j.d_out) mj.push_back(MapJob{f.in, j.n, j.d_out, j.ct, m});
+      if (j.d_out)   // every shard's rows with the frame's palette
+        for (int sh = 0; sh < S; ++sh)
+          if (f.n[sh] > 0) mj.push_back(MapJob{f.in[sh], f.n[sh], j.d_out + f.first[sh], j.ct, m});
     }
     if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream);
   }
@@ -677,11 +750,49 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   if (trace_) {
     const double t_end = host_us();
     std::fprintf(stderr,
-                 "divquant-hip trace: frames=%d rounds=%d cluster=%.1fus (build %.1f, wait %.1f, "
-                 "replay %.1f) map+sync=%.1fus total=%.1fus\n",
-                 nframes, last_rounds, t_clu - t_run0, tr_build_us_, tr_wait_us_, tr_replay_us_,
-                 t_end - t_clu, t_end - t_run0);
+                 "divquant-hip trace: frames=%d shards=%d rounds=%d cluster=%.1fus (build %.1f, "
+                 "wait %.1f, replay %.1f) map+sync=%.1fus total=%.1fus\n",
+                 nframes, S, last_rounds, t_clu - t_run0, tr_build_us_, tr_wait_us_,
+                 tr_replay_us_, t_end - t_clu, t_end - t_run0);
   }
+}
+
+// ---------------------------------------------------------------------------
+// RCCL communicator (row-tile sharding across processes, one GPU each).
+void Engine::comm_unique_id(char id[128]) {
+  ncclUniqueId u;
+  DQ_CHECK(ncclGetUniqueId(&u) == ncclSuccess, "ncclGetUniqueId failed");
+  std::memcpy(id, u.internal, 128);
+}
+
+void Engine::comm_init(int nranks, int rank, const char id[128]) {
+  DQ_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / world size");
+  DQ_HIP(hipSetDevice(device_));
+  comm_destroy();
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, 128);
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&c, nranks, u, rank);
+  if (r != ncclSuccess) die("ncclCommInitRank", __FILE__, __LINE__, ncclGetErrorString(r));
+  comm_ = c;
+  comm_ranks_ = nranks;
+  comm_rank_ = rank;
+}
+
+void Engine::comm_destroy() {
+  if (!comm_) return;
+  ncclCommDestroy((ncclComm_t)comm_);
+  comm_ = nullptr;
+  comm_ranks_ = 1;
+  comm_rank_ = 0;
+}
+
+// The per-pass exchange of row-tile sharding: the logical nodes' 8 u64
+// totals summed over all processes, in place, on the round's stream.
+void Engine::allreduce_totals(int nlogical, hipStream_t stream) {
+  const ncclResult_t r = ncclAllReduce(d_tot_, d_tot_, (size_t)nlogical * 8, ncclUint64, ncclSum,
+                                       (ncclComm_t)comm_, stream);
+  if (r != ncclSuccess) die("ncclAllReduce", __FILE__, __LINE__, ncclGetErrorString(r));
 }
 
 // ---------------------------------------------------------------------------

@@ -35,7 +35,12 @@ namespace dq {
     if (!(cond)) ::dq::die(#cond, __FILE__, __LINE__, msg);               \
   } while (0)
 
+// Row-range shards a frame may be split into inside ONE process (virtual
+// shards on one GPU: the exact arithmetic of multi-GPU row sharding).
+constexpr int kMaxShard = 8;
+
 // A node of a frame's split tree: one cluster as it exists between splits.
+// Its points are spread over the frame's shards: one local segment per shard.
 struct Node {
   int frame = 0;
   int child_old = -1, child_new = -1;
@@ -45,23 +50,28 @@ struct Node {
   double mean[3] = {0, 0, 0};        // mean[]     (:309)
   double var[3] = {0, 0, 0};         // var[]      (:314)
   double tse = 0.0;                  // tse[]      (:304)
-  uint32_t off = 0, len = 0;         // segment (len == size[] of the cluster)
+  uint64_t glen = 0;                 // size[] of the cluster (all shards, all processes)
+  uint32_t off[kMaxShard] = {}, len[kMaxShard] = {};   // local segment per shard
   int parent = -1;
-  // the round the node was split in: its record and tiles stay on the device
+  // the round the node was split in: its records and tiles stay on the device
   // so that a later round can partition it (fused with its children's split)
-  const DevNode* dnode = nullptr;
-  const Tile* dtiles = nullptr;
-  int ntiles = 0;
+  const DevNode* dnode[kMaxShard] = {};
+  const Tile* dtiles[kMaxShard] = {};
+  int ntiles[kMaxShard] = {};
   bool partitioned = false;          // children's points written to child_buf(buf)
 };
 
 // One quant_recurse / DivQuantCluster input.
 struct FrameJob {
-  const uint32_t* d_in = nullptr;    // device, n points
+  const uint32_t* d_in = nullptr;    // device, n points (this process's rows)
   uint32_t n = 0;
   uint32_t* d_out = nullptr;         // device, mapped colours (nullptr: cluster only)
   int k = 0;                         // requested clusters
   uint32_t* ct = nullptr;            // host, >= k entries
+  // row-tile sharding
+  int nshard = 1;                    // row ranges of d_in processed as separate shards
+  uint32_t width = 0;                // row length: shard boundaries on whole rows (0: any)
+  uint64_t n_global = 0;             // points of the whole frame over all processes (0: n)
   // outputs
   int k_out = 0;                     // colours written to ct
   int num_empty = 0;                 // empty clusters (:1067-1069)
@@ -106,6 +116,14 @@ class Engine {
   uint32_t* staged_out() { return d_stage_out_; }
 
   hipStream_t stream() const { return stream_; }
+
+  // Row-tile sharding across processes (one GPU each): an RCCL communicator
+  // over which every pass's node totals are allreduced.
+  static void comm_unique_id(char id[128]);
+  void comm_init(int nranks, int rank, const char id[128]);
+  void comm_destroy();
+  int comm_ranks() const { return comm_ranks_; }
+  void allreduce_totals(int nlogical, hipStream_t stream);
   int device() const { return device_; }
   std::mutex& mutex() { return mu_; }
 
@@ -129,8 +147,12 @@ class Engine {
   struct FrameState {
     FrameJob* job = nullptr;
     double s = 0.0;                   // get_double_scale
-    uint32_t base = 0;                // frame offset in P0/P1 (16-B aligned)
-    const uint32_t* in = nullptr;     // 16-B aligned input (maybe a staged copy)
+    // per shard: offset in P0/P1 (16-B aligned), 16-B aligned input (maybe a
+    // staged copy), points, and offset of the shard's rows in the frame
+    uint32_t base[kMaxShard] = {};
+    const uint32_t* in[kMaxShard] = {};
+    uint32_t n[kMaxShard] = {};
+    uint32_t first[kMaxShard] = {};
     std::vector<int> leaf;            // cluster index -> node id
     std::priority_queue<std::pair<std::pair<double, int>, int>> heap;  // ((tse,-idx), node)
     int new_index = 1, old_index = 0;
@@ -148,7 +170,7 @@ class Engine {
   void replay(FrameState& f);
   void next_active(FrameState& f, std::vector<int>* active);
   void finish_frame(FrameState& f, bool last);
-  const uint32_t* buf_ptr(int buf, const FrameState& f) const;
+  const uint32_t* buf_ptr(int buf, const FrameState& f, int shard) const;
   void timed_begin(hipStream_t stream);
   void timed_end(int kind, double bytes, hipStream_t stream);
   void collect_timing();
@@ -206,6 +228,11 @@ class Engine {
   void ensure_map_stage(size_t nmaps);
 
   std::vector<Node> nodes_;
+  int nshard_ = 1;                    // shard records per logical node in this run
+  uint64_t* d_tot_ = nullptr;         // sharded rounds: per logical node totals
+  size_t cap_tot_ = 0;
+  void* comm_ = nullptr;              // ncclComm_t across processes (row-tile sharding)
+  int comm_ranks_ = 1, comm_rank_ = 0;
   std::vector<int> slot_of_, parent_pos_;   // run_round scratch, indexed by node id
   std::vector<FrameState> frames_;
   struct PendingEvent { hipEvent_t a, b; int kind; double bytes; };

@@ -37,14 +37,23 @@ struct RoundArgs {
   uint64_t seq;             // round sequence number (tags the status words)
   int32_t fixed_point;      // epilogues finalise nodes at a 2-means fixed point
   int32_t it;               // 2-means iteration of an epilogue launch
-  int32_t nn;               // nodes in the round
+  int32_t nn;               // node records in the round (logical nodes x shards)
+  // sharded rounds (a frame split into row ranges, one record per shard):
+  uint64_t* tot;            // per logical node: 8 u64 totals (nodesum, then allreduce)
+  int32_t nshard;           // records per logical node (record r = node * nshard + shard)
+  int32_t pad;
 };
 
 // One statistics pass over tiles [0, ntiles) of the round (one workgroup per tile).
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
-// The FP64 update after a pass, one workgroup per node: sums the node's tile
-// partials and publishes the next pass's decision (or the split's results).
-void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream);
+// The FP64 update after a pass, one workgroup per node record: sums the
+// node's tile partials (from_totals: reads the node's global totals instead)
+// and publishes the next pass's decision (or the split's results).
+void launch_epilogue(int kind, const RoundArgs& a, int nnodes, bool from_totals,
+                     hipStream_t stream);
+// Sharded rounds: per logical node, the sums of the pass over all its shard
+// records' tiles into a.tot (to be allreduced across processes).
+void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stream);
 // Fused partition + split pass over the round's PartTiles: writes each
 // parent's points into its two children's segments (old half first, then new
 // half) of the child buffer, using the parent's final 2-means decision, and

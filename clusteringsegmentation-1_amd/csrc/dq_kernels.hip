@@ -365,18 +365,106 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Epilogue: one workgroup per node of the round.
-//   * sums the node's tile partials in u64 (PASS_SPLIT of a node whose
-//     parent was partitioned this round: its half of the parent's fused
-//     partition+split partials instead);
-//   * thread 0 runs the FP64 update (node_update);
-//   * a node whose split became final: each tile's first OLD point's rank
-//     among the node's old points (the partition's write cursors), and the
-//     results written straight to host memory (NodeResult);
-//   * 2-means launches: every workgroup arrives on the launch's counter; the
-//     last to arrive publishes (round seq, nodes still active) to the host,
-//     which stops launching iterations once no node is active.
+// This lane's share of the sums of one node record's pass: its tile partials
+// in u64 (PASS_SPLIT of a record whose parent was partitioned this round: its
+// half of the parent's fused partition+split partials instead).
 template <int KIND>
+__device__ __forceinline__ void sum_record(const RoundArgs& a, const DevNode* w, uint64_t acc[7]) {
+  if (KIND == PASS_SPLIT && w->split_pb >= 0) {
+    // children's (cnt, sums) of the fused pass: [0..3] old half, [4..7] new half
+    const g_cu4* sp4 = (const g_cu4*)a.sparts;
+    const int side = w->split_side;
+    for (int i = w->split_pb + (int)threadIdx.x; i < w->split_pe; i += kBlock) {
+      const u32x4 x = sp4[2 * i + side];
+      acc[0] += x[0];
+      acc[1] += x[1];
+      acc[2] += x[2];
+      acc[3] += x[3];
+    }
+    return;
+  }
+  const int tb = w->tile_begin, te = w->tile_end;
+  const g_cu4* parts4 = (const g_cu4*)a.parts;
+  constexpr bool kSquares = KIND != PASS_SPLIT;
+  for (int base = tb; base < te; base += 4 * kBlock) {
+    u32x4 x[4], y[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {   // issue every load of the chunk first
+      const int i = base + u * kBlock + (int)threadIdx.x;
+      if (i < te) {
+        x[u] = parts4[2 * i];
+        if (kSquares) y[u] = parts4[2 * i + 1];
+      } else {
+        x[u] = (u32x4){0u, 0u, 0u, 0u};
+        y[u] = (u32x4){0u, 0u, 0u, 0u};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc[0] += x[u][0];
+      acc[1] += x[u][1];
+      acc[2] += x[u][2];
+      acc[3] += x[u][3];
+      if (kSquares) {
+        acc[4] += y[u][0];
+        acc[5] += y[u][1];
+        acc[6] += y[u][2];
+      }
+    }
+  }
+}
+
+// Workgroup sum of the lanes' acc[] into tot[] (valid in thread 0).
+__device__ __forceinline__ void block_sum7(uint64_t acc[7], uint64_t (*red)[8], uint64_t tot[7]) {
+#pragma unroll
+  for (int k = 0; k < F_NUM; ++k) acc[k] = wave_sum_u64(acc[k]);
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < F_NUM; ++k) red[wave_id()][k] = acc[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < F_NUM; ++k) {
+      tot[k] = 0;
+      for (int v = 0; v < kBlock / 64; ++v) tot[k] += red[v][k];
+    }
+  }
+}
+
+// Sharded rounds: one workgroup per LOGICAL node sums the pass over all its
+// shard records into a.tot (8 u64; the host then allreduces a.tot across
+// processes with RCCL -- integer sums, so exact in any order).
+template <int KIND>
+__global__ __launch_bounds__(kBlock) void nodesum_kernel(RoundArgs a) {
+  constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
+  __shared__ uint64_t red[kBlock / 64][8];
+  const DevNode* w0 = a.nodes + (size_t)blockIdx.x * a.nshard;
+  uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (!(kMeans && w0->done_it != 0))   // (all records of a node agree on done_it)
+    for (int sh = 0; sh < a.nshard; ++sh) sum_record<KIND>(a, w0 + sh, acc);
+  uint64_t tot[7];
+  block_sum7(acc, red, tot);   // (valid in thread 0)
+  if (threadIdx.x == 0) {
+    uint64_t* g = a.tot + (size_t)blockIdx.x * 8;
+    for (int k = 0; k < F_NUM; ++k) g[k] = tot[k];
+    g[7] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Epilogue: one workgroup per node record of the round.
+//   * the node's sums: its own partials (FROM_TOT: the logical node's global
+//     totals from nodesum + allreduce; its own partials then only give the
+//     record's local new-half size);
+//   * thread 0 runs the FP64 update (node_update) -- every record of a
+//     logical node runs it on the same totals, so all agree bit for bit;
+//   * a record whose split became final: the partition's per-(tile, wave)
+//     write cursors, and the results written straight to host memory
+//     (NodeResult);
+//   * 2-means launches: every workgroup arrives on the launch's counter; the
+//     last to arrive publishes (round seq, records still active) to the host,
+//     which stops launching iterations once no node is active.
+template <int KIND, bool FROM_TOT>
 __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
   constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
   DevNode* w = a.nodes + blockIdx.x;
@@ -387,64 +475,21 @@ __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
   if (threadIdx.x == 0) final_results = 0;
   if (!skip) {
     const int tb = w->tile_begin, te = w->tile_end;
-    const g_cu4* parts4 = (const g_cu4*)a.parts;
     uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    if (KIND == PASS_SPLIT && w->split_pb >= 0) {
-      // children's (cnt, sums) of the fused pass: [0..3] old half, [4..7] new half
-      const g_cu4* sp4 = (const g_cu4*)a.sparts;
-      const int side = w->split_side;
-      for (int i = w->split_pb + (int)threadIdx.x; i < w->split_pe; i += kBlock) {
-        const u32x4 x = sp4[2 * i + side];
-        acc[0] += x[0];
-        acc[1] += x[1];
-        acc[2] += x[2];
-        acc[3] += x[3];
-      }
-    } else {
-      constexpr bool kSquares = KIND != PASS_SPLIT;
-      for (int base = tb; base < te; base += 4 * kBlock) {
-        u32x4 x[4], y[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {   // issue every load of the chunk first
-          const int i = base + u * kBlock + (int)threadIdx.x;
-          if (i < te) {
-            x[u] = parts4[2 * i];
-            if (kSquares) y[u] = parts4[2 * i + 1];
-          } else {
-            x[u] = (u32x4){0u, 0u, 0u, 0u};
-            y[u] = (u32x4){0u, 0u, 0u, 0u};
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          acc[0] += x[u][0];
-          acc[1] += x[u][1];
-          acc[2] += x[u][2];
-          acc[3] += x[u][3];
-          if (kSquares) {
-            acc[4] += y[u][0];
-            acc[5] += y[u][1];
-            acc[6] += y[u][2];
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < F_NUM; ++k) acc[k] = wave_sum_u64(acc[k]);
-    if (lane_id() == 0) {
-#pragma unroll
-      for (int k = 0; k < F_NUM; ++k) red[wave_id()][k] = acc[k];
-    }
-    __syncthreads();   // (every thread has read done_it above)
+    sum_record<KIND>(a, w, acc);
+    uint64_t tot[7];
+    block_sum7(acc, red, tot);   // (every thread has read done_it above)
     if (threadIdx.x == 0) {
-      uint64_t tot[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
-      for (int k = 0; k < F_NUM; ++k)
-        for (int v = 0; v < kBlock / 64; ++v) tot[k] += red[v][k];
+      const uint32_t local_new = (uint32_t)tot[F_CNT];
+      if (FROM_TOT) {
+        const uint64_t* g = a.tot + (size_t)(blockIdx.x / a.nshard) * 8;
+        for (int k = 0; k < F_NUM; ++k) tot[k] = g[k];
+      }
       const bool fin = node_update<KIND>(w, &sres, tot, a.fixed_point != 0);
       if (fin) {
         for (int c = 0; c < 3; ++c) { sres.tm[c] = w->tm[c]; sres.tv[c] = w->tv[c]; }
-        w->n_new_local = (uint32_t)tot[F_CNT];   // single shard: local == global
-        sres.n_new_local = (uint32_t)tot[F_CNT];
+        w->n_new_local = local_new;
+        sres.n_new_local = local_new;
         sres.done_it = w->done_it;
       }
       final_results = fin ? 1 : 0;
@@ -878,14 +923,35 @@ void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) {
   }
 }
 
-void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream) {
+void launch_epilogue(int kind, const RoundArgs& a, int nnodes, bool from_totals,
+                     hipStream_t stream) {
   if (nnodes <= 0) return;
   const dim3 g(nnodes), b(kBlock);
+  if (from_totals) {
+    switch (kind) {
+      case PASS_INIT: epilogue_kernel<PASS_INIT, true><<<g, b, 0, stream>>>(a); break;
+      case PASS_SPLIT: epilogue_kernel<PASS_SPLIT, true><<<g, b, 0, stream>>>(a); break;
+      case PASS_KMEANS: epilogue_kernel<PASS_KMEANS, true><<<g, b, 0, stream>>>(a); break;
+      default: epilogue_kernel<PASS_KLAST, true><<<g, b, 0, stream>>>(a); break;
+    }
+    return;
+  }
   switch (kind) {
-    case PASS_INIT: epilogue_kernel<PASS_INIT><<<g, b, 0, stream>>>(a); break;
-    case PASS_SPLIT: epilogue_kernel<PASS_SPLIT><<<g, b, 0, stream>>>(a); break;
-    case PASS_KMEANS: epilogue_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a); break;
-    default: epilogue_kernel<PASS_KLAST><<<g, b, 0, stream>>>(a); break;
+    case PASS_INIT: epilogue_kernel<PASS_INIT, false><<<g, b, 0, stream>>>(a); break;
+    case PASS_SPLIT: epilogue_kernel<PASS_SPLIT, false><<<g, b, 0, stream>>>(a); break;
+    case PASS_KMEANS: epilogue_kernel<PASS_KMEANS, false><<<g, b, 0, stream>>>(a); break;
+    default: epilogue_kernel<PASS_KLAST, false><<<g, b, 0, stream>>>(a); break;
+  }
+}
+
+void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stream) {
+  if (nlogical <= 0) return;
+  const dim3 g(nlogical), b(kBlock);
+  switch (kind) {
+    case PASS_INIT: nodesum_kernel<PASS_INIT><<<g, b, 0, stream>>>(a); break;
+    case PASS_SPLIT: nodesum_kernel<PASS_SPLIT><<<g, b, 0, stream>>>(a); break;
+    case PASS_KMEANS: nodesum_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a); break;
+    default: nodesum_kernel<PASS_KLAST><<<g, b, 0, stream>>>(a); break;
   }
 }
 

@@ -51,6 +51,27 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t *const *d_in,
                            const uint32_t *n, uint32_t *const *d_out, uint32_t k,
                            uint32_t *ct, uint32_t *k_out, int max_iters,
                            void *stream);
+/* Row-tile sharding.  Frame i's rows are d_in[i] (n[i] points,
+ * width[i] per row; width NULL or 0: shard boundaries on 4-point multiples).
+ * Inside this process the rows are split into nshard (1..8) row ranges that
+ * are processed as separate shards on `device` (the exact arithmetic of
+ * multi-GPU sharding); across processes, n_global[i] (NULL or 0: n[i]) is the
+ * whole frame's size and every pass's integer node totals are allreduced
+ * over the communicator of dq_hip_comm_init (RCCL over xGMI).  Every
+ * process gets the same colortables; d_out[i] receives this process's rows
+ * mapped (d_out NULL: clustering only).  Returns empty clusters, -1 on bad
+ * arguments, -2 if n_global > n without a communicator. */
+int dq_hip_quant_rows_dev(int device, int nframes, const uint32_t *const *d_in,
+                          const uint32_t *n, const uint32_t *width,
+                          const uint64_t *n_global, int nshard,
+                          uint32_t *const *d_out, uint32_t k, uint32_t *ct,
+                          uint32_t *k_out, int max_iters, void *stream);
+/* RCCL communicator of the engine on `device` (one process per GPU): rank 0
+ * creates the 128-byte id, the launcher broadcasts it (e.g. with
+ * torch.distributed), every rank calls dq_hip_comm_init.  Return 0 / < 0. */
+int dq_hip_comm_unique_id(void *id128);
+int dq_hip_comm_init(int device, int nranks, int rank, const void *id128);
+int dq_hip_comm_destroy(int device);
 /* Clustering only (quant_varpart_fast, DivQuantCluster.cpp:1099-1179):
  * writes the non-empty cluster colours (cluster-index order, NOT deduped). */
 int dq_hip_cluster_dev(int device, const uint32_t *d_in, uint32_t n,
