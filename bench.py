@@ -1,20 +1,33 @@
 #!/usr/bin/env python3
 """bench.py -- DivQuant hot path (quant_recurse: cluster + dedup + map) on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--frames F]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+                    [--mode frames|rows] [--frames F]
 
-One step = quant_recurse semantics (K=256, max_iters=10) on every frame this
-rank owns (F synthetic uniform-random 24-bit RGB frames of the config's shape,
-already resident in HBM).  N>1 (launched by torch.distributed.run, one rank per
-GPU): frames are independent objects, so each rank owns its own F frames and
-there is no data-path collective ("scaling": "weak"); the barrier and the
-max-over-ranks timing use the process group only.
+Workload (BASELINE.json metric "Mpixels/sec DivQuant K=256 on 4K RGB"):
 
-Prints ONE JSON line on rank 0.  `roofline` is measured live on the library's
-stream with HIP events around every launch of the dominant kernel (the 2-means
-statistics pass); `cpu_baseline` times the reference DivQuant (oracle/_ref,
-built from the unmodified reference sources) or, if that build is absent, the
-oracle's restatement, on one frame, on one host core, rank 0 only.
+* --mode frames (default): one step = quant_recurse (K=256, max_iters=10,
+  cluster + colortable dedup + map) on each of the F synthetic uniform-random
+  24-bit 3840x2160 frames this rank owns, already resident in HBM, in ONE
+  batched call (every pass of a split round is one launch over all F frames).
+  Default F = 8: C4's per-GPU share (C4 = 64 4K frames over 8 GPUs, so
+  --gpus 8 is exactly C4).  Frames are independent objects: no data-path
+  collective, "scaling": "weak".  The single-frame latency of C3 (one 4K
+  frame per call) is measured in the same run and reported in detail.c3.
+* --mode rows: ONE frame of the config (e.g. --config c5: the 16384x16384
+  K=1024 gigapixel tile) row-tile sharded over the N ranks; every pass's
+  integer node totals are allreduced with RCCL over xGMI ("scaling":
+  "strong": the total work is fixed).
+
+N>1 is launched by torch.distributed.run, one rank per GPU.  Prints ONE JSON
+line on rank 0.  `roofline` is the kernel with the largest measured time in
+the step, timed live on the library's stream with HIP events around every
+launch, against the 8 TB/s HBM peak; `traffic` comes from the committed
+rocprofv3 PMC counters of the same command (profiles/pmc_traffic.json, see
+tools/pmc_bench.sh) when they exist.  `cpu_baseline` times the reference
+DivQuant (oracle/_ref, built from the unmodified reference sources) -- or,
+if that build is absent, the oracle's restatement -- on one 4K frame, one
+host core, rank 0 at N=1 only.
 """
 import argparse
 import ctypes
@@ -28,13 +41,19 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-CONFIGS = {   # BASELINE.json configs (C4/C5 are multi-GPU shapes)
+CONFIGS = {   # BASELINE.json configs (C4 = 64 x c3 frames; C5 = c5 row-sharded)
     "c1": (256, 256, 16),
     "c2": (1920, 1080, 256),
     "c3": (3840, 2160, 256),
     "c5": (16384, 16384, 1024),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# algorithmic bytes of the kernel kinds the roofline may name (bytes per point
+# the engine attributes to each launch: 4 read, +4 written for the partition)
+ROOF_KERNELS = {"pass_kmeans": "pass_kernel<PASS_KMEANS>", "partition": "partsplit_kernel",
+                "pass_split": "pass_kernel<PASS_SPLIT>", "pass_init": "pass_kernel<PASS_INIT>",
+                "map": "map_kernel"}
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
 def parse():
@@ -43,9 +62,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--frames", type=int, default=1, help="frames per rank per step")
+    ap.add_argument("--mode", default="frames", choices=["frames", "rows"])
+    ap.add_argument("--frames", type=int, default=8, help="frames per rank per step (frames mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline region")
+    ap.add_argument("--no-c3", action="store_true", help="skip the single-frame C3 measurement")
     return ap.parse_args()
 
 
@@ -105,6 +126,11 @@ def frame_seed(rank, frame):
     return 0x5EED + 1000 * rank + frame
 
 
+def row_range(h, rank, world):
+    """Row-tile sharding: rank r owns rows [r*H/N, (r+1)*H/N)."""
+    return h * rank // world, h * (rank + 1) // world
+
+
 def timed_region(step, steps, world, sync):
     """Barrier + device sync on both sides of exactly `steps` steps."""
     import torch.distributed as dist
@@ -130,6 +156,31 @@ def max_over_ranks(dt, world, device="cpu"):
     return float(t.item())
 
 
+def pick_roofline(stats, pmc_key):
+    """The roofline object of the kernel kind with the largest measured time."""
+    cand = {k: v for k, v in stats.items() if k in ROOF_KERNELS and v[0] > 0 and v[1] > 0 and v[2] > 0}
+    if not cand:
+        return None
+    kind = max(cand, key=lambda k: cand[k][1])
+    launches, ms, alg = cand[kind]
+    gbs = alg / (ms / 1e3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": ROOF_KERNELS[kind], "launches": launches,
+            "avg_launch_us": round(ms * 1e3 / launches, 2),
+            "alg_bytes_per_launch": round(alg / launches),
+            "share_of_step_kernel_time": round(ms / sum(v[1] for v in stats.values() if v[1] > 0), 3)}
+    if os.path.exists(PMC_FILE):
+        try:
+            pmc = json.load(open(PMC_FILE)).get(pmc_key, {}).get(ROOF_KERNELS[kind])
+        except ValueError:
+            pmc = None
+        if pmc:
+            roof["traffic"] = round(pmc["hbm_bytes_per_launch"])
+            roof["traffic_source"] = pmc["source"]
+    return roof
+
+
 def main():
     a = parse()
     import torch
@@ -139,22 +190,55 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pkg = load_package()
+    stream = torch.cuda.current_stream(dev)
 
     w, h, k = CONFIGS[a.config]
     n = w * h
-    frames = []
-    for f in range(a.frames):
-        g = torch.Generator(device=dev)
-        g.manual_seed(frame_seed(rank, f))
-        frames.append(torch.randint(0, 1 << 24, (n,), dtype=torch.int32, device=dev, generator=g))
-    outs = [torch.empty_like(f) for f in frames]
-    stream = torch.cuda.current_stream(dev)
+    if a.mode == "frames":
+        nf = a.frames
+        frames = []
+        for f in range(nf):
+            g = torch.Generator(device=dev)
+            g.manual_seed(frame_seed(rank, f))
+            frames.append(torch.randint(0, 1 << 24, (n,), dtype=torch.int32, device=dev, generator=g))
+        outs = [torch.empty_like(f) for f in frames]
 
-    def step():
-        if a.frames == 1:
-            pkg.quant_device(frames[0], outs[0], k, max_iters=10, device=local, stream=stream)
-        else:   # one batched call: every pass of a round covers all frames
-            pkg.quant_batch_device(frames, outs, k, max_iters=10, device=local, stream=stream)
+        def step():   # one batched call: every pass of a round covers all frames
+            if nf == 1:
+                pkg.quant_device(frames[0], outs[0], k, max_iters=10, device=local, stream=stream)
+            else:
+                pkg.quant_batch_device(frames, outs, k, max_iters=10, device=local, stream=stream)
+        px_per_step = n * nf * world
+        workload = ("C4 per-GPU share: %d x %dx%d frames per rank per step, K=%d, quant_recurse "
+                    "max_iters=10 (cluster + dedup + map), one batched call" % (nf, w, h, k)
+                    if nf > 1 else "C3: one %dx%d frame per step, K=%d, quant_recurse" % (w, h, k))
+        parallelism = "frames-per-rank x%d" % world
+        scaling = "weak"
+    else:
+        if world > 1:
+            pkg.comm_init_torch(device=local)
+        r0, r1 = row_range(h, rank, world)
+        g = torch.Generator(device=dev)
+        g.manual_seed(frame_seed(0, 0))   # the same frame on every rank; each keeps its rows
+        mine = torch.empty(((r1 - r0) * w,), dtype=torch.int32, device=dev)
+        # generate the frame row-block by row-block (no full copy needed on any rank)
+        for rb in range(0, h, 1024):
+            blk = torch.randint(0, 1 << 24, (min(1024, h - rb) * w,), dtype=torch.int32, device=dev,
+                                generator=g)
+            lo, hi = max(rb, r0), min(rb + 1024, r1)
+            if lo < hi:
+                mine[(lo - r0) * w:(hi - r0) * w] = blk[(lo - rb) * w:(hi - rb) * w]
+        out = torch.empty_like(mine)
+
+        def step():
+            pkg.quant_rows_device([mine], [out], k, widths=[w], n_globals=[n], nshard=1,
+                                  max_iters=10, device=local, stream=stream)
+        nf = 1
+        px_per_step = n
+        workload = ("%s: one %dx%d frame, K=%d, row-tile sharded over %d rank(s), RCCL allreduce "
+                    "of the node totals per pass" % (a.config.upper(), w, h, k, world))
+        parallelism = "row-tiles x%d" % world
+        scaling = "strong"
 
     for _ in range(a.warmup):
         step()
@@ -163,9 +247,8 @@ def main():
     dt = timed_region(step, a.steps, world, lambda: torch.cuda.synchronize(dev))
     # --- roofline region: the same steps again with HIP events around every
     # launch (on the library's launch stream) for per-kernel durations
-    timing = not a.no_timing
     stats = {}
-    if timing:
+    if not a.no_timing:
         pkg.reset_stats(device=local)
         pkg.set_timing(True, device=local)
         for _ in range(a.steps):
@@ -175,23 +258,31 @@ def main():
         stats = pkg.get_stats(device=local)
     rounds = pkg.last_rounds(device=local)
     swept = pkg.last_points_swept(device=local)
+    full = pkg.last_points_full(device=local)
+
+    # --- C3 single-frame latency (same frame shape, one frame per call)
+    c3 = None
+    if a.mode == "frames" and not a.no_c3 and nf > 1:
+        def one():
+            pkg.quant_device(frames[0], outs[0], k, max_iters=10, device=local, stream=stream)
+        for _ in range(2):
+            one()
+        dt1 = timed_region(one, a.steps, world, lambda: torch.cuda.synchronize(dev))
+        dt1 = max_over_ranks(dt1, world, dev)
+        c3 = {"ms_per_frame": round(dt1 * 1e3 / a.steps, 3),
+              "Mpix_per_s": round(n * world * a.steps / dt1 / 1e6, 2),
+              "workload": "one %dx%d frame per call (C3), %d rank(s)" % (w, h, world)}
 
     dt = max_over_ranks(dt, world, dev)
-    total_px = n * a.frames * a.steps * world
-    value = total_px / dt / 1e6
+    value = px_per_step * a.steps / dt / 1e6
 
     if rank == 0:
-        km = stats.get("pass_kmeans", (0, 0.0, 0.0))
-        roof = None
-        if timing and km[0] > 0 and km[1] > 0:
-            gbs = km[2] / (km[1] / 1e3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "pass_kernel<PASS_KMEANS>",
-                    "launches": km[0], "avg_launch_us": round(km[1] * 1e3 / km[0], 2),
-                    "alg_bytes_per_launch": round(km[2] / km[0])}
-        # whole-pipeline algorithmic bytes (BASELINE.md B_alg = 4N + 44*sum|C_j| + 8N)
-        per_frame_ms = dt * 1e3 / (a.steps * a.frames)
+        pmc_key = "%s_%s_f%d_n%d" % (a.mode, a.config, nf, world)
+        roof = pick_roofline(stats, pmc_key) if stats else None
+        # whole-pipeline algorithmic bytes (B_alg = 4N + 44*sum|C_j| + 8N;
+        # sum|C_j| = log2(K) N for uniform inputs)
+        lk = int(round(np.log2(k)))
+        b_alg = (4 + 44 * lk + 8) * px_per_step * a.steps
         res = {
             "metric": "Mpixels/sec DivQuant K=%d on %dx%d RGB" % (k, w, h),
             "value": round(value, 2),
@@ -201,24 +292,30 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(dt * 1e3 / a.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "u8x3 pixels, u64 sums, f64 epilogue",
+            "dtype": "u8x3 pixels in u32, u32/u64 integer sums, f64 updates",
             "data": "synthetic uniform-random 24-bit RGB frames (torch.randint on device)",
-            "config": {"workload": "quant_recurse %dx%d K=%d max_iters=10 (cluster+dedup+map)" % (w, h, k),
-                       "frames_per_rank_per_step": a.frames, "parallelism": "frames-per-rank x%d" % world},
+            "config": {"workload": workload, "frames_per_rank_per_step": nf if a.mode == "frames" else None,
+                       "width": w, "height": h, "k": k, "max_iters": 10, "parallelism": parallelism},
             "roofline": roof,
-            "detail": {"ms_per_frame": round(per_frame_ms, 3), "rounds_last_frame": rounds,
-                       "points_swept_last_frame": swept,
+            "detail": {"ms_per_frame": round(dt * 1e3 / a.steps / (nf * world if a.mode == "frames" else 1), 3),
+                       "pipeline_alg_GBps": round(b_alg / dt / 1e9, 1),
+                       "pipeline_alg_frac_per_gpu": round(b_alg / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
+                       "rounds_last_frame": rounds, "points_swept_last_call": swept,
+                       "points_full_iterations_last_call": full,
+                       "c3": c3,
                        "kernels": {kname: {"launches": v[0], "ms": round(v[1], 3),
                                            "GBps": round(v[2] / (v[1] / 1e3) / 1e9, 1) if v[1] > 0 and v[2] > 0 else None}
                                    for kname, v in stats.items() if v[0]}},
         }
         if world == 1 and not a.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(w, h, k)
+            res["cpu_baseline"] = cpu_baseline(3840, 2160, 256)
         print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist
+        if a.mode == "rows":
+            pkg.comm_destroy(device=local)
         dist.destroy_process_group()
 
 

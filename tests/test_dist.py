@@ -58,3 +58,17 @@ def test_two_rank_harness(tmp_path):
     assert outs[0]["dtmax"] >= max(o["dt"] for o in outs) - 1e-9
     # disjoint frames per rank
     assert not set(outs[0]["seeds"]) & set(outs[1]["seeds"])
+
+
+def test_row_ranges_partition_the_frame():
+    """Row-tile sharding (bench --mode rows): rank r owns rows [r*H/N, (r+1)*H/N)
+    -- disjoint, ordered, covering every row, balanced to one row."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for h in (1, 7, 2160, 16384):
+        for world in range(1, 9):
+            rr = [bench.row_range(h, r, world) for r in range(world)]
+            assert rr[0][0] == 0 and rr[-1][1] == h
+            assert all(rr[i][1] == rr[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in rr]
+            assert max(sizes) - min(sizes) <= 1
