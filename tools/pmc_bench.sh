@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-pmc}; shift || true
 O=$R/gpurun_out/$TAG
 mkdir -p $O
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-timing $*"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-timing --no-c3 $*"
 K="--kernel-include-regex (partsplit|pass_kernel|map_kernel|epilogue)"
 cd /tmp
 run() {   # name counters...
@@ -18,7 +18,7 @@ run() {   # name counters...
 }
 run fetch FETCH_SIZE
 run write WRITE_SIZE
-run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES
-run sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT
-run ta TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_HIT_sum TCC_MISS_sum
-echo pmc done
+[ -n "$PMC_FULL" ] && run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES
+[ -n "$PMC_FULL" ] && run sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT
+[ -n "$PMC_FULL" ] && run ta TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_HIT_sum TCC_MISS_sum
+true; echo pmc done
