@@ -13,8 +13,11 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
+#include <vector>
+#include <thread>
 #include <vector>
 
 #include "../../include/DivQuantHeader.h"
@@ -108,8 +111,6 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
     return -1;
   for (int i = 0; i < nframes; ++i)
     if (!d_in[i] || !d_out[i] || n[i] == 0) return -1;
-  Engine& e = engine_for(device);
-  std::lock_guard<std::mutex> g(e.mutex());
   std::vector<dq::FrameJob> jobs(nframes);
   for (int i = 0; i < nframes; ++i) {
     jobs[i].d_in = d_in[i];
@@ -118,7 +119,56 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
     jobs[i].k = (int)k;
     jobs[i].ct = ct + (size_t)i * k;
   }
-  e.run(jobs.data(), nframes, max_iters, true, (hipStream_t)stream);
+  const int lanes = std::min(nframes, dq::batch_lanes());
+  Engine& e0 = engine_for(device);
+  if (lanes <= 1) {
+    std::lock_guard<std::mutex> g(e0.mutex());
+    e0.run(jobs.data(), nframes, max_iters, true, (hipStream_t)stream);
+  } else {
+    // frames [f0(l), f0(l+1)) on lane l; every lane first waits for the
+    // caller's stream (the frames may have been produced there)
+    DQ_HIP(hipSetDevice(device));
+    hipEvent_t ready;
+    DQ_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    DQ_HIP(hipEventRecord(ready, (hipStream_t)stream));
+    std::vector<std::thread> th;
+    for (int l = lanes - 1; l >= 0; --l) {
+      const int f0 = nframes * l / lanes, f1 = nframes * (l + 1) / lanes;
+      Engine& e = engine_for(device, l);
+      if (l > 0) {   // lanes inherit lane 0's switches
+        e.set_fixed_point(e0.fixed_point());
+        e.set_timing(e0.timing());
+      }
+      auto work = [&e, &jobs, f0, f1, max_iters, ready, device]() {
+        DQ_HIP(hipSetDevice(device));
+        std::lock_guard<std::mutex> g(e.mutex());
+        DQ_HIP(hipStreamWaitEvent(e.stream(), ready, 0));
+        e.run(jobs.data() + f0, f1 - f0, max_iters, true, e.stream());
+      };
+      if (l > 0) th.emplace_back(work);
+      else work();
+    }
+    for (auto& t : th) t.join();
+    DQ_HIP(hipEventDestroy(ready));
+    // lane 0 reports for the batch: the last frame's diagnostics, summed counters
+    Engine& el = engine_for(device, lanes - 1);
+    std::lock_guard<std::mutex> g(e0.mutex());
+    uint64_t swept = 0, full = 0;
+    int rounds = 0;
+    for (int l = 0; l < lanes; ++l) {
+      Engine& e = engine_for(device, l);
+      swept += e.last_points_swept;
+      full += e.last_points_full;
+      rounds = std::max(rounds, e.last_rounds);
+      if (l > 0) e0.absorb_stats(e);
+    }
+    e0.last_means = el.last_means;
+    e0.last_sizes = el.last_sizes;
+    e0.last_trace = el.last_trace;
+    e0.last_rounds = rounds;
+    e0.last_points_swept = swept;
+    e0.last_points_full = full;
+  }
   int empty = 0;
   for (int i = 0; i < nframes; ++i) {
     k_out[i] = (uint32_t)jobs[i].k_out;

@@ -48,12 +48,13 @@ Engine::Engine(int device) : device_(device) {
   fixed_point_ = !(full && full[0] == '1');
   const char* tr = getenv("DQ_HIP_TRACE");
   trace_ = tr && tr[0] == '1';
+  if (const char* v = getenv("DQ_HIP_TILES")) tiles_target_ = std::max(64, atoi(v));
+  if (const char* v = getenv("DQ_HIP_TILE_MAX"))
+    tile_max_ = (uint32_t)std::max<int>(kSweep, std::min<int>((int)kMaxTilePx, atoi(v))) / kSweep * kSweep;
   const char* la = getenv("DQ_HIP_LOOKAHEAD");
   if (la && la[0]) lookahead_ = std::max(0, std::min(8, atoi(la)));
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  DQ_HIP(hipMalloc((void**)&d_cell_rec_, (size_t)kCells * kCellRecWords * sizeof(uint32_t)));
-  DQ_HIP(hipMalloc((void**)&d_cell_idx_, (size_t)kCells * kCellCap * sizeof(uint16_t)));
 }
 
 Engine::~Engine() {
@@ -285,11 +286,12 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     }
   for (int p : parents)
     for (int sh = 0; sh < S; ++sh) parent_total += nodes_[p].len[sh];
-  // Tile length: whole 4096-point sweeps, ~1024 tiles for big rounds (4 per
-  // CU: measured best for one 4K frame and for 8-frame batches, microbench).
-  uint64_t tl = (total + 1023) / 1024;
+  // Tile length: whole 4096-point sweeps, about tiles_target_ tiles for big
+  // rounds, at most tile_max_ points (a node still active late in a round is
+  // swept by ceil(len / tl) workgroups only).
+  uint64_t tl = (total + tiles_target_ - 1) / tiles_target_;
   tl = ((tl + kSweep - 1) / kSweep) * kSweep;
-  tl = std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, kMaxTilePx));
+  tl = std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, tile_max_));
   size_t ntiles = 0, nt_own = 0;
   for (int a = 0; a < nl; ++a) {   // empty records get one empty tile (their epilogue still runs)
     for (int sh = 0; sh < S; ++sh)
@@ -828,23 +830,27 @@ void sorted_palette(const uint32_t* ct, int k, uint32_t* pal_out, uint16_t* lut_
   for (int v = 0; v < 766; ++v) lut_out[v] = (uint16_t)lut[v];
 }
 
-// Per-map block of the map staging: [palette: kMapPal words | LUT: 768 u16]
+// Per-map block of the map staging: [palette: kMapPal words | LUT: 768 u16];
+// the staging starts with the MapTask table of the launch.
 constexpr size_t kMapPal = 16384;
 constexpr size_t kMapBlockWords = kMapPal + 768 / 2;
+constexpr int kMapChunk = 16;   // tasks per batched launch (cell tables: 2.5 MB each)
 }  // namespace
 
 void Engine::ensure_map_stage(size_t nmaps) {
   if (nmaps <= cap_mapstage_ && h_mapstage_) return;
   if (h_mapstage_) DQ_HIP(hipHostFree(h_mapstage_));
   if (d_mapstage_) DQ_HIP(hipFree(d_mapstage_));
-  DQ_HIP(hipHostMalloc((void**)&h_mapstage_, nmaps * kMapBlockWords * 4, hipHostMallocDefault));
-  DQ_HIP(hipMalloc((void**)&d_mapstage_, nmaps * kMapBlockWords * 4));
+  const size_t words = nmaps * (kMapBlockWords + sizeof(MapTask) / 4);
+  DQ_HIP(hipHostMalloc((void**)&h_mapstage_, words * 4, hipHostMallocDefault));
+  DQ_HIP(hipMalloc((void**)&d_mapstage_, words * 4));
   cap_mapstage_ = nmaps;
 }
 
 // map_colors_mps (DivQuantMapColors.cpp:243-539) for several (input, output,
-// colortable) triples: host palettes for all of them, ONE upload, then per
-// map the cell build and the map kernel, ONE synchronisation at the end.
+// colortable) triples: host palettes for all of them, ONE upload, then ONE
+// cell-build launch and ONE map launch per chunk of up to kMapChunk tasks,
+// ONE synchronisation at the end.
 void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
   DQ_HIP(hipSetDevice(device_));
   if (!stream) stream = stream_;
@@ -854,40 +860,102 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
   }
   // the staging is reused: the previous map's upload must have been consumed
   DQ_HIP(hipStreamSynchronize(stream));
-  ensure_map_stage(njobs);
-  for (int i = 0; i < njobs; ++i) {
-    uint32_t* blk = h_mapstage_ + i * kMapBlockWords;
-    sorted_palette(jobs[i].ct, jobs[i].k, blk, reinterpret_cast<uint16_t*>(blk + kMapPal));
+  const int chunk = std::min(njobs, kMapChunk);
+  ensure_map_stage(chunk);
+  if ((size_t)chunk > cap_cells_) {
+    if (d_cell_rec_) DQ_HIP(hipFree(d_cell_rec_));
+    if (d_cell_idx_) DQ_HIP(hipFree(d_cell_idx_));
+    DQ_HIP(hipMalloc((void**)&d_cell_rec_, (size_t)chunk * kCells * kCellRecWords * sizeof(uint32_t)));
+    DQ_HIP(hipMalloc((void**)&d_cell_idx_, (size_t)chunk * kCells * kCellCap * sizeof(uint16_t)));
+    cap_cells_ = chunk;
   }
-  DQ_HIP(hipMemcpyAsync(d_mapstage_, h_mapstage_, njobs * kMapBlockWords * 4,
-                        hipMemcpyHostToDevice, stream));
-  for (int i = 0; i < njobs; ++i) {
-    const MapJob& j = jobs[i];
-    const uint32_t* dpal = d_mapstage_ + i * kMapBlockWords;
-    const uint16_t* dlut = reinterpret_cast<const uint16_t*>(dpal + kMapPal);
-    const uint32_t* in = j.d_in;
-    uint32_t* out = j.d_out;
-    const size_t want = align4(j.n) + 4;
-    const bool staged = ((uintptr_t)in & 15) != 0 || ((uintptr_t)out & 15) != 0;
-    if (staged) {   // the map kernel uses 16-B loads/stores: go through aligned staging
-      if (2 * want > cap_map_align_) {
-        DQ_HIP(hipStreamSynchronize(stream));
-        if (d_map_align_) DQ_HIP(hipFree(d_map_align_));
-        DQ_HIP(hipMalloc((void**)&d_map_align_, want * 2 * sizeof(uint32_t)));
-        cap_map_align_ = want * 2;
-      }
-      DQ_HIP(hipMemcpyAsync(d_map_align_, in, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
-      in = d_map_align_;
-      out = d_map_align_ + want;
+  for (int c0 = 0; c0 < njobs; c0 += chunk) {
+    const int nt = std::min(chunk, njobs - c0);
+    if (c0 > 0) DQ_HIP(hipStreamSynchronize(stream));   // staging reuse
+    MapTask* ht = reinterpret_cast<MapTask*>(h_mapstage_);
+    uint32_t* hblk0 = h_mapstage_ + (size_t)chunk * sizeof(MapTask) / 4;
+    uint32_t* dblk0 = d_mapstage_ + (size_t)chunk * sizeof(MapTask) / 4;
+    int kmax = 1;
+    uint32_t nblocks = 0;
+    std::vector<int> staged;   // tasks whose in/out needed aligned staging
+    for (int t = 0; t < nt; ++t) {
+      const MapJob& j = jobs[c0 + t];
+      uint32_t* hb = hblk0 + (size_t)t * kMapBlockWords;
+      const uint32_t* db = dblk0 + (size_t)t * kMapBlockWords;
+      sorted_palette(j.ct, j.k, hb, reinterpret_cast<uint16_t*>(hb + kMapPal));
+      MapTask& m = ht[t];
+      m.in = j.d_in;
+      m.out = j.d_out;
+      if (((uintptr_t)j.d_in & 15) != 0 || ((uintptr_t)j.d_out & 15) != 0) staged.push_back(t);
+      m.pal = db;
+      m.lut = reinterpret_cast<const uint16_t*>(db + kMapPal);
+      m.cell_rec = d_cell_rec_ + (size_t)t * kCells * kCellRecWords;
+      m.cell_idx = d_cell_idx_ + (size_t)t * kCells * kCellCap;
+      m.n = j.n;
+      m.k = j.k;
+      m.grp_per_block = map_groups_per_block(j.n);
+      m.block_begin = nblocks;
+      const uint32_t groups = j.n / 8;
+      nblocks += std::max<uint32_t>(1, (groups + m.grp_per_block - 1) / m.grp_per_block);
+      kmax = std::max(kmax, j.k);
     }
-    timed_begin(stream);
-    launch_build_cells(dpal, j.k, d_cell_rec_, d_cell_idx_, stream);
-    timed_end(ST_CELLS, 0.0, stream);
-    timed_begin(stream);
-    launch_map(in, j.n, out, dpal, j.k, dlut, d_cell_rec_, d_cell_idx_, stream);
-    timed_end(ST_MAP, 8.0 * (double)j.n, stream);
-    if (staged)
-      DQ_HIP(hipMemcpyAsync(j.d_out, out, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
+    // misaligned in/out (the kernel uses 16-B accesses): aligned staging, one
+    // task at a time through a private buffer
+    size_t need = 0;
+    for (int t : staged) need = std::max<size_t>(need, 2 * (align4(ht[t].n) + 4));
+    if (need > cap_map_align_) {
+      DQ_HIP(hipStreamSynchronize(stream));
+      if (d_map_align_) DQ_HIP(hipFree(d_map_align_));
+      DQ_HIP(hipMalloc((void**)&d_map_align_, need * sizeof(uint32_t)));
+      cap_map_align_ = need;
+    }
+    const size_t bytes = (size_t)chunk * sizeof(MapTask) + (size_t)nt * kMapBlockWords * 4;
+    if (staged.empty()) {
+      DQ_HIP(hipMemcpyAsync(d_mapstage_, h_mapstage_, bytes, hipMemcpyHostToDevice, stream));
+      const MapTask* dt = reinterpret_cast<const MapTask*>(d_mapstage_);
+      timed_begin(stream);
+      launch_build_cells(dt, nt, kmax, stream);
+      timed_end(ST_CELLS, 0.0, stream);
+      double px = 0;
+      for (int t = 0; t < nt; ++t) px += ht[t].n;
+      timed_begin(stream);
+      launch_map(dt, nt, kmax, nblocks, stream);
+      timed_end(ST_MAP, 8.0 * px, stream);
+    } else {
+      // rare path: run the chunk task by task, staging misaligned buffers
+      for (int t = 0; t < nt; ++t) {
+        const MapJob& j = jobs[c0 + t];
+        MapTask one = ht[t];
+        const bool st = ((uintptr_t)j.d_in & 15) != 0 || ((uintptr_t)j.d_out & 15) != 0;
+        const size_t want = align4(j.n) + 4;
+        if (st) {
+          DQ_HIP(hipMemcpyAsync(d_map_align_, j.d_in, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
+          one.in = d_map_align_;
+          one.out = d_map_align_ + want;
+        }
+        one.block_begin = 0;
+        one.cell_rec = d_cell_rec_;
+        one.cell_idx = d_cell_idx_;
+        DQ_HIP(hipStreamSynchronize(stream));   // staging slot 0 reuse
+        ht[0] = one;
+        if (t != 0) std::memcpy(hblk0, hblk0 + (size_t)t * kMapBlockWords, kMapBlockWords * 4);
+        ht[0].pal = dblk0;
+        ht[0].lut = reinterpret_cast<const uint16_t*>(dblk0 + kMapPal);
+        DQ_HIP(hipMemcpyAsync(d_mapstage_, h_mapstage_,
+                              (size_t)chunk * sizeof(MapTask) + kMapBlockWords * 4,
+                              hipMemcpyHostToDevice, stream));
+        const MapTask* dt = reinterpret_cast<const MapTask*>(d_mapstage_);
+        const uint32_t nb = std::max<uint32_t>(1, (j.n / 8 + one.grp_per_block - 1) / one.grp_per_block);
+        timed_begin(stream);
+        launch_build_cells(dt, 1, j.k, stream);
+        timed_end(ST_CELLS, 0.0, stream);
+        timed_begin(stream);
+        launch_map(dt, 1, j.k, nb, stream);
+        timed_end(ST_MAP, 8.0 * (double)j.n, stream);
+        if (st)
+          DQ_HIP(hipMemcpyAsync(j.d_out, d_map_align_ + want, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
+      }
+    }
   }
   DQ_HIP(hipStreamSynchronize(stream));
   collect_timing();
@@ -899,15 +967,23 @@ void Engine::map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
   map_many(&j, 1, stream);
 }
 
-Engine& engine_for(int device) {
+Engine& engine_for(int device, int lane) {
   static std::mutex mu;
-  static std::map<int, Engine*> engines;
+  static std::map<std::pair<int, int>, Engine*> engines;
   std::lock_guard<std::mutex> g(mu);
-  auto it = engines.find(device);
+  auto it = engines.find({device, lane});
   if (it != engines.end()) return *it->second;
   Engine* e = new Engine(device);
-  engines[device] = e;
+  engines[{device, lane}] = e;
   return *e;
+}
+
+int batch_lanes() {
+  static int lanes = [] {
+    const char* v = getenv("DQ_HIP_LANES");
+    return v && v[0] ? std::max(1, std::min(kMaxLanes, atoi(v))) : 3;
+  }();
+  return lanes;
 }
 
 }  // namespace dq

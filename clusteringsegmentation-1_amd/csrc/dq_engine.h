@@ -136,6 +136,16 @@ class Engine {
   uint64_t last_points_full = 0;      // the same without fixed-point finalisation
 
   void set_timing(bool on) { timing_ = on; }
+  bool timing() const { return timing_; }
+  // add another engine's kernel stats to this one's (and clear them there)
+  void absorb_stats(Engine& o) {
+    for (int i = 0; i < ST_COUNT; ++i) {
+      stats[i].launches += o.stats[i].launches;
+      stats[i].ms += o.stats[i].ms;
+      stats[i].bytes += o.stats[i].bytes;
+    }
+    o.reset_stats();
+  }
   // Finalise a split when its 2-means reaches an exact fixed point (default
   // on; results are identical either way -- dq_kernels.hip, node_update).
   void set_fixed_point(bool on) { fixed_point_ = on; }
@@ -215,12 +225,15 @@ class Engine {
   size_t cap_stat_ = 0;
   uint64_t seq_ = 0;                  // round sequence number
   int lookahead_ = 1;                 // 2-means iterations queued past the one awaited
+  int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TILES)
+  uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TILE_MAX)
   // host-side trace (DQ_HIP_TRACE=1): per-run phase times on stderr
   bool trace_ = false;
   double tr_wait_us_ = 0, tr_build_us_ = 0, tr_replay_us_ = 0;
 
   // map tables
-  uint32_t* d_cell_rec_ = nullptr;
+  uint32_t* d_cell_rec_ = nullptr;    // per map task of a chunk
+  size_t cap_cells_ = 0;
   uint16_t* d_cell_idx_ = nullptr;
   uint32_t* h_mapstage_ = nullptr;   // pinned: per map [sorted palette | start LUT]
   uint32_t* d_mapstage_ = nullptr;
@@ -241,7 +254,13 @@ class Engine {
   hipEvent_t take_event();
 };
 
-// Process-wide engine for a device (created on first use).
-Engine& engine_for(int device);
+// Process-wide engines of a device (created on first use).  Lane 0 serves
+// every call and holds the diagnostics; a batch of frames is split over
+// batch_lanes() lanes, each an engine with its own stream driven by its own
+// host thread, so one group's kernels fill the GPU while another group's host
+// replays its round (DQ_HIP_LANES, default 3: measured best for 8 4K frames).
+constexpr int kMaxLanes = 8;
+Engine& engine_for(int device, int lane = 0);
+int batch_lanes();
 
 }  // namespace dq

@@ -116,10 +116,19 @@ struct alignas(32) PartTile {
 };
 
 // Per-launch completion counters of the round's 2-means epilogues (device
-// memory, zeroed with the round's tables).
-struct alignas(16) LaunchCtr {
-  uint64_t word;            // low 32 bits: workgroups arrived; high: nodes not final
-  uint64_t pad;
+// memory, zeroed with the round's tables).  Each word: low 32 bits =
+// arrivals, high 32 = records not final.  Workgroup b arrives on shard
+// b % kArrShards (one atomic per workgroup on one address serialises at
+// ~13 ns: 1024 workgroups cost ~13 us); a shard's last arriver forwards the
+// shard's active count to `top`, whose last arriver publishes the status.
+constexpr int kArrShards = 16;
+struct alignas(64) ArrWord {
+  uint64_t word;
+  uint64_t pad[7];
+};
+struct alignas(64) LaunchCtr {
+  ArrWord shard[kArrShards];
+  ArrWord top;
 };
 
 // The last-arriving epilogue workgroup of 2-means iteration `it` publishes

@@ -60,13 +60,26 @@ void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stre
 // accumulates the children's split-pass statistics.
 void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream);
 
-// Map: candidate records per colour cell, then the per-pixel argmin over
-// (squared distance, MPS visit rank).
-void launch_build_cells(const uint32_t* pal_sorted, int k, uint32_t* cell_rec,
-                        uint16_t* cell_idx, hipStream_t stream);
-void launch_map(const uint32_t* in, uint32_t n, uint32_t* out,
-                const uint32_t* pal_sorted, int k, const uint16_t* lut_init,
-                const uint32_t* cell_rec, const uint16_t* cell_idx,
-                hipStream_t stream);
+// One map_colors_mps job of a batched map launch (device-resident table).
+struct alignas(16) MapTask {
+  const uint32_t* in;       // n pixels (16-B aligned)
+  uint32_t* out;            // n mapped colours (16-B aligned)
+  const uint32_t* pal;      // k colours sorted by R+G+B (reference comparator)
+  const uint16_t* lut;      // 766 start entries (lut_init)
+  uint32_t* cell_rec;       // kCells x 16 B candidate records
+  uint16_t* cell_idx;       // kCells x kCellCap overflow lists
+  uint32_t n;
+  int32_t k;
+  uint32_t block_begin;     // first map workgroup of this task
+  uint32_t grp_per_block;   // groups of kMapPx pixels per workgroup
+};
+
+// Map: candidate records per colour cell for every task (one launch), then
+// the per-pixel argmin over (squared distance, MPS visit rank) for every
+// task (one launch of nblocks workgroups; task t owns workgroups
+// [block_begin, block_begin + ceil(n / kMapPx / grp_per_block))).
+void launch_build_cells(const MapTask* tasks, int ntasks, int kmax, hipStream_t stream);
+uint32_t map_groups_per_block(uint32_t n);
+void launch_map(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream);
 
 }  // namespace dq

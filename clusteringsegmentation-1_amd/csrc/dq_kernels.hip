@@ -461,9 +461,10 @@ __global__ __launch_bounds__(kBlock) void nodesum_kernel(RoundArgs a) {
 //   * a record whose split became final: the partition's per-(tile, wave)
 //     write cursors, and the results written straight to host memory
 //     (NodeResult);
-//   * 2-means launches: every workgroup arrives on the launch's counter; the
-//     last to arrive publishes (round seq, records still active) to the host,
-//     which stops launching iterations once no node is active.
+//   * 2-means launches: every workgroup arrives on the launch's (sharded)
+//     counter; the last to arrive publishes (round seq, records still
+//     active) to the host, which stops launching iterations once no node is
+//     active.
 template <int KIND, bool FROM_TOT>
 __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
   constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
@@ -545,14 +546,24 @@ __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
     if (threadIdx.x < 64) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (threadIdx.x == 0) {
-        // one 64-bit arrival: low word = workgroups arrived, high = still active
+        // 64-bit arrivals (low word = arrived, high = still active) on this
+        // workgroup's shard, then the shard's last arriver on the top word
+        LaunchCtr* c = a.ctr + a.it;
+        const uint32_t sh = blockIdx.x % kArrShards;
+        const uint32_t nsh = min((uint32_t)a.nn, (uint32_t)kArrShards);
+        const uint32_t in_shard = ((uint32_t)a.nn - sh + kArrShards - 1) / kArrShards;
         const uint64_t mine = 1ull | ((uint64_t)(!skip && !final_results) << 32);
-        const uint64_t old = __hip_atomic_fetch_add(&a.ctr[a.it].word, mine, __ATOMIC_RELAXED,
+        const uint64_t old = __hip_atomic_fetch_add(&c->shard[sh].word, mine, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)old == (uint32_t)a.nn - 1) {
-          const uint64_t act = (old >> 32) + (mine >> 32);
-          __hip_atomic_store(a.hstat + a.it, (a.seq << 32) | (act << 1) | 1ull, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)old == in_shard - 1) {
+          const uint64_t fwd = 1ull | (((old >> 32) + (mine >> 32)) << 32);
+          const uint64_t t = __hip_atomic_fetch_add(&c->top.word, fwd, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)t == nsh - 1) {
+            const uint64_t act = (t >> 32) + (fwd >> 32);
+            __hip_atomic_store(a.hstat + a.it, (a.seq << 32) | (act << 1) | 1ull,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
         }
       }
     }
@@ -721,65 +732,73 @@ __global__ __launch_bounds__(kBlock) void partsplit_kernel(RoundArgs a) {
 // Map, step 1: per colour cell (8x8x8 values), the palette entries whose
 // minimum distance to the cell does not exceed the smallest maximum distance
 // of any entry to the cell.  Every exact argmin for a colour of the cell is
-// among them (ties included: <=).  One WAVE per cell: lanes stride the palette
-// (coalesced), a wave min gives the bound, ballots compact the candidates in
-// palette order.
+// among them (ties included: <=).  grid = (kCells / kCellsPerBlock, tasks):
+// the task's palette is staged in LDS once per workgroup; one WAVE per cell at
+// a time (lanes stride the palette, a wave min gives the bound, ballots
+// compact the candidates in palette order).
 // Record (16 B): x[15:0] count c; x[31:16], y, z, w: the first kCellInline
 // candidates' sorted indices (u16), unused slots = k (a sentinel entry that is
 // farther than any real one); c > kCellInline: all c indices in
 // cell_idx[cell*kCellCap ...]; c == kCellBrute: scan the whole palette.
-__global__ __launch_bounds__(kBlock) void build_cells_kernel(
-    const uint32_t* __restrict__ pal, int k, uint32_t* __restrict__ cell_rec,
-    uint16_t* __restrict__ cell_idx) {
+constexpr int kCellsPerBlock = 16;
+__global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __restrict__ tasks) {
+  const MapTask tk = tasks[blockIdx.y];
+  const int k = tk.k;
+  extern __shared__ uint32_t spal_c[];   // k colours
   __shared__ uint16_t srec[kBlock / 64][8];
+  for (int i = threadIdx.x; i < k; i += kBlock) spal_c[i] = as_g(tk.pal)[i];
+  __syncthreads();
   const uint32_t lane = lane_id(), w = wave_id();
-  const uint32_t cell = blockIdx.x * (kBlock / 64) + w;   // grid = kCells / 4: always valid
   const int cw = 1 << (8 - kCellBits);
-  const int lo0 = (int)(cell >> (2 * kCellBits)) * cw;
-  const int lo1 = (int)((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
-  const int lo2 = (int)(cell & ((1 << kCellBits) - 1)) * cw;
-  const int hi0 = lo0 + cw - 1, hi1 = lo1 + cw - 1, hi2 = lo2 + cw - 1;
   auto far2 = [](int v, int lo, int hi) { const int x = max(v - lo, hi - v); return x * x; };
   auto near2 = [](int v, int lo, int hi) {
     const int x = v < lo ? lo - v : (v > hi ? v - hi : 0);
     return x * x;
   };
-  g_cu32* gp = as_g(pal);
-  int bound = 0x7FFFFFFF;
-  for (int e = (int)lane; e < k; e += 64) {
-    const uint32_t q = gp[e];
-    bound = min(bound, far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) +
-                           far2(q & 0xFF, lo2, hi2));
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) bound = min(bound, __shfl_xor(bound, o, 64));
-  if (lane < 8) srec[w][lane] = (uint16_t)k;
-  uint16_t* lst = cell_idx + (size_t)cell * kCellCap;
-  uint32_t count = 0;
-  for (int base = 0; base < k; base += 64) {
-    const int e = base + (int)lane;
-    bool cand = false;
-    if (e < k) {
-      const uint32_t q = gp[e];
-      cand = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
-                 near2(q & 0xFF, lo2, hi2) <= bound;
+  for (int ci = (int)w; ci < kCellsPerBlock; ci += kBlock / 64) {
+    const uint32_t cell = blockIdx.x * kCellsPerBlock + ci;   // grid.x = kCells / kCellsPerBlock
+    const int lo0 = (int)(cell >> (2 * kCellBits)) * cw;
+    const int lo1 = (int)((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
+    const int lo2 = (int)(cell & ((1 << kCellBits) - 1)) * cw;
+    const int hi0 = lo0 + cw - 1, hi1 = lo1 + cw - 1, hi2 = lo2 + cw - 1;
+    int bound = 0x7FFFFFFF;
+    for (int e = (int)lane; e < k; e += 64) {
+      const uint32_t q = spal_c[e];
+      bound = min(bound, far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) +
+                             far2(q & 0xFF, lo2, hi2));
     }
-    const uint64_t m = __ballot(cand);
-    const uint32_t pos = count + mbcnt64(m);
-    if (cand && pos < (uint32_t)kCellCap) lst[pos] = (uint16_t)e;
-    if (cand && pos < (uint32_t)kCellInline) srec[w][1 + pos] = (uint16_t)e;
-    count += (uint32_t)__popcll(m);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  if (lane == 0) {
-    const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
-    uint4 r;
-    r.x = c | ((uint32_t)srec[w][1] << 16);
-    r.y = srec[w][2] | ((uint32_t)srec[w][3] << 16);
-    r.z = srec[w][4] | ((uint32_t)srec[w][5] << 16);
-    r.w = srec[w][6] | ((uint32_t)srec[w][7] << 16);
-    reinterpret_cast<uint4*>(cell_rec)[cell] = r;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) bound = min(bound, __shfl_xor(bound, o, 64));
+    if (lane < 8) srec[w][lane] = (uint16_t)k;
+    uint16_t* lst = tk.cell_idx + (size_t)cell * kCellCap;
+    uint32_t count = 0;
+    for (int base = 0; base < k; base += 64) {
+      const int e = base + (int)lane;
+      bool cand = false;
+      if (e < k) {
+        const uint32_t q = spal_c[e];
+        cand = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
+                   near2(q & 0xFF, lo2, hi2) <= bound;
+      }
+      const uint64_t m = __ballot(cand);
+      const uint32_t pos = count + mbcnt64(m);
+      if (cand && pos < (uint32_t)kCellCap) lst[pos] = (uint16_t)e;
+      if (cand && pos < (uint32_t)kCellInline) srec[w][1 + pos] = (uint16_t)e;
+      count += (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
+      uint4 r;
+      r.x = c | ((uint32_t)srec[w][1] << 16);
+      r.y = srec[w][2] | ((uint32_t)srec[w][3] << 16);
+      r.z = srec[w][4] | ((uint32_t)srec[w][5] << 16);
+      r.w = srec[w][6] | ((uint32_t)srec[w][7] << 16);
+      reinterpret_cast<uint4*>(tk.cell_rec)[cell] = r;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -795,6 +814,8 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(
 // j is recovered from sad (4j = 4s+1 +- sad).  Inline candidates are
 // branch-free; only cells with more than kCellInline candidates take a
 // wave-uniform slow path over their list.
+// Batched: workgroup b serves the task whose [block_begin, +blocks) holds b
+// and maps that task's groups of kMapPx pixels [lb*gpb, (lb+1)*gpb).
 constexpr int kMapPx = 8;   // pixels per lane per iteration (two 16-B loads)
 
 template <bool kWide>
@@ -804,22 +825,31 @@ __device__ __forceinline__ uint32_t entry_from_sad(uint32_t S, uint32_t sad) {
 }
 
 template <bool kWide>
-__global__ __launch_bounds__(kBlock) void map_kernel(
-    const uint32_t* __restrict__ in, uint32_t n, uint32_t* __restrict__ out,
-    const uint32_t* __restrict__ pal, int k, const uint16_t* __restrict__ lut,
-    const uint32_t* __restrict__ cell_rec, const uint16_t* __restrict__ cell_idx) {
+__global__ __launch_bounds__(kBlock) void map_kernel(const MapTask* __restrict__ tasks, int ntasks) {
+  int ti = 0;
+  while (ti + 1 < ntasks && tasks[ti + 1].block_begin <= blockIdx.x) ++ti;
+  const MapTask tk = tasks[ti];
+  const uint32_t* __restrict__ in = tk.in;
+  uint32_t* __restrict__ out = tk.out;
+  const uint32_t n = tk.n;
+  const int k = tk.k;
+  const uint16_t* __restrict__ cell_idx = tk.cell_idx;
   extern __shared__ uint32_t smem[];
   uint2* spal = reinterpret_cast<uint2*>(smem);              // k+1: colour, |c|^2 + 2^19
   uint16_t* slut = reinterpret_cast<uint16_t*>(smem + 2 * (k + 1));
+  g_cu32* gpal = as_g(tk.pal);
+  typedef const __attribute__((address_space(1))) uint16_t g_cu16;
+  g_cu16* glut = (g_cu16*)tk.lut;
+  g_cu16* gidx = (g_cu16*)cell_idx;
   for (int i = threadIdx.x; i <= k; i += kBlock) {
-    const uint32_t q = i < k ? pal[i] : 0u;
+    const uint32_t q = i < k ? gpal[i] : 0u;
     // the sentinel (index k, unused inline slots) has d' = 2^20 - 1: it never wins
     const uint32_t c2 = i < k ? __builtin_amdgcn_udot4(q, q, 0u, false) + (1u << 19) : 0xFFFFFu;
     spal[i] = make_uint2(q, c2);
   }
-  for (int i = threadIdx.x; i < 766; i += kBlock) slut[i] = lut[i];
+  for (int i = threadIdx.x; i < 766; i += kBlock) slut[i] = glut[i];
   __syncthreads();
-  g_cu4* rec4 = (g_cu4*)cell_rec;
+  g_cu4* rec4 = (g_cu4*)tk.cell_rec;
   g_cu4* in4 = (g_cu4*)in;
   typedef __attribute__((address_space(1))) u32x4 g_u4;
 
@@ -832,10 +862,12 @@ __global__ __launch_bounds__(kBlock) void map_kernel(
   };
 
   const uint32_t ngrp = n / kMapPx;
-  const uint32_t stride = gridDim.x * kBlock;
-  for (uint32_t g = blockIdx.x * kBlock + threadIdx.x;; g += stride) {
-    const bool have = g < ngrp;
-    if (!__any(have)) break;
+  const uint32_t lb = blockIdx.x - tk.block_begin;
+  const uint32_t g0 = lb * tk.grp_per_block;
+  const uint32_t g1 = min(ngrp, g0 + tk.grp_per_block);
+  for (uint32_t gb = g0; gb < g1; gb += kBlock) {
+    const uint32_t g = gb + threadIdx.x;
+    const bool have = g < g1;
     uint32_t px[kMapPx];
     {
       const u32x4 a = have ? in4[2 * g] : (u32x4){0u, 0u, 0u, 0u};
@@ -886,7 +918,7 @@ __global__ __launch_bounds__(kBlock) void map_kernel(
         if (cnt == kCellBrute) {
           for (int j = 0; j < k; ++j) { const uint64_t key = full_key(p, S, (uint32_t)j); best = key < best ? key : best; }
         } else {
-          const uint16_t* lst = cell_idx + (size_t)cell[e] * kCellCap;
+          g_cu16* lst = gidx + (size_t)cell[e] * kCellCap;
           for (uint32_t m = 0; m < cnt; ++m) { const uint64_t key = full_key(p, S, lst[m]); best = key < best ? key : best; }
         }
         const uint32_t sad = (uint32_t)(kWide ? (best & 0xFFFFFFFFull) : (best & 0xFFFu));
@@ -898,15 +930,15 @@ __global__ __launch_bounds__(kBlock) void map_kernel(
       ((g_u4*)as_gw(out))[2 * g + 1] = (u32x4){res[4], res[5], res[6], res[7]};
     }
   }
-  // tail (n % kMapPx points): block 0, one point per lane, whole palette
+  // tail (n % kMapPx points): the task's first workgroup, one point per lane, whole palette
   const uint32_t t = ngrp * kMapPx + threadIdx.x;
-  if (blockIdx.x == 0 && t < n) {
-    const uint32_t p = in[t] & 0xFFFFFFu;
+  if (lb == 0 && t < n) {
+    const uint32_t p = as_g(in)[t] & 0xFFFFFFu;
     const uint32_t S = 4u * slut[((p >> 16) & 0xFF) + ((p >> 8) & 0xFF) + (p & 0xFF)] + 1u;
     uint64_t best = ~0ull;
     for (int j = 0; j < k; ++j) { const uint64_t key = full_key(p, S, (uint32_t)j); best = key < best ? key : best; }
     const uint32_t sad = (uint32_t)(kWide ? (best & 0xFFFFFFFFull) : (best & 0xFFFu));
-    out[t] = spal[entry_from_sad<kWide>(S, sad)].x;
+    as_gw(out)[t] = spal[entry_from_sad<kWide>(S, sad)].x;
   }
 }
 
@@ -960,28 +992,26 @@ void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream) {
   partsplit_kernel<<<dim3(nptiles), dim3(kBlock), 0, stream>>>(a);
 }
 
-void launch_build_cells(const uint32_t* pal_sorted, int k, uint32_t* cell_rec,
-                        uint16_t* cell_idx, hipStream_t stream) {
-  static_assert(kCells % (kBlock / 64) == 0, "one wave per cell");
-  build_cells_kernel<<<dim3(kCells / (kBlock / 64)), dim3(kBlock), 0, stream>>>(
-      pal_sorted, k, cell_rec, cell_idx);
+void launch_build_cells(const MapTask* tasks, int ntasks, int kmax, hipStream_t stream) {
+  static_assert(kCells % kCellsPerBlock == 0, "whole cells per workgroup");
+  if (ntasks <= 0) return;
+  build_cells_kernel<<<dim3(kCells / kCellsPerBlock, ntasks), dim3(kBlock), (size_t)kmax * 4,
+                       stream>>>(tasks);
 }
 
-void launch_map(const uint32_t* in, uint32_t n, uint32_t* out,
-                const uint32_t* pal_sorted, int k, const uint16_t* lut_init,
-                const uint32_t* cell_rec, const uint16_t* cell_idx,
-                hipStream_t stream) {
-  if (n == 0) return;
-  const size_t lds = (size_t)(k + 1) * 8 + 768 * 2;
-  uint32_t blocks = (n / kMapPx + kBlock - 1) / kBlock;
-  if (blocks > 2048) blocks = 2048;
-  if (blocks == 0) blocks = 1;
-  if (k <= 1024)   // 12-bit rank field in the 32-bit key
-    map_kernel<false><<<dim3(blocks), dim3(kBlock), lds, stream>>>(in, n, out, pal_sorted, k,
-                                                                  lut_init, cell_rec, cell_idx);
+uint32_t map_groups_per_block(uint32_t n) {
+  // ~8 groups of kMapPx pixels per lane per workgroup: 16K pixels
+  (void)n;
+  return 8u * kBlock;
+}
+
+void launch_map(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream) {
+  if (ntasks <= 0 || nblocks == 0) return;
+  const size_t lds = (size_t)(kmax + 1) * 8 + 768 * 2;
+  if (kmax <= 1024)   // 12-bit rank field in the 32-bit key
+    map_kernel<false><<<dim3(nblocks), dim3(kBlock), lds, stream>>>(tasks, ntasks);
   else
-    map_kernel<true><<<dim3(blocks), dim3(kBlock), lds, stream>>>(in, n, out, pal_sorted, k,
-                                                                 lut_init, cell_rec, cell_idx);
+    map_kernel<true><<<dim3(nblocks), dim3(kBlock), lds, stream>>>(tasks, ntasks);
 }
 
 }  // namespace dq

@@ -247,3 +247,26 @@ def test_fixed_point_finalisation_is_exact(gpu):
                 assert gpu.last_points_swept() < full
     finally:
         gpu.set_fixed_point(True)
+
+
+def test_batch_over_lanes(gpu):
+    """A batch of frames in one call is split over engine lanes (own stream,
+    own host thread each): every frame bit-exact against the oracle, and the
+    diagnostics report the batch's last frame."""
+    import torch
+    frames = [fx.xorshift(200000 + 1000 * i, seed=300 + i) for i in range(5)]
+    frames[2] &= 0xF0F0F0
+    t_in = [torch.from_numpy(p.view(np.int32)).to("cuda:0") for p in frames]
+    t_out = [torch.empty_like(t) for t in t_in]
+    cts, _ = gpu.quant_batch_device(t_in, t_out, 64)
+    torch.cuda.synchronize()
+    for px, t, ct in zip(frames, t_out, cts):
+        orc_out = np.zeros(len(px), np.uint32)
+        kk = ctypes.c_uint32(64)
+        ct2 = np.zeros(64, np.uint32)
+        fx.oracle().dqo_quant_recurse(ctypes.c_uint32(len(px)), fx.vp(px), fx.vp(orc_out),
+                                      ctypes.byref(kk), fx.vp(ct2))
+        assert np.array_equal(ct, ct2[:kk.value])
+        assert np.array_equal(t.cpu().numpy().view(np.uint32), orc_out)
+    ref_trace = _oracle_cluster(frames[-1], 64)[3]
+    assert np.array_equal(gpu.last_trace(64), ref_trace)
