@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline region")
     ap.add_argument("--no-c3", action="store_true", help="skip the single-frame C3 measurement")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="engine lanes per batch (0: library default); the roofline region always uses 1")
     return ap.parse_args()
 
 
@@ -169,7 +171,9 @@ def pick_roofline(stats, pmc_key):
             "kernel": ROOF_KERNELS[kind], "launches": launches,
             "avg_launch_us": round(ms * 1e3 / launches, 2),
             "alg_bytes_per_launch": round(alg / launches),
-            "share_of_step_kernel_time": round(ms / sum(v[1] for v in stats.values() if v[1] > 0), 3)}
+            "share_of_step_kernel_time": round(ms / sum(v[1] for v in stats.values() if v[1] > 0), 3),
+            "measured": "HIP events around every launch on the engine's stream, one engine lane "
+                        "(kernels not overlapped), same workload as the timed region"}
     if os.path.exists(PMC_FILE):
         try:
             pmc = json.load(open(PMC_FILE)).get(pmc_key, {}).get(ROOF_KERNELS[kind])
@@ -240,6 +244,8 @@ def main():
         parallelism = "row-tiles x%d" % world
         scaling = "strong"
 
+    pkg.set_lanes(a.lanes)
+    lanes = pkg.get_lanes()
     for _ in range(a.warmup):
         step()
     # --- timed region: no per-launch events (they would perturb the timing)
@@ -249,6 +255,10 @@ def main():
     # launch (on the library's launch stream) for per-kernel durations
     stats = {}
     if not a.no_timing:
+        # kernels measured un-overlapped: one engine lane, so an event pair
+        # around a launch times that kernel alone on the GPU
+        pkg.set_lanes(1)
+        step()
         pkg.reset_stats(device=local)
         pkg.set_timing(True, device=local)
         for _ in range(a.steps):
@@ -256,6 +266,7 @@ def main():
         torch.cuda.synchronize(dev)
         pkg.set_timing(False, device=local)
         stats = pkg.get_stats(device=local)
+        pkg.set_lanes(a.lanes)
     rounds = pkg.last_rounds(device=local)
     swept = pkg.last_points_swept(device=local)
     full = pkg.last_points_full(device=local)
@@ -297,6 +308,7 @@ def main():
             "dtype": "u8x3 pixels in u32, u32/u64 integer sums, f64 updates",
             "data": "synthetic uniform-random 24-bit RGB frames (torch.randint on device)",
             "config": {"workload": workload, "frames_per_rank_per_step": nf if a.mode == "frames" else None,
+                       "engine_lanes": lanes if a.mode == "frames" else 1,
                        "width": w, "height": h, "k": k, "max_iters": 10, "parallelism": parallelism},
             "roofline": roof,
             "detail": {"ms_per_frame": round(dt * 1e3 / a.steps / (nf * world if a.mode == "frames" else 1), 3),

@@ -81,6 +81,8 @@ def lib():
         "dq_hip_get_stat": ([c.c_int, c.c_int, c.POINTER(c.c_uint64), c.POINTER(c.c_double),
                              c.POINTER(c.c_double)], c.c_int),
         "dq_hip_stat_name": ([c.c_int], c.c_char_p),
+        "dq_hip_set_lanes": ([c.c_int], None),
+        "dq_hip_get_lanes": ([], c.c_int),
         "quant_recurse": ([c.c_uint32, vp, vp, u32p, vp, c.c_int], None),
     }
     for name, (args, res) in sigs.items():
@@ -302,6 +304,15 @@ def last_points_full(device=0):
 def set_fixed_point(on, device=0):
     """Fixed-point finalisation of 2-means splits (identical outputs)."""
     lib().dq_hip_set_fixed_point(device, 1 if on else 0)
+
+
+def set_lanes(lanes):
+    """Engine lanes a batch is split over (0: default, DQ_HIP_LANES or 3)."""
+    lib().dq_hip_set_lanes(int(lanes))
+
+
+def get_lanes():
+    return lib().dq_hip_get_lanes()
 
 
 def set_timing(on, device=0):

@@ -301,6 +301,9 @@ void dq_hip_set_fixed_point(int device, int on) { engine_for(device).set_fixed_p
 
 void dq_hip_set_timing(int device, int on) { engine_for(device).set_timing(on != 0); }
 
+void dq_hip_set_lanes(int lanes) { dq::set_batch_lanes(lanes); }
+int dq_hip_get_lanes(void) { return dq::batch_lanes(); }
+
 void dq_hip_reset_stats(int device) { engine_for(device).reset_stats(); }
 
 int dq_hip_get_stat(int device, int kind, uint64_t* launches, double* ms, double* bytes) {

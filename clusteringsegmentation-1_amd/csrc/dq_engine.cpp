@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <chrono>
 #include <unordered_set>
 
@@ -978,12 +979,17 @@ Engine& engine_for(int device, int lane) {
   return *e;
 }
 
+static std::atomic<int> g_lanes_override{0};
+
 int batch_lanes() {
   static int lanes = [] {
     const char* v = getenv("DQ_HIP_LANES");
     return v && v[0] ? std::max(1, std::min(kMaxLanes, atoi(v))) : 3;
   }();
-  return lanes;
+  const int o = g_lanes_override.load();
+  return o > 0 ? std::min(o, kMaxLanes) : lanes;
 }
+
+void set_batch_lanes(int lanes) { g_lanes_override.store(std::max(0, lanes)); }
 
 }  // namespace dq

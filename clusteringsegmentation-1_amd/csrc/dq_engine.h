@@ -262,5 +262,6 @@ class Engine {
 constexpr int kMaxLanes = 8;
 Engine& engine_for(int device, int lane = 0);
 int batch_lanes();
+void set_batch_lanes(int lanes);   // 0: the default
 
 }  // namespace dq

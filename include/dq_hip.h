@@ -98,6 +98,11 @@ uint64_t dq_hip_last_points_full(int device);
  * Outputs are identical either way; only the swept points differ. */
 void dq_hip_set_fixed_point(int device, int on);
 
+/* Engine lanes a batch of frames is split over (each: own stream, own host
+ * thread; DQ_HIP_LANES, default 3).  lanes = 0 restores the default. */
+void dq_hip_set_lanes(int lanes);
+int dq_hip_get_lanes(void);
+
 /* ---- per-kernel timing (HIP events on the launch stream) -----------------
  * kinds: 0 init pass, 1 split pass, 2 2-means pass, 3 last 2-means pass,
  * 4 epilogue, 5 partition, 6 map cells, 7 map.  bytes = algorithmic bytes. */
