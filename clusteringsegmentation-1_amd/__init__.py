@@ -24,7 +24,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libdivquant_hip.so")
+# DQ_HIP_LIB: another build of the same library (kernel variants in experiments)
+LIB_PATH = os.environ.get("DQ_HIP_LIB") or os.path.join(PKG_DIR, "libdivquant_hip.so")
 
 STAT_KINDS = ["pass_init", "pass_split", "pass_kmeans", "pass_klast",
               "epilogue", "partition", "map_cells", "map"]

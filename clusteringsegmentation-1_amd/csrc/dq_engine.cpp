@@ -675,6 +675,9 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     }
   }
   DQ_CHECK(total < (1ull << 32), "batch larger than 2^32 points");
+  for (int i = 0; i < nframes; ++i)
+    for (int sh = 0; sh < S; ++sh)   // partition stores use 32-bit byte offsets
+      DQ_CHECK(frames_[i].n[sh] < (1u << 29), "a frame shard holds at most 2^29 points");
   ensure_pixels(total);
   if (align_need > cap_align_) {
     if (d_align_) DQ_HIP(hipFree(d_align_));

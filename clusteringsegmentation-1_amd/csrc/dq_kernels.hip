@@ -637,7 +637,13 @@ __device__ __forceinline__ void decide_sweep(const u32x4 v[kVecPerThread], uint3
 // two contiguous runs of the child buffer), with the next sweep's loads in
 // flight.  No LDS and no barrier until the final reduction of the sums.
 // One 32-B partial per tile: [0..3] old child, [4..7] new child.
-__global__ __launch_bounds__(kBlock) void partsplit_kernel(RoundArgs a) {
+#ifndef DQ_PS_WAVES
+#define DQ_PS_WAVES 1
+#endif
+#ifndef DQ_PS_PREFETCH
+#define DQ_PS_PREFETCH 1
+#endif
+__global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArgs a) {
   constexpr int kSlots = kVecPerThread * 4;
   const PartTile pt = a.ptiles[blockIdx.x];
   const Tile* tp = pt.tile;
@@ -645,7 +651,9 @@ __global__ __launch_bounds__(kBlock) void partsplit_kernel(RoundArgs a) {
   const uint32_t w = wave_id(), l = lane_id();
   const uint32_t start = tp->start, end = tp->end;
   g_cu4* src4 = as_g4(nd.src);
-  g_u32* dst = as_gw(nd.dst);
+  // child buffer of the frame shard: every index < off + len < 2^30
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+      nd.dst, (short)0, (int)((nd.off + nd.len) * 4u), 0x00020000);
   const Params q = nd.prm;
   const uint32_t n_old = nd.len - nd.n_new_local;
   uint32_t oc = nd.off + tp->old_base[w];
@@ -691,23 +699,54 @@ __global__ __launch_bounds__(kBlock) void partsplit_kernel(RoundArgs a) {
     // --- next sweep's loads in flight during the stores
     const uint32_t nvs = vs + kSweep;
     const bool nfull = nvs >= start && nvs + kSweep <= end;
+#if DQ_PS_PREFETCH
     u32x4 vn[kVecPerThread];
     if (nvs < end) {
       if (nfull) load_sweep<true>(src4, nvs, end, vn);
       else load_sweep<false>(src4, nvs, end, vn);
     }
-    // --- this wave's points, slot by slot, ranked by ballot
+#endif
+    // --- this wave's points, slot by slot, ranked by ballot; raw buffer
+    //     stores (SGPR descriptor + 32-bit offset).  In a full sweep every
+    //     slot is valid: a lane's rank among the new points is its lane id
+    //     minus its rank among the old ones (one ballot, one mbcnt pair).
+    //     Partial sweeps: out-of-range offsets are dropped by the buffer
+    //     bounds check, so invalid slots get one.
+    if (full) {
 #pragma unroll
-    for (int sidx = 0; sidx < kSlots; ++sidx) {
-      const bool o = (oldm >> sidx) & 1u, n = (newm >> sidx) & 1u;
-      const uint64_t bo = __ballot(o), bn = __ballot(n);
-      const uint32_t idx = o ? oc + mbcnt64(bo) : nc + mbcnt64(bn);
-      if (o || n) dst[idx] = vec_elem(v[sidx >> 2], sidx & 3);
-      oc += (uint32_t)__popcll(bo);
-      nc += (uint32_t)__popcll(bn);
+      for (int sidx = 0; sidx < kSlots; ++sidx) {
+        const bool o = (oldm >> sidx) & 1u;
+        const uint64_t bo = __ballot(o);
+        const uint32_t ro = mbcnt64(bo);
+        const uint32_t idx = o ? oc + ro : nc + (l - ro);
+        __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
+                                              (int)(idx * 4u), 0, 0);
+        const uint32_t co = (uint32_t)__popcll(bo);
+        oc += co;
+        nc += 64u - co;
+      }
+    } else {
+#pragma unroll
+      for (int sidx = 0; sidx < kSlots; ++sidx) {
+        const bool o = (oldm >> sidx) & 1u, n = (newm >> sidx) & 1u;
+        const uint64_t bo = __ballot(o), bn = __ballot(n);
+        uint32_t idx = o ? oc + mbcnt64(bo) : nc + mbcnt64(bn);
+        idx = (o || n) ? idx : 0x3FFFFFFFu;
+        __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
+                                              (int)(idx * 4u), 0, 0);
+        oc += (uint32_t)__popcll(bo);
+        nc += (uint32_t)__popcll(bn);
+      }
     }
+#if DQ_PS_PREFETCH
 #pragma unroll
     for (int j = 0; j < kVecPerThread; ++j) v[j] = vn[j];
+#else
+    if (nvs < end) {
+      if (nfull) load_sweep<true>(src4, nvs, end, v);
+      else load_sweep<false>(src4, nvs, end, v);
+    }
+#endif
     vs = nvs;
     full = nfull;
   }
