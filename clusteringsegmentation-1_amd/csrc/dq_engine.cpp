@@ -52,6 +52,7 @@ Engine::Engine(int device) : device_(device) {
   if (const char* v = getenv("DQ_HIP_TILES")) tiles_target_ = std::max(64, atoi(v));
   if (const char* v = getenv("DQ_HIP_TILE_MAX"))
     tile_max_ = (uint32_t)std::max<int>(kSweep, std::min<int>((int)kMaxTilePx, atoi(v))) / kSweep * kSweep;
+  if (const char* v = getenv("DQ_HIP_LDS_MAP")) use_lds_map_ = v[0] != '0';
   const char* la = getenv("DQ_HIP_LOOKAHEAD");
   if (la && la[0]) lookahead_ = std::max(0, std::min(8, atoi(la)));
   DQ_HIP(hipSetDevice(device_));
@@ -869,9 +870,15 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
   if ((size_t)chunk > cap_cells_) {
     if (d_cell_rec_) DQ_HIP(hipFree(d_cell_rec_));
     if (d_cell_idx_) DQ_HIP(hipFree(d_cell_idx_));
+    if (d_cell_c32_) DQ_HIP(hipFree(d_cell_c32_));
     DQ_HIP(hipMalloc((void**)&d_cell_rec_, (size_t)chunk * kCells * kCellRecWords * sizeof(uint32_t)));
     DQ_HIP(hipMalloc((void**)&d_cell_idx_, (size_t)chunk * kCells * kCellCap * sizeof(uint16_t)));
+    DQ_HIP(hipMalloc((void**)&d_cell_c32_, (size_t)chunk * kCells * sizeof(uint32_t)));
     cap_cells_ = chunk;
+  }
+  if (num_cus_ == 0) {
+    DQ_HIP(hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_));
+    num_cus_ = std::max(1, num_cus_);
   }
   for (int c0 = 0; c0 < njobs; c0 += chunk) {
     const int nt = std::min(chunk, njobs - c0);
@@ -882,6 +889,13 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     int kmax = 1;
     uint32_t nblocks = 0;
     std::vector<int> staged;   // tasks whose in/out needed aligned staging
+    double ntot = 0;
+    for (int t = 0; t < nt; ++t) {
+      ntot += jobs[c0 + t].n;
+      kmax = std::max(kmax, jobs[c0 + t].k);
+    }
+    // K <= 1024: the LDS-table map, one workgroup per CU over all tasks
+    const bool lds_map = kmax <= 1024 && use_lds_map_;
     for (int t = 0; t < nt; ++t) {
       const MapJob& j = jobs[c0 + t];
       uint32_t* hb = hblk0 + (size_t)t * kMapBlockWords;
@@ -895,13 +909,18 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       m.lut = reinterpret_cast<const uint16_t*>(db + kMapPal);
       m.cell_rec = d_cell_rec_ + (size_t)t * kCells * kCellRecWords;
       m.cell_idx = d_cell_idx_ + (size_t)t * kCells * kCellCap;
+      m.cell_c32 = d_cell_c32_ + (size_t)t * kCells;
       m.n = j.n;
       m.k = j.k;
-      m.grp_per_block = map_groups_per_block(j.n);
-      m.block_begin = nblocks;
       const uint32_t groups = j.n / 8;
+      if (lds_map) {
+        const uint32_t want = std::max<uint32_t>(1, (uint32_t)std::lround(num_cus_ * (double)j.n / ntot));
+        m.grp_per_block = std::max<uint32_t>(1, (groups + want - 1) / want);
+      } else {
+        m.grp_per_block = map_groups_per_block(j.n);
+      }
+      m.block_begin = nblocks;
       nblocks += std::max<uint32_t>(1, (groups + m.grp_per_block - 1) / m.grp_per_block);
-      kmax = std::max(kmax, j.k);
     }
     // misaligned in/out (the kernel uses 16-B accesses): aligned staging, one
     // task at a time through a private buffer
@@ -923,7 +942,8 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       double px = 0;
       for (int t = 0; t < nt; ++t) px += ht[t].n;
       timed_begin(stream);
-      launch_map(dt, nt, kmax, nblocks, stream);
+      if (lds_map) launch_map_lds(dt, nt, kmax, nblocks, stream);
+      else launch_map(dt, nt, kmax, nblocks, stream);
       timed_end(ST_MAP, 8.0 * px, stream);
     } else {
       // rare path: run the chunk task by task, staging misaligned buffers
@@ -938,8 +958,10 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
           one.out = d_map_align_ + want;
         }
         one.block_begin = 0;
+        one.grp_per_block = map_groups_per_block(j.n);
         one.cell_rec = d_cell_rec_;
         one.cell_idx = d_cell_idx_;
+        one.cell_c32 = d_cell_c32_;
         DQ_HIP(hipStreamSynchronize(stream));   // staging slot 0 reuse
         ht[0] = one;
         if (t != 0) std::memcpy(hblk0, hblk0 + (size_t)t * kMapBlockWords, kMapBlockWords * 4);

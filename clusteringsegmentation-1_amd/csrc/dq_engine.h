@@ -232,6 +232,9 @@ class Engine {
   double tr_wait_us_ = 0, tr_build_us_ = 0, tr_replay_us_ = 0;
 
   // map tables
+  uint32_t* d_cell_c32_ = nullptr;    // compact records per map task of a chunk
+  int num_cus_ = 0;
+  bool use_lds_map_ = true;           // DQ_HIP_LDS_MAP=0: the L2-gather map kernel
   uint32_t* d_cell_rec_ = nullptr;    // per map task of a chunk
   size_t cap_cells_ = 0;
   uint16_t* d_cell_idx_ = nullptr;

@@ -68,6 +68,7 @@ struct alignas(16) MapTask {
   const uint16_t* lut;      // 766 start entries (lut_init)
   uint32_t* cell_rec;       // kCells x 16 B candidate records
   uint16_t* cell_idx;       // kCells x kCellCap overflow lists
+  uint32_t* cell_c32;       // kCells compact records (K <= 1024, LDS-resident in the map)
   uint32_t n;
   int32_t k;
   uint32_t block_begin;     // first map workgroup of this task
@@ -81,5 +82,10 @@ struct alignas(16) MapTask {
 void launch_build_cells(const MapTask* tasks, int ntasks, int kmax, hipStream_t stream);
 uint32_t map_groups_per_block(uint32_t n);
 void launch_map(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream);
+// K <= 1024: the same map with the compact cell table staged in LDS (one
+// 1024-thread workgroup per CU); map_lds_blocks gives each task's share of
+// the grid (block_begin / grp_per_block set by the caller from it).
+constexpr int kMapLdsBlock = 1024;
+void launch_map_lds(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream);
 
 }  // namespace dq

@@ -768,23 +768,32 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
   }
 }
 
-// Map, step 1: per colour cell (8x8x8 values), the palette entries whose
-// minimum distance to the cell does not exceed the smallest maximum distance
-// of any entry to the cell.  Every exact argmin for a colour of the cell is
-// among them (ties included: <=).  grid = (kCells / kCellsPerBlock, tasks):
-// the task's palette is staged in LDS once per workgroup; one WAVE per cell at
-// a time (lanes stride the palette, a wave min gives the bound, ballots
-// compact the candidates in palette order).
-// Record (16 B): x[15:0] count c; x[31:16], y, z, w: the first kCellInline
-// candidates' sorted indices (u16), unused slots = k (a sentinel entry that is
-// farther than any real one); c > kCellInline: all c indices in
-// cell_idx[cell*kCellCap ...]; c == kCellBrute: scan the whole palette.
+// Map, step 1: per colour cell (8x8x8 values), the palette entries that can
+// be the nearest entry of some colour of the cell.  Two exact filters:
+//   (a) min distance of e to the cell <= the smallest max distance of any
+//       entry to the cell (else some entry is closer for every colour);
+//   (b) pairwise dominance: e is dropped when ONE other candidate f is
+//       strictly closer than e for every colour x of the cell, i.e.
+//       2 (e - f).x < |e|^2 - |f|^2 at the cell corner maximising (e - f).x
+//       (strict: an entry that can tie is kept -- ties are broken by the MPS
+//       rank in the map).
+// Every exact argmin for a colour of the cell survives both, so the map's
+// answer is unchanged.  grid = (kCells / kCellsPerBlock, tasks): the task's
+// palette is staged in LDS once per workgroup; one WAVE per cell at a time.
+// Outputs per cell (surviving candidates in palette order):
+//   16-B record: x[15:0] count c; x[31:16], y, z, w: the first kCellInline
+//     indices (u16), unused slots = k (a sentinel farther than any entry);
+//     c > kCellInline: all c indices in cell_idx[cell*kCellCap ...];
+//     c == kCellBrute: scan the whole palette;
+//   compact 32-bit record (K <= 1024): 1..3 candidates inline (10-bit
+//     indices, unused slots repeat the first), else (count << 16 | cell)
+//     with bits 31:30 = 0 (count 63: whole palette).
 constexpr int kCellsPerBlock = 16;
 __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __restrict__ tasks) {
   const MapTask tk = tasks[blockIdx.y];
   const int k = tk.k;
   extern __shared__ uint32_t spal_c[];   // k colours
-  __shared__ uint16_t srec[kBlock / 64][8];
+  __shared__ uint16_t scand[kBlock / 64][kCellCap];
   for (int i = threadIdx.x; i < k; i += kBlock) spal_c[i] = as_g(tk.pal)[i];
   __syncthreads();
   const uint32_t lane = lane_id(), w = wave_id();
@@ -808,8 +817,7 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) bound = min(bound, __shfl_xor(bound, o, 64));
-    if (lane < 8) srec[w][lane] = (uint16_t)k;
-    uint16_t* lst = tk.cell_idx + (size_t)cell * kCellCap;
+    // (a): candidates in palette order (the first kCellCap kept in LDS)
     uint32_t count = 0;
     for (int base = 0; base < k; base += 64) {
       const int e = base + (int)lane;
@@ -821,20 +829,64 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
       }
       const uint64_t m = __ballot(cand);
       const uint32_t pos = count + mbcnt64(m);
-      if (cand && pos < (uint32_t)kCellCap) lst[pos] = (uint16_t)e;
-      if (cand && pos < (uint32_t)kCellInline) srec[w][1 + pos] = (uint16_t)e;
+      if (cand && pos < (uint32_t)kCellCap) scand[w][pos] = (uint16_t)e;
       count += (uint32_t)__popcll(m);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (b): pairwise dominance among them (lane i tests candidate i)
+    uint32_t fcount = count;
+    if (count <= (uint32_t)kCellCap && count > 1) {
+      bool keep = false;
+      uint32_t ei = 0;
+      if (lane < count) {
+        ei = scand[w][lane];
+        const uint32_t qe = spal_c[ei];
+        const int e0 = (qe >> 16) & 0xFF, e1 = (qe >> 8) & 0xFF, e2 = qe & 0xFF;
+        const int ee = e0 * e0 + e1 * e1 + e2 * e2;
+        keep = true;
+        for (uint32_t j = 0; j < count; ++j) {
+          if (j == lane) continue;
+          const uint32_t qf = spal_c[scand[w][j]];
+          const int f0 = (qf >> 16) & 0xFF, f1 = (qf >> 8) & 0xFF, f2 = qf & 0xFF;
+          const int d0 = e0 - f0, d1 = e1 - f1, d2 = e2 - f2;
+          const int dx = d0 * (d0 > 0 ? hi0 : lo0) + d1 * (d1 > 0 ? hi1 : lo1) + d2 * (d2 > 0 ? hi2 : lo2);
+          if (2 * dx < ee - (f0 * f0 + f1 * f1 + f2 * f2)) { keep = false; break; }
+        }
+      }
+      const uint64_t km = __ballot(keep);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (keep) scand[w][mbcnt64(km)] = (uint16_t)ei;
+      fcount = (uint32_t)__popcll(km);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const bool brute = count > (uint32_t)kCellCap;
+    if (!brute && lane < fcount) tk.cell_idx[(size_t)cell * kCellCap + lane] = scand[w][lane];
     if (lane == 0) {
-      const uint32_t c = count > (uint32_t)kCellCap ? kCellBrute : count;
+      const uint32_t c = brute ? kCellBrute : fcount;
+      uint32_t slot[kCellInline];
+#pragma unroll
+      for (int i = 0; i < kCellInline; ++i) slot[i] = (!brute && (uint32_t)i < fcount) ? scand[w][i] : (uint32_t)k;
       uint4 r;
-      r.x = c | ((uint32_t)srec[w][1] << 16);
-      r.y = srec[w][2] | ((uint32_t)srec[w][3] << 16);
-      r.z = srec[w][4] | ((uint32_t)srec[w][5] << 16);
-      r.w = srec[w][6] | ((uint32_t)srec[w][7] << 16);
+      r.x = c | (slot[0] << 16);
+      r.y = slot[1] | (slot[2] << 16);
+      r.z = slot[3] | (slot[4] << 16);
+      r.w = slot[5] | (slot[6] << 16);
       reinterpret_cast<uint4*>(tk.cell_rec)[cell] = r;
+      uint32_t c32;
+      if (!brute && fcount >= 1 && fcount <= 3) {
+        const uint32_t j0 = slot[0];
+        const uint32_t j1 = fcount > 1 ? slot[1] : j0;
+        const uint32_t j2 = fcount > 2 ? slot[2] : j0;
+        c32 = (fcount << 30) | j0 | (j1 << 10) | (j2 << 20);
+      } else {
+        c32 = ((brute ? 63u : fcount) << 16) | cell;
+      }
+      if (tk.cell_c32) tk.cell_c32[cell] = c32;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -981,6 +1033,164 @@ __global__ __launch_bounds__(kBlock) void map_kernel(const MapTask* __restrict__
   }
 }
 
+// Map with the compact cell table in LDS (K <= 1024): one workgroup of
+// kMapLdsBlock threads per CU stages its task's 32768 compact records
+// (128 KB), the sorted palette and the start LUT, then maps its share of the
+// task's pixels, 8 per lane per iteration.  The 1-3 inline candidates of a
+// cell are evaluated branch-free.  Pixels of cells with more candidates are
+// queued in LDS (per wave, in slot order) and resolved cooperatively: lane i
+// takes queue entry i and scans that cell's list (one 16-B load for the
+// first 8 indices); the results return through the queue.  Queue overflow
+// (more than 64 such pixels in one wave-iteration) falls back to a per-lane
+// loop.  Same keys and the same answer as map_kernel.
+constexpr int kMapQ = 64;
+__global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __restrict__ tasks,
+                                                              int ntasks) {
+  int ti = 0;
+  while (ti + 1 < ntasks && tasks[ti + 1].block_begin <= blockIdx.x) ++ti;
+  const MapTask tk = tasks[ti];
+  const uint32_t n = tk.n;
+  const int k = tk.k;
+  extern __shared__ uint32_t smem[];
+  uint32_t* stab = smem;                                      // kCells compact records
+  uint32_t* squeue = smem + kCells;                           // per wave: kMapQ pixels / results
+  uint2* spal = reinterpret_cast<uint2*>(squeue + (kMapLdsBlock / 64) * kMapQ);   // k+1
+  uint16_t* slut = reinterpret_cast<uint16_t*>(reinterpret_cast<uint32_t*>(spal) + 2 * (k + 1));
+  typedef const __attribute__((address_space(1))) uint16_t g_cu16;
+  {
+    g_cu4* t4 = (g_cu4*)tk.cell_c32;
+    u32x4* s4 = reinterpret_cast<u32x4*>(stab);
+#pragma unroll 4
+    for (int i = threadIdx.x; i < kCells / 4; i += kMapLdsBlock) s4[i] = t4[i];
+    g_cu32* gpal = as_g(tk.pal);
+    for (int i = threadIdx.x; i <= k; i += kMapLdsBlock) {
+      const uint32_t q = i < k ? gpal[i] : 0u;
+      const uint32_t c2 = i < k ? __builtin_amdgcn_udot4(q, q, 0u, false) + (1u << 19) : 0xFFFFFu;
+      spal[i] = make_uint2(q, c2);
+    }
+    g_cu16* glut = (g_cu16*)tk.lut;
+    for (int i = threadIdx.x; i < 766; i += kMapLdsBlock) slut[i] = glut[i];
+  }
+  __syncthreads();
+  const uint32_t lane = lane_id();
+  uint32_t* wq = squeue + wave_id() * kMapQ;
+  g_cu4* gidx4 = (g_cu4*)tk.cell_idx;
+  g_cu16* gidx = (g_cu16*)tk.cell_idx;
+  g_cu4* in4 = (g_cu4*)tk.in;
+  typedef __attribute__((address_space(1))) u32x4 g_u4;
+  g_u4* out4 = (g_u4*)as_gw(tk.out);
+
+  auto key = [&](uint32_t p, uint32_t S, uint32_t j) -> uint32_t {
+    const uint2 en = spal[j];
+    const uint32_t d = (uint32_t)((int32_t)en.y - 2 * (int32_t)__builtin_amdgcn_udot4(p, en.x, 0u, false));
+    const uint32_t sad = __builtin_amdgcn_sad_u16(4u * j, S, 0u);
+    return (d << 12) | sad;
+  };
+  auto answer = [&](uint32_t S, uint32_t best) -> uint32_t {
+    return spal[entry_from_sad<false>(S, best & 0xFFFu)].x;
+  };
+  auto cell_of = [](uint32_t p) -> uint32_t {
+    return ((p >> (24 - kCellBits)) << (2 * kCellBits)) |
+           (((p >> (16 - kCellBits)) & ((1u << kCellBits) - 1)) << kCellBits) |
+           ((p >> (8 - kCellBits)) & ((1u << kCellBits) - 1));
+  };
+  auto start_of = [&](uint32_t p) -> uint32_t {
+    return 4u * slut[((p >> 16) & 0xFF) + ((p >> 8) & 0xFF) + (p & 0xFF)] + 1u;
+  };
+  // the exact answer for a pixel of an overflow cell (record r)
+  auto resolve = [&](uint32_t p, uint32_t S, uint32_t r) -> uint32_t {
+    const uint32_t cnt = (r >> 16) & 0x3Fu;
+    uint32_t best = 0xFFFFFFFFu;
+    if (cnt == 63u) {
+      for (int j = 0; j < k; ++j) best = min(best, key(p, S, (uint32_t)j));
+    } else {
+      const uint32_t row = (r & 0xFFFFu) * (kCellCap / 8);   // 8 u16 per 16 B
+      const u32x4 f8 = gidx4[row];
+      const uint32_t l8[8] = {f8[0] & 0xFFFFu, f8[0] >> 16, f8[1] & 0xFFFFu, f8[1] >> 16,
+                              f8[2] & 0xFFFFu, f8[2] >> 16, f8[3] & 0xFFFFu, f8[3] >> 16};
+#pragma unroll
+      for (uint32_t m = 0; m < 8; ++m)
+        if (m < cnt) best = min(best, key(p, S, l8[m]));
+      for (uint32_t m = 8; m < cnt; ++m) best = min(best, key(p, S, gidx[(r & 0xFFFFu) * kCellCap + m]));
+    }
+    return answer(S, best);
+  };
+
+  const uint32_t ngrp = n / kMapPx;
+  const uint32_t lb = blockIdx.x - tk.block_begin;
+  const uint32_t g0 = lb * tk.grp_per_block;
+  const uint32_t g1 = min(ngrp, g0 + tk.grp_per_block);
+  for (uint32_t gb = g0; gb < g1; gb += kMapLdsBlock) {
+    const uint32_t g = gb + threadIdx.x;
+    const bool have = g < g1;
+    uint32_t px[kMapPx];
+    {
+      const u32x4 a = have ? in4[2 * g] : (u32x4){0u, 0u, 0u, 0u};
+      const u32x4 b = have ? in4[2 * g + 1] : (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { px[e] = a[e] & 0xFFFFFFu; px[4 + e] = b[e] & 0xFFFFFFu; }
+    }
+    uint32_t res[kMapPx], rec[kMapPx], Ss[kMapPx];
+#pragma unroll
+    for (int e = 0; e < kMapPx; ++e) {
+      rec[e] = stab[cell_of(px[e])];
+      Ss[e] = start_of(px[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < kMapPx; ++e) {
+      const uint32_t p = px[e], S = Ss[e], r = rec[e];
+      uint32_t best = key(p, S, r & 0x3FFu);
+      best = min(best, key(p, S, (r >> 10) & 0x3FFu));
+      best = min(best, key(p, S, (r >> 20) & 0x3FFu));
+      res[e] = answer(S, best);
+    }
+    // overflow cells: queue (slot order), resolve cooperatively, read back
+    uint32_t qpos[kMapPx];
+    uint32_t qn = 0;
+#pragma unroll
+    for (int e = 0; e < kMapPx; ++e) {
+      const bool ov = have && (rec[e] >> 30) == 0;
+      const uint64_t m = __ballot(ov);
+      const uint32_t pos = qn + mbcnt64(m);
+      qpos[e] = ov ? pos : 0xFFFFFFFFu;
+      if (ov && pos < (uint32_t)kMapQ) wq[pos] = px[e];
+      qn += (uint32_t)__popcll(m);
+    }
+    if (qn > 0) {   // wave-uniform
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane < min(qn, (uint32_t)kMapQ)) {
+        const uint32_t p = wq[lane];
+        wq[lane] = resolve(p, start_of(p), stab[cell_of(p)]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int e = 0; e < kMapPx; ++e) {
+        if (qpos[e] < (uint32_t)kMapQ) res[e] = wq[qpos[e]];
+        else if (qpos[e] != 0xFFFFFFFFu) res[e] = resolve(px[e], Ss[e], rec[e]);   // queue full
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (have) {
+      out4[2 * g] = (u32x4){res[0], res[1], res[2], res[3]};
+      out4[2 * g + 1] = (u32x4){res[4], res[5], res[6], res[7]};
+    }
+  }
+  // tail (n % kMapPx points): the task's first workgroup, whole palette
+  const uint32_t t = ngrp * kMapPx + threadIdx.x;
+  if (lb == 0 && t < n) {
+    const uint32_t p = as_g(tk.in)[t] & 0xFFFFFFu;
+    const uint32_t S = start_of(p);
+    uint32_t best = 0xFFFFFFFFu;
+    for (int j = 0; j < k; ++j) best = min(best, key(p, S, (uint32_t)j));
+    as_gw(tk.out)[t] = answer(S, best);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Launchers.
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) {
@@ -1042,6 +1252,19 @@ uint32_t map_groups_per_block(uint32_t n) {
   // ~8 groups of kMapPx pixels per lane per workgroup: 16K pixels
   (void)n;
   return 8u * kBlock;
+}
+
+void launch_map_lds(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream) {
+  if (ntasks <= 0 || nblocks == 0) return;
+  const size_t lds = (size_t)kCells * 4 + (size_t)(kMapLdsBlock / 64) * kMapQ * 4 +
+                     (size_t)(kmax + 1) * 8 + 768 * 2;
+  static bool attr = false;
+  if (!attr) {   // more than 64 KB of dynamic LDS
+    (void)hipFuncSetAttribute((const void*)map_lds_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  map_lds_kernel<<<dim3(nblocks), dim3(kMapLdsBlock), lds, stream>>>(tasks, ntasks);
 }
 
 void launch_map(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream) {

@@ -67,7 +67,7 @@ def test_epilogue_fma_only_in_divisions(kernels, tmp_path):
 
 
 def test_streaming_kernels_use_global_memory(kernels):
-    for part in ("pass_kernel", "partsplit_kernel", "map_kernel"):
+    for part in ("pass_kernel", "partsplit_kernel", "map_kernel", "map_lds_kernel"):
         for name, body in _named(kernels, part).items():
             assert not re.search(r"\bflat_(load|store)", body), name
             assert re.search(r"global_load_dwordx4", body), name

@@ -270,3 +270,28 @@ def test_batch_over_lanes(gpu):
         assert np.array_equal(t.cpu().numpy().view(np.uint32), orc_out)
     ref_trace = _oracle_cluster(frames[-1], 64)[3]
     assert np.array_equal(gpu.last_trace(64), ref_trace)
+
+
+@pytest.mark.parametrize("kind", ["cluster1024", "cluster256", "line512", "uniform1024"])
+def test_map_dense_palettes(gpu, kind):
+    """Palettes whose cells have many candidates (a tight cluster of entries:
+    most cells overflow the inline slots or need the whole palette), against
+    the oracle's literal map_colors_mps walk.  Exercises the map's overflow
+    queue and its queue-full fallback."""
+    rng = np.random.default_rng({"cluster1024": 1, "cluster256": 2, "line512": 3, "uniform1024": 4}[kind])
+    if kind.startswith("cluster"):
+        k = int(kind[7:])
+        c = rng.integers(100, 116, (k, 3))
+    elif kind == "line512":
+        k = 512
+        t = rng.integers(0, 256, k)
+        c = np.stack([t, (t * 3) % 256, 255 - t], 1)
+    else:
+        k = 1024
+        c = rng.integers(0, 256, (k, 3))
+    pal = ((c[:, 0] << 16) | (c[:, 1] << 8) | c[:, 2]).astype(np.uint32)
+    px = fx.xorshift(300007, seed=77)
+    out = gpu.map_colors_mps(px, pal)
+    ref = np.zeros_like(px)
+    fx.oracle().dqo_map(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(ref), fx.vp(pal), ctypes.c_int(k))
+    assert np.array_equal(out, ref)
