@@ -772,14 +772,14 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
 // be the nearest entry of some colour of the cell.  Two exact filters:
 //   (a) min distance of e to the cell <= the smallest max distance of any
 //       entry to the cell (else some entry is closer for every colour);
-//   (b) pairwise dominance: e is dropped when ONE other candidate f is
-//       strictly closer than e for every colour x of the cell, i.e.
-//       2 (e - f).x < |e|^2 - |f|^2 at the cell corner maximising (e - f).x
-//       (strict: an entry that can tie is kept -- ties are broken by the MPS
-//       rank in the map).
+//   (b) dominance: e is dropped when ONE other candidate f (one of the 4
+//       with the smallest max distance) is strictly closer than e for every
+//       colour x of the cell, i.e. 2 (e - f).x < |e|^2 - |f|^2 at the cell
+//       corner maximising (e - f).x (strict: an entry that can tie is kept
+//       -- ties are broken by the MPS rank in the map).
 // Every exact argmin for a colour of the cell survives both, so the map's
-// answer is unchanged.  grid = (kCells / kCellsPerBlock, tasks): the task's
-// palette is staged in LDS once per workgroup; one WAVE per cell at a time.
+// answer is unchanged.  grid = (kCells / kBlock, tasks): the task's palette
+// is staged in LDS once per workgroup.
 // Outputs per cell (surviving candidates in palette order):
 //   16-B record: x[15:0] count c; x[31:16], y, z, w: the first kCellInline
 //     indices (u16), unused slots = k (a sentinel farther than any entry);
@@ -788,109 +788,114 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
 //   compact 32-bit record (K <= 1024): 1..3 candidates inline (10-bit
 //     indices, unused slots repeat the first), else (count << 16 | cell)
 //     with bits 31:30 = 0 (count 63: whole palette).
-constexpr int kCellsPerBlock = 16;
+// One LANE per cell (grid.x = kCells / kBlock): every lane of a wave reads
+// the same palette entry at the same time (LDS broadcast); each lane keeps
+// its loose candidate list in a transposed LDS array.
 __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __restrict__ tasks) {
   const MapTask tk = tasks[blockIdx.y];
   const int k = tk.k;
   extern __shared__ uint32_t spal_c[];   // k colours
-  __shared__ uint16_t scand[kBlock / 64][kCellCap];
+  __shared__ uint32_t scand[kCellCap * kBlock];   // [i][thread]
   for (int i = threadIdx.x; i < k; i += kBlock) spal_c[i] = as_g(tk.pal)[i];
   __syncthreads();
-  const uint32_t lane = lane_id(), w = wave_id();
+  const uint32_t tid = threadIdx.x;
+  const uint32_t cell = blockIdx.x * kBlock + tid;
   const int cw = 1 << (8 - kCellBits);
+  const int lo0 = (int)(cell >> (2 * kCellBits)) * cw;
+  const int lo1 = (int)((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
+  const int lo2 = (int)(cell & ((1 << kCellBits) - 1)) * cw;
+  const int hi0 = lo0 + cw - 1, hi1 = lo1 + cw - 1, hi2 = lo2 + cw - 1;
   auto far2 = [](int v, int lo, int hi) { const int x = max(v - lo, hi - v); return x * x; };
   auto near2 = [](int v, int lo, int hi) {
-    const int x = v < lo ? lo - v : (v > hi ? v - hi : 0);
+    const int x = max(max(lo - v, v - hi), 0);
     return x * x;
   };
-  for (int ci = (int)w; ci < kCellsPerBlock; ci += kBlock / 64) {
-    const uint32_t cell = blockIdx.x * kCellsPerBlock + ci;   // grid.x = kCells / kCellsPerBlock
-    const int lo0 = (int)(cell >> (2 * kCellBits)) * cw;
-    const int lo1 = (int)((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
-    const int lo2 = (int)(cell & ((1 << kCellBits) - 1)) * cw;
-    const int hi0 = lo0 + cw - 1, hi1 = lo1 + cw - 1, hi2 = lo2 + cw - 1;
-    int bound = 0x7FFFFFFF;
-    for (int e = (int)lane; e < k; e += 64) {
-      const uint32_t q = spal_c[e];
-      bound = min(bound, far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) +
-                             far2(q & 0xFF, lo2, hi2));
-    }
+  int bound = 0x7FFFFFFF;
+#pragma unroll 8
+  for (int e = 0; e < k; ++e) {
+    const uint32_t q = spal_c[e];
+    bound = min(bound, far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) +
+                           far2(q & 0xFF, lo2, hi2));
+  }
+  // (a) loose candidates, palette order
+  uint32_t count = 0;
+#pragma unroll 8
+  for (int e = 0; e < k; ++e) {
+    const uint32_t q = spal_c[e];
+    const bool cand = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
+                          near2(q & 0xFF, lo2, hi2) <= bound;
+    if (cand && count < (uint32_t)kCellCap) scand[count * kBlock + tid] = (uint32_t)e;
+    count += cand ? 1u : 0u;
+  }
+  // (b) dominance by the 4 candidates with the smallest max distance (as
+  //     tight as all pairs on the measured palettes, O(4c) instead of c^2),
+  //     compacted in place (order kept)
+  const bool brute = count > (uint32_t)kCellCap;
+  uint32_t fcount = brute ? 0u : count;
+  if (!brute && count > 1) {
+    constexpr int kRefs = 4;
+    int rf[kRefs] = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
+    uint32_t rq[kRefs] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < count; ++i) {   // the 4 smallest (far2, colour)
+      const uint32_t q = spal_c[scand[i * kBlock + tid]];
+      int f = far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) + far2(q & 0xFF, lo2, hi2);
+      uint32_t c = q;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) bound = min(bound, __shfl_xor(bound, o, 64));
-    // (a): candidates in palette order (the first kCellCap kept in LDS)
-    uint32_t count = 0;
-    for (int base = 0; base < k; base += 64) {
-      const int e = base + (int)lane;
-      bool cand = false;
-      if (e < k) {
-        const uint32_t q = spal_c[e];
-        cand = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
-                   near2(q & 0xFF, lo2, hi2) <= bound;
-      }
-      const uint64_t m = __ballot(cand);
-      const uint32_t pos = count + mbcnt64(m);
-      if (cand && pos < (uint32_t)kCellCap) scand[w][pos] = (uint16_t)e;
-      count += (uint32_t)__popcll(m);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // (b): pairwise dominance among them (lane i tests candidate i)
-    uint32_t fcount = count;
-    if (count <= (uint32_t)kCellCap && count > 1) {
-      bool keep = false;
-      uint32_t ei = 0;
-      if (lane < count) {
-        ei = scand[w][lane];
-        const uint32_t qe = spal_c[ei];
-        const int e0 = (qe >> 16) & 0xFF, e1 = (qe >> 8) & 0xFF, e2 = qe & 0xFF;
-        const int ee = e0 * e0 + e1 * e1 + e2 * e2;
-        keep = true;
-        for (uint32_t j = 0; j < count; ++j) {
-          if (j == lane) continue;
-          const uint32_t qf = spal_c[scand[w][j]];
-          const int f0 = (qf >> 16) & 0xFF, f1 = (qf >> 8) & 0xFF, f2 = qf & 0xFF;
-          const int d0 = e0 - f0, d1 = e1 - f1, d2 = e2 - f2;
-          const int dx = d0 * (d0 > 0 ? hi0 : lo0) + d1 * (d1 > 0 ? hi1 : lo1) + d2 * (d2 > 0 ? hi2 : lo2);
-          if (2 * dx < ee - (f0 * f0 + f1 * f1 + f2 * f2)) { keep = false; break; }
+      for (int r = 0; r < kRefs; ++r) {
+        if (f < rf[r]) {
+          const int tf = rf[r];
+          const uint32_t tq = rq[r];
+          rf[r] = f;
+          rq[r] = c;
+          f = tf;
+          c = tq;
         }
       }
-      const uint64_t km = __ballot(keep);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (keep) scand[w][mbcnt64(km)] = (uint16_t)ei;
-      fcount = (uint32_t)__popcll(km);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    const bool brute = count > (uint32_t)kCellCap;
-    if (!brute && lane < fcount) tk.cell_idx[(size_t)cell * kCellCap + lane] = scand[w][lane];
-    if (lane == 0) {
-      const uint32_t c = brute ? kCellBrute : fcount;
-      uint32_t slot[kCellInline];
+    const int nref = (int)min(count, (uint32_t)kRefs);
+    uint32_t kept = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+      const uint32_t ei = scand[i * kBlock + tid];
+      const uint32_t qe = spal_c[ei];
+      const int e0 = (qe >> 16) & 0xFF, e1 = (qe >> 8) & 0xFF, e2 = qe & 0xFF;
+      const int ee = e0 * e0 + e1 * e1 + e2 * e2;
+      bool keep = true;
 #pragma unroll
-      for (int i = 0; i < kCellInline; ++i) slot[i] = (!brute && (uint32_t)i < fcount) ? scand[w][i] : (uint32_t)k;
-      uint4 r;
-      r.x = c | (slot[0] << 16);
-      r.y = slot[1] | (slot[2] << 16);
-      r.z = slot[3] | (slot[4] << 16);
-      r.w = slot[5] | (slot[6] << 16);
-      reinterpret_cast<uint4*>(tk.cell_rec)[cell] = r;
-      uint32_t c32;
-      if (!brute && fcount >= 1 && fcount <= 3) {
-        const uint32_t j0 = slot[0];
-        const uint32_t j1 = fcount > 1 ? slot[1] : j0;
-        const uint32_t j2 = fcount > 2 ? slot[2] : j0;
-        c32 = (fcount << 30) | j0 | (j1 << 10) | (j2 << 20);
-      } else {
-        c32 = ((brute ? 63u : fcount) << 16) | cell;
+      for (int r = 0; r < kRefs; ++r) {
+        if (r >= nref) break;
+        const uint32_t qf = rq[r];
+        const int f0 = (qf >> 16) & 0xFF, f1 = (qf >> 8) & 0xFF, f2 = qf & 0xFF;
+        const int d0 = e0 - f0, d1 = e1 - f1, d2 = e2 - f2;
+        const int dx = d0 * (d0 > 0 ? hi0 : lo0) + d1 * (d1 > 0 ? hi1 : lo1) + d2 * (d2 > 0 ? hi2 : lo2);
+        // (f == e: dx = 0 = rhs, never strict)
+        keep = keep && !(2 * dx < ee - (f0 * f0 + f1 * f1 + f2 * f2));
       }
-      if (tk.cell_c32) tk.cell_c32[cell] = c32;
+      if (keep) scand[(kept++) * kBlock + tid] = ei;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    fcount = kept;
   }
+  uint16_t* lst = tk.cell_idx + (size_t)cell * kCellCap;
+  for (uint32_t i = 0; i < fcount; ++i) lst[i] = (uint16_t)scand[i * kBlock + tid];
+  const uint32_t c = brute ? kCellBrute : fcount;
+  uint32_t slot[kCellInline];
+#pragma unroll
+  for (int i = 0; i < kCellInline; ++i) slot[i] = (uint32_t)i < fcount ? scand[i * kBlock + tid] : (uint32_t)k;
+  uint4 r;
+  r.x = c | (slot[0] << 16);
+  r.y = slot[1] | (slot[2] << 16);
+  r.z = slot[3] | (slot[4] << 16);
+  r.w = slot[5] | (slot[6] << 16);
+  reinterpret_cast<uint4*>(tk.cell_rec)[cell] = r;
+  uint32_t c32;
+  if (fcount >= 1 && fcount <= 3) {
+    const uint32_t j0 = slot[0];
+    const uint32_t j1 = fcount > 1 ? slot[1] : j0;
+    const uint32_t j2 = fcount > 2 ? slot[2] : j0;
+    c32 = (fcount << 30) | j0 | (j1 << 10) | (j2 << 20);
+  } else {
+    c32 = ((brute ? 63u : fcount) << 16) | cell;
+  }
+  if (tk.cell_c32) tk.cell_c32[cell] = c32;
 }
 
 // Map, step 2.  The answer is the entry minimising (squared distance, MPS
@@ -1242,9 +1247,15 @@ void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream) {
 }
 
 void launch_build_cells(const MapTask* tasks, int ntasks, int kmax, hipStream_t stream) {
-  static_assert(kCells % kCellsPerBlock == 0, "whole cells per workgroup");
+  static_assert(kCells % kBlock == 0, "whole cells per workgroup");
   if (ntasks <= 0) return;
-  build_cells_kernel<<<dim3(kCells / kCellsPerBlock, ntasks), dim3(kBlock), (size_t)kmax * 4,
+  static bool attr = false;
+  if (!attr) {   // palettes up to 16384 entries: up to 64 KB of dynamic LDS beside 32 KB static
+    (void)hipFuncSetAttribute((const void*)build_cells_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    attr = true;
+  }
+  build_cells_kernel<<<dim3(kCells / kBlock, ntasks), dim3(kBlock), (size_t)kmax * 4,
                        stream>>>(tasks);
 }
 
