@@ -50,6 +50,7 @@ Engine::Engine(int device) : device_(device) {
   const char* tr = getenv("DQ_HIP_TRACE");
   trace_ = tr && tr[0] == '1';
   if (const char* v = getenv("DQ_HIP_TILES")) tiles_target_ = std::max(64, atoi(v));
+  if (const char* v = getenv("DQ_HIP_NODE_TILES")) node_tiles_ = std::max(1, atoi(v));
   if (const char* v = getenv("DQ_HIP_TILE_MAX"))
     tile_max_ = (uint32_t)std::max<int>(kSweep, std::min<int>((int)kMaxTilePx, atoi(v))) / kSweep * kSweep;
   if (const char* v = getenv("DQ_HIP_LDS_MAP")) use_lds_map_ = v[0] != '0';
@@ -294,10 +295,20 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   uint64_t tl = (total + tiles_target_ - 1) / tiles_target_;
   tl = ((tl + kSweep - 1) / kSweep) * kSweep;
   tl = std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, tile_max_));
+  // per record: at least node_tiles_ tiles (a node still active late in a
+  // round is then swept by several workgroups, not one)
+  auto tile_len = [&](uint64_t len) -> uint64_t {
+    uint64_t t = (len + node_tiles_ - 1) / node_tiles_;
+    t = ((t + kSweep - 1) / kSweep) * kSweep;
+    return std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, t));
+  };
   size_t ntiles = 0, nt_own = 0;
   for (int a = 0; a < nl; ++a) {   // empty records get one empty tile (their epilogue still runs)
-    for (int sh = 0; sh < S; ++sh)
-      ntiles += std::max<size_t>(1, (nodes_[order[a]].len[sh] + tl - 1) / tl);
+    for (int sh = 0; sh < S; ++sh) {
+      const uint64_t len = nodes_[order[a]].len[sh];
+      const uint64_t tln = tile_len(len);
+      ntiles += std::max<size_t>(1, (len + tln - 1) / tln);
+    }
     if (a == n_own - 1) nt_own = ntiles;
   }
   size_t nptiles = 0;
@@ -371,11 +382,12 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       d.prm.thr = thr;
       d.prm.shift = shift;
       d.tile_begin = t;
-      for (uint64_t o = 0; o == 0 || o < n.len[sh]; o += tl) {
+      const uint64_t tln = tile_len(n.len[sh]);
+      for (uint64_t o = 0; o == 0 || o < n.len[sh]; o += tln) {
         Tile& tt = ht[t++];
         tt.node = a * S + sh;
         tt.start = n.off[sh] + (uint32_t)o;
-        tt.end = n.off[sh] + (uint32_t)std::min<uint64_t>(n.len[sh], o + tl);
+        tt.end = n.off[sh] + (uint32_t)std::min<uint64_t>(n.len[sh], o + tln);
       }
       d.tile_end = t;
     }

@@ -226,6 +226,7 @@ class Engine {
   uint64_t seq_ = 0;                  // round sequence number
   int lookahead_ = 1;                 // 2-means iterations queued past the one awaited
   int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TILES)
+  int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_NODE_TILES)
   uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TILE_MAX)
   // host-side trace (DQ_HIP_TRACE=1): per-run phase times on stderr
   bool trace_ = false;
