@@ -1021,7 +1021,7 @@ static std::atomic<int> g_lanes_override{0};
 int batch_lanes() {
   static int lanes = [] {
     const char* v = getenv("DQ_HIP_LANES");
-    return v && v[0] ? std::max(1, std::min(kMaxLanes, atoi(v))) : 3;
+    return v && v[0] ? std::max(1, std::min(kMaxLanes, atoi(v))) : 2;
   }();
   const int o = g_lanes_override.load();
   return o > 0 ? std::min(o, kMaxLanes) : lanes;

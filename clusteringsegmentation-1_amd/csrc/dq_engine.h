@@ -262,7 +262,7 @@ class Engine {
 // every call and holds the diagnostics; a batch of frames is split over
 // batch_lanes() lanes, each an engine with its own stream driven by its own
 // host thread, so one group's kernels fill the GPU while another group's host
-// replays its round (DQ_HIP_LANES, default 3: measured best for 8 4K frames).
+// replays its round (DQ_HIP_LANES, default 2: measured best for 8 4K frames, interleaved A/B).
 constexpr int kMaxLanes = 8;
 Engine& engine_for(int device, int lane = 0);
 int batch_lanes();

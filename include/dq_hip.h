@@ -99,7 +99,7 @@ uint64_t dq_hip_last_points_full(int device);
 void dq_hip_set_fixed_point(int device, int on);
 
 /* Engine lanes a batch of frames is split over (each: own stream, own host
- * thread; DQ_HIP_LANES, default 3).  lanes = 0 restores the default. */
+ * thread; DQ_HIP_LANES, default 2).  lanes = 0 restores the default. */
 void dq_hip_set_lanes(int lanes);
 int dq_hip_get_lanes(void);
 
