@@ -48,7 +48,8 @@ Engine::Engine(int device) : device_(device) {
   const char* full = getenv("DQ_HIP_FULL_ITERS");
   fixed_point_ = !(full && full[0] == '1');
   const char* tr = getenv("DQ_HIP_TRACE");
-  trace_ = tr && tr[0] == '1';
+  trace_ = tr && (tr[0] == '1' || tr[0] == '2');
+  trace_rounds_ = tr && tr[0] == '2';
   if (const char* v = getenv("DQ_HIP_TILES")) tiles_target_ = std::max(64, atoi(v));
   if (const char* v = getenv("DQ_HIP_NODE_TILES")) node_tiles_ = std::max(1, atoi(v));
   if (const char* v = getenv("DQ_HIP_TILE_MAX"))
@@ -284,11 +285,11 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   uint64_t total = 0, own_total = 0, parent_total = 0;   // local points
   for (int a = 0; a < nl; ++a)
     for (int sh = 0; sh < S; ++sh) {
-      total += nodes_[order[a]].len[sh];
-      if (a < n_own) own_total += nodes_[order[a]].len[sh];
+      total += seg(order[a], sh).len;
+      if (a < n_own) own_total += seg(order[a], sh).len;
     }
   for (int p : parents)
-    for (int sh = 0; sh < S; ++sh) parent_total += nodes_[p].len[sh];
+    for (int sh = 0; sh < S; ++sh) parent_total += seg(p, sh).len;
   // Tile length: whole 4096-point sweeps, about tiles_target_ tiles for big
   // rounds, at most tile_max_ points (a node still active late in a round is
   // swept by ceil(len / tl) workgroups only).
@@ -305,7 +306,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   size_t ntiles = 0, nt_own = 0;
   for (int a = 0; a < nl; ++a) {   // empty records get one empty tile (their epilogue still runs)
     for (int sh = 0; sh < S; ++sh) {
-      const uint64_t len = nodes_[order[a]].len[sh];
+      const uint64_t len = seg(order[a], sh).len;
       const uint64_t tln = tile_len(len);
       ntiles += std::max<size_t>(1, (len + tln - 1) / tln);
     }
@@ -313,7 +314,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   }
   size_t nptiles = 0;
   for (int p : parents)
-    for (int sh = 0; sh < S; ++sh) nptiles += nodes_[p].ntiles[sh];
+    for (int sh = 0; sh < S; ++sh) nptiles += seg(p, sh).ntiles;
 
   // the round's block: [DevNode nr | Tile ntiles | PartTile nptiles | LaunchCtr max_iters]
   auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
@@ -343,7 +344,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     for (size_t i = 0; i < parents.size(); ++i)
       for (int sh = 0; sh < S; ++sh) {
         pt_first[i * S + sh] = q;
-        q += nodes_[parents[i]].ntiles[sh];
+        q += seg(parents[i], sh).ntiles;
       }
   }
   int t = 0;
@@ -366,8 +367,9 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       DevNode& d = hn[a * S + sh];
       d.src = buf_ptr(n.buf, fs, sh);
       d.dst = (child_buf(n.buf) == BUF_P0 ? d_p0_ : d_p1_) + fs.base[sh];
-      d.off = n.off[sh];
-      d.len = n.len[sh];
+      const Seg& sg = seg(order[a], sh);
+      d.off = sg.off;
+      d.len = sg.len;
       d.s = fs.s;
       d.tw = n.w;
       d.split_pb = -1;
@@ -375,19 +377,19 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       if (a >= n_own) {
         const int pi = parent_pos_[n.parent];
         d.split_pb = pt_first[pi * S + sh];
-        d.split_pe = d.split_pb + nodes_[n.parent].ntiles[sh];
+        d.split_pe = d.split_pb + seg(n.parent, sh).ntiles;
         d.split_side = nodes_[n.parent].child_new == order[a] ? 1 : 0;
       }
       for (int c = 0; c < 3; ++c) { d.tm[c] = n.mean[c]; d.tv[c] = n.var[c]; }
       d.prm.thr = thr;
       d.prm.shift = shift;
       d.tile_begin = t;
-      const uint64_t tln = tile_len(n.len[sh]);
-      for (uint64_t o = 0; o == 0 || o < n.len[sh]; o += tln) {
+      const uint64_t tln = tile_len(sg.len);
+      for (uint64_t o = 0; o == 0 || o < sg.len; o += tln) {
         Tile& tt = ht[t++];
         tt.node = a * S + sh;
-        tt.start = n.off[sh] + (uint32_t)o;
-        tt.end = n.off[sh] + (uint32_t)std::min<uint64_t>(n.len[sh], o + tln);
+        tt.start = sg.off + (uint32_t)o;
+        tt.end = sg.off + (uint32_t)std::min<uint64_t>(sg.len, o + tln);
       }
       d.tile_end = t;
     }
@@ -403,20 +405,25 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
         thr[c] = sl >= 0 ? hn[sl * S].prm.thr : 256;   // 256: nothing counted
         shift[c] = sl >= 0 ? hn[sl * S].prm.shift : 0;
       }
-      for (int sh = 0; sh < S; ++sh)
-        for (int i = 0; i < pn.ntiles[sh]; ++i) {
+      for (int sh = 0; sh < S; ++sh) {
+        const Seg& ps = seg(p, sh);
+        for (int i = 0; i < ps.ntiles; ++i) {
           PartTile& pt = hp[q++];
-          pt.tile = pn.dtiles[sh] + i;
-          pt.parent = pn.dnode[sh];
+          pt.tile = ps.dtiles + i;
+          pt.parent = ps.dnode;
           pt.thr[0] = thr[0];
           pt.thr[1] = thr[1];
           pt.shift[0] = shift[0];
           pt.shift[1] = shift[1];
         }
+      }
     }
   }
+  const double tb1 = trace_ ? host_us() : 0.0;
   DQ_HIP(hipMemcpyAsync(dblk, h_stage_, bytes, hipMemcpyHostToDevice, stream));
-  if (trace_) tr_build_us_ += host_us() - tb0;
+  const double tb2 = trace_ ? host_us() : 0.0;
+  if (trace_) tr_build_us_ += tb2 - tb0;
+  const double tw0 = tr_wait_us_;
 
   const uint64_t seq = ++seq_;
   RoundArgs ra;
@@ -487,6 +494,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     DQ_CHECK(known < max_iters, "nodes still active after the last 2-means iteration");
   }
 
+  const double tp0 = trace_ ? host_us() : 0.0;
   // points actually swept: iteration `it` reads a node iff it is not final
   // before it (done_it <= 0: final at the last iteration, or it < done_it)
   auto swept_in = [&](int it) {
@@ -494,7 +502,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     for (int a = 0; a < nl; ++a) {
       const int di = h_res_[a * S].done_it;
       if (di <= 0 || it < di)
-        for (int sh = 0; sh < S; ++sh) px += nodes_[order[a]].len[sh];
+        for (int sh = 0; sh < S; ++sh) px += seg(order[a], sh).len;
     }
     return px;
   };
@@ -515,20 +523,9 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       for (int c = 0; c < 3; ++c) { nodes_[id].mean[c] = r.tm[c]; nodes_[id].var[c] = r.tv[c]; }
     }
     Node co, cn;
+    const int io = (int)nodes_.size();
     {
-      Node& p = nodes_[id];
-      for (int sh = 0; sh < S; ++sh) {
-        const DevNode& d = hn[a * S + sh];
-        p.dnode[sh] = dn + a * S + sh;
-        p.dtiles[sh] = dt + d.tile_begin;
-        p.ntiles[sh] = d.tile_end - d.tile_begin;
-        const uint32_t n_new = h_res_[a * S + sh].n_new_local;
-        const uint32_t n_old = p.len[sh] - n_new;
-        co.off[sh] = p.off[sh];
-        co.len[sh] = n_old;
-        cn.off[sh] = p.off[sh] + n_old;
-        cn.len[sh] = n_new;
-      }
+      const Node& p = nodes_[id];
       co.frame = cn.frame = p.frame;
       co.parent = cn.parent = id;
       co.w = r.ow;
@@ -545,13 +542,36 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       co.glen = p.glen - r.n_new;
       co.buf = cn.buf = child_buf(p.buf);
     }
-    const int io = (int)nodes_.size();
     nodes_.push_back(co);
     nodes_.push_back(cn);
+    segs_.resize((size_t)(io + 2) * S);
+    for (int sh = 0; sh < S; ++sh) {
+      const DevNode& d = hn[a * S + sh];
+      Seg& ps = seg(id, sh);
+      ps.dnode = dn + a * S + sh;
+      ps.dtiles = dt + d.tile_begin;
+      ps.ntiles = d.tile_end - d.tile_begin;
+      const uint32_t n_new = h_res_[a * S + sh].n_new_local;
+      const uint32_t n_old = ps.len - n_new;
+      Seg& so = seg(io, sh);
+      Seg& sn = seg(io + 1, sh);
+      so.off = ps.off;
+      so.len = n_old;
+      sn.off = ps.off + n_old;
+      sn.len = n_new;
+    }
     Node& pp = nodes_[id];
     pp.child_old = io;
     pp.child_new = io + 1;
     pp.expanded = true;
+  }
+  if (trace_rounds_) {
+    const double tp1 = host_us();
+    std::fprintf(stderr,
+                 "divquant-hip round: nodes=%d records=%d tiles=%zu parttiles=%zu upload=%zuB "
+                 "fill=%.1fus memcpy=%.1fus launch+wait=%.1fus (wait %.1f) post=%.1fus\n",
+                 nl, nr, ntiles, nptiles, bytes, tb1 - tb0, tb2 - tb1, tp0 - tb2,
+                 tr_wait_us_ - tw0, tp1 - tp0);
   }
 }
 
@@ -575,11 +595,18 @@ void Engine::replay(FrameState& f) {
     if (f.new_index == k - 1) { ++f.new_index; return; }     // :823-832
     // STEP 4 (:876-887): max TSE above DBL_MIN, lowest index among equals;
     // if none qualifies old_index stays (the old half is split again).
-    if (nodes_[co].tse > DBL_MIN) f.heap.push({{nodes_[co].tse, -f.old_index}, co});
-    if (nodes_[cn].tse > DBL_MIN) f.heap.push({{nodes_[cn].tse, -f.new_index}, cn});
-    while (!f.heap.empty() && f.leaf[-f.heap.top().first.second] != f.heap.top().second)
-      f.heap.pop();
-    if (!f.heap.empty()) f.old_index = -f.heap.top().first.second;
+    auto push = [&](double tse, int idx, int node) {
+      f.heap.push_back({{tse, -idx}, node});
+      std::push_heap(f.heap.begin(), f.heap.end());
+    };
+    if (nodes_[co].tse > DBL_MIN) push(nodes_[co].tse, f.old_index, co);
+    if (nodes_[cn].tse > DBL_MIN) push(nodes_[cn].tse, f.new_index, cn);
+    // drop stale entries (a leaf index now holding another node)
+    while (!f.heap.empty() && f.leaf[-f.heap.front().first.second] != f.heap.front().second) {
+      std::pop_heap(f.heap.begin(), f.heap.end());
+      f.heap.pop_back();
+    }
+    if (!f.heap.empty()) f.old_index = -f.heap.front().first.second;
     ++f.new_index;
   }
 }
@@ -589,18 +616,19 @@ void Engine::replay(FrameState& f) {
 // leaf outside the current top r can never be picked in the remaining splits.
 void Engine::next_active(FrameState& f, std::vector<int>* active) {
   if (f.need < 0) return;
-  const int r = f.job->k - f.new_index;
+  const size_t r = (size_t)(f.job->k - f.new_index);
   active->push_back(f.need);
-  auto h = f.heap;
-  int taken = 0;
-  while (!h.empty() && taken < r) {
-    const auto top = h.top();
-    h.pop();
-    const int idx = -top.first.second, node = top.second;
-    if (f.leaf[idx] != node) continue;
-    ++taken;
-    if (!nodes_[node].expanded && node != f.need) active->push_back(node);
+  // the valid leaves of the greedy order, then its top r (keys are unique)
+  top_.clear();
+  for (const auto& e : f.heap)
+    if (f.leaf[-e.first.second] == e.second) top_.push_back(e);
+  if (top_.size() > r) {
+    std::nth_element(top_.begin(), top_.begin() + r, top_.end(),
+                     [](const HeapEnt& a, const HeapEnt& b) { return b < a; });
+    top_.resize(r);
   }
+  for (const auto& e : top_)
+    if (!nodes_[e.second].expanded && e.second != f.need) active->push_back(e.second);
 }
 
 // Final centres (:1029-1094): round, pack, drop empty clusters.
@@ -647,6 +675,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
 
   frames_.assign(nframes, FrameState());
   nodes_.clear();
+  segs_.clear();
   arena_chunk_ = 0;   // the previous run's tables are dead (its launches were drained)
   arena_used_ = 0;
   last_rounds = 0;
@@ -706,6 +735,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     // get_double_scale (DivQuantMapColors.cpp:205-220), on the whole frame
     f.s = 1.0 / (std::ceil(1 / 1.0) * std::ceil((double)ng / 1.0));
     Node root;
+    Seg root_seg[kMaxShard];
     root.frame = i;
     root.w = 1.0;          // :329
     root.glen = ng;
@@ -718,12 +748,13 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
         f.in[sh] = d_align_ + aoff;
         aoff += align4(f.n[sh]) + 4;
       }
-      root.off[sh] = 0;
-      root.len[sh] = f.n[sh];
+      root_seg[sh].off = 0;
+      root_seg[sh].len = f.n[sh];
     }
     f.leaf.assign(j.k, -1);
     f.leaf[0] = (int)nodes_.size();
     nodes_.push_back(root);
+    for (int sh = 0; sh < S; ++sh) segs_.push_back(root_seg[sh]);
     if (j.k > 1) active.push_back(f.leaf[0]);
   }
 
@@ -768,6 +799,8 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   DQ_HIP(hipStreamSynchronize(stream));
   if (trace_) {
     const double t_end = host_us();
+    std::fprintf(stderr, "divquant-hip trace: map prep %.1fus, map launch+sync %.1fus\n",
+                 tr_mapprep_us_, tr_mapsync_us_);
     std::fprintf(stderr,
                  "divquant-hip trace: frames=%d shards=%d rounds=%d cluster=%.1fus (build %.1f, "
                  "wait %.1f, replay %.1f) map+sync=%.1fus total=%.1fus\n",
@@ -847,8 +880,9 @@ void sorted_palette(const uint32_t* ct, int k, uint32_t* pal_out, uint16_t* lut_
   for (int v = 0; v < 766; ++v) lut_out[v] = (uint16_t)lut[v];
 }
 
-// Per-map block of the map staging: [palette: kMapPal words | LUT: 768 u16];
-// the staging starts with the MapTask table of the launch.
+// Per-map block of the map staging: [LUT: 768 u16 | palette: k words,
+// padded to 16 B], blocks packed; the staging starts with the MapTask table
+// of the launch.
 constexpr size_t kMapPal = 16384;
 constexpr size_t kMapBlockWords = kMapPal + 768 / 2;
 constexpr int kMapChunk = 16;   // tasks per batched launch (cell tables: 2.5 MB each)
@@ -876,7 +910,9 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     DQ_CHECK(jobs[i].k <= (int)kMapPal, "colormapSize > 16384 is not supported by the LDS palette");
   }
   // the staging is reused: the previous map's upload must have been consumed
+  const double tm0 = trace_ ? host_us() : 0.0;
   DQ_HIP(hipStreamSynchronize(stream));
+  const double tm1 = trace_ ? host_us() : 0.0;
   const int chunk = std::min(njobs, kMapChunk);
   ensure_map_stage(chunk);
   if ((size_t)chunk > cap_cells_) {
@@ -908,17 +944,22 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     }
     // K <= 1024: the LDS-table map, one workgroup per CU over all tasks
     const bool lds_map = kmax <= 1024 && use_lds_map_;
+    size_t woff = 0;   // packed blocks
+    std::vector<size_t> blk_off(nt), blk_words(nt);
     for (int t = 0; t < nt; ++t) {
       const MapJob& j = jobs[c0 + t];
-      uint32_t* hb = hblk0 + (size_t)t * kMapBlockWords;
-      const uint32_t* db = dblk0 + (size_t)t * kMapBlockWords;
-      sorted_palette(j.ct, j.k, hb, reinterpret_cast<uint16_t*>(hb + kMapPal));
+      blk_off[t] = woff;
+      blk_words[t] = 768 / 2 + (((size_t)j.k + 3) & ~(size_t)3);
+      woff += blk_words[t];
+      uint32_t* hb = hblk0 + blk_off[t];
+      const uint32_t* db = dblk0 + blk_off[t];
+      sorted_palette(j.ct, j.k, hb + 768 / 2, reinterpret_cast<uint16_t*>(hb));
       MapTask& m = ht[t];
       m.in = j.d_in;
       m.out = j.d_out;
       if (((uintptr_t)j.d_in & 15) != 0 || ((uintptr_t)j.d_out & 15) != 0) staged.push_back(t);
-      m.pal = db;
-      m.lut = reinterpret_cast<const uint16_t*>(db + kMapPal);
+      m.pal = db + 768 / 2;
+      m.lut = reinterpret_cast<const uint16_t*>(db);
       m.cell_rec = d_cell_rec_ + (size_t)t * kCells * kCellRecWords;
       m.cell_idx = d_cell_idx_ + (size_t)t * kCells * kCellCap;
       m.cell_c32 = d_cell_c32_ + (size_t)t * kCells;
@@ -944,7 +985,8 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       DQ_HIP(hipMalloc((void**)&d_map_align_, need * sizeof(uint32_t)));
       cap_map_align_ = need;
     }
-    const size_t bytes = (size_t)chunk * sizeof(MapTask) + (size_t)nt * kMapBlockWords * 4;
+    const size_t bytes = (size_t)chunk * sizeof(MapTask) + woff * 4;
+    if (trace_) tr_mapprep_us_ = host_us() - tm1;
     if (staged.empty()) {
       DQ_HIP(hipMemcpyAsync(d_mapstage_, h_mapstage_, bytes, hipMemcpyHostToDevice, stream));
       const MapTask* dt = reinterpret_cast<const MapTask*>(d_mapstage_);
@@ -976,11 +1018,11 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
         one.cell_c32 = d_cell_c32_;
         DQ_HIP(hipStreamSynchronize(stream));   // staging slot 0 reuse
         ht[0] = one;
-        if (t != 0) std::memcpy(hblk0, hblk0 + (size_t)t * kMapBlockWords, kMapBlockWords * 4);
-        ht[0].pal = dblk0;
-        ht[0].lut = reinterpret_cast<const uint16_t*>(dblk0 + kMapPal);
+        if (t != 0) std::memmove(hblk0, hblk0 + blk_off[t], blk_words[t] * 4);
+        ht[0].pal = dblk0 + 768 / 2;
+        ht[0].lut = reinterpret_cast<const uint16_t*>(dblk0);
         DQ_HIP(hipMemcpyAsync(d_mapstage_, h_mapstage_,
-                              (size_t)chunk * sizeof(MapTask) + kMapBlockWords * 4,
+                              (size_t)chunk * sizeof(MapTask) + blk_words[t] * 4,
                               hipMemcpyHostToDevice, stream));
         const MapTask* dt = reinterpret_cast<const MapTask*>(d_mapstage_);
         const uint32_t nb = std::max<uint32_t>(1, (j.n / 8 + one.grp_per_block - 1) / one.grp_per_block);
@@ -995,7 +1037,12 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       }
     }
   }
+  const double tm2 = trace_ ? host_us() : 0.0;
   DQ_HIP(hipStreamSynchronize(stream));
+  if (trace_) {
+    tr_mapsync_us_ = host_us() - tm2;
+    std::fprintf(stderr, "divquant-hip map: first sync %.1fus\n", tm1 - tm0);
+  }
   collect_timing();
 }
 

@@ -40,25 +40,30 @@ namespace dq {
 constexpr int kMaxShard = 8;
 
 // A node of a frame's split tree: one cluster as it exists between splits.
-// Its points are spread over the frame's shards: one local segment per shard.
+// Its points are spread over the frame's shards: one local segment per
+// shard, kept in Engine::segs_ (entry node * nshard + shard).
 struct Node {
   int frame = 0;
   int child_old = -1, child_new = -1;
-  bool expanded = false;
+  int parent = -1;
   int32_t buf = 0;                   // 0: caller's input, 1: P0, 2: P1
+  bool expanded = false;
+  bool partitioned = false;          // children's points written to child_buf(buf)
   double w = 0.0;                    // weight[]   (:290, :862-863)
   double mean[3] = {0, 0, 0};        // mean[]     (:309)
   double var[3] = {0, 0, 0};         // var[]      (:314)
   double tse = 0.0;                  // tse[]      (:304)
   uint64_t glen = 0;                 // size[] of the cluster (all shards, all processes)
-  uint32_t off[kMaxShard] = {}, len[kMaxShard] = {};   // local segment per shard
-  int parent = -1;
-  // the round the node was split in: its records and tiles stay on the device
-  // so that a later round can partition it (fused with its children's split)
-  const DevNode* dnode[kMaxShard] = {};
-  const Tile* dtiles[kMaxShard] = {};
-  int ntiles[kMaxShard] = {};
-  bool partitioned = false;          // children's points written to child_buf(buf)
+};
+
+// A node's local segment in one shard, and -- once the node has been split --
+// its record and tiles on the device (kept for the whole run so that a later
+// round can partition it, fused with its children's split pass).
+struct Seg {
+  uint32_t off = 0, len = 0;
+  int32_t ntiles = 0;
+  const DevNode* dnode = nullptr;
+  const Tile* dtiles = nullptr;
 };
 
 // One quant_recurse / DivQuantCluster input.
@@ -154,6 +159,8 @@ class Engine {
   KernelStat stats[ST_COUNT];
 
  private:
+  using HeapEnt = std::pair<std::pair<double, int>, int>;
+  std::vector<HeapEnt> top_;          // next_active scratch
   struct FrameState {
     FrameJob* job = nullptr;
     double s = 0.0;                   // get_double_scale
@@ -164,7 +171,7 @@ class Engine {
     uint32_t n[kMaxShard] = {};
     uint32_t first[kMaxShard] = {};
     std::vector<int> leaf;            // cluster index -> node id
-    std::priority_queue<std::pair<std::pair<double, int>, int>> heap;  // ((tse,-idx), node)
+    std::vector<HeapEnt> heap;        // max-heap of ((tse, -idx), node) (std::push_heap)
     int new_index = 1, old_index = 0;
     int need = -1;                    // node the replay waits for (-1: done)
     std::vector<int64_t> trace;
@@ -229,8 +236,9 @@ class Engine {
   int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_NODE_TILES)
   uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TILE_MAX)
   // host-side trace (DQ_HIP_TRACE=1): per-run phase times on stderr
-  bool trace_ = false;
+  bool trace_ = false, trace_rounds_ = false;   // DQ_HIP_TRACE=1 / 2 (per round)
   double tr_wait_us_ = 0, tr_build_us_ = 0, tr_replay_us_ = 0;
+  double tr_mapprep_us_ = 0, tr_mapsync_us_ = 0;
 
   // map tables
   uint32_t* d_cell_c32_ = nullptr;    // compact records per map task of a chunk
@@ -245,6 +253,8 @@ class Engine {
   void ensure_map_stage(size_t nmaps);
 
   std::vector<Node> nodes_;
+  std::vector<Seg> segs_;             // node * nshard_ + shard
+  Seg& seg(int node, int shard) { return segs_[(size_t)node * nshard_ + shard]; }
   int nshard_ = 1;                    // shard records per logical node in this run
   uint64_t* d_tot_ = nullptr;         // sharded rounds: per logical node totals
   size_t cap_tot_ = 0;

@@ -368,13 +368,14 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
 // This lane's share of the sums of one node record's pass: its tile partials
 // in u64 (PASS_SPLIT of a record whose parent was partitioned this round: its
 // half of the parent's fused partition+split partials instead).
-template <int KIND>
-__device__ __forceinline__ void sum_record(const RoundArgs& a, const DevNode* w, uint64_t acc[7]) {
+template <int KIND, int W = kBlock>
+__device__ __forceinline__ void sum_record(const RoundArgs& a, const DevNode* w, uint64_t acc[7],
+                                           int tid = (int)threadIdx.x) {
   if (KIND == PASS_SPLIT && w->split_pb >= 0) {
     // children's (cnt, sums) of the fused pass: [0..3] old half, [4..7] new half
     const g_cu4* sp4 = (const g_cu4*)a.sparts;
     const int side = w->split_side;
-    for (int i = w->split_pb + (int)threadIdx.x; i < w->split_pe; i += kBlock) {
+    for (int i = w->split_pb + tid; i < w->split_pe; i += W) {
       const u32x4 x = sp4[2 * i + side];
       acc[0] += x[0];
       acc[1] += x[1];
@@ -386,11 +387,11 @@ __device__ __forceinline__ void sum_record(const RoundArgs& a, const DevNode* w,
   const int tb = w->tile_begin, te = w->tile_end;
   const g_cu4* parts4 = (const g_cu4*)a.parts;
   constexpr bool kSquares = KIND != PASS_SPLIT;
-  for (int base = tb; base < te; base += 4 * kBlock) {
+  for (int base = tb; base < te; base += 4 * W) {
     u32x4 x[4], y[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {   // issue every load of the chunk first
-      const int i = base + u * kBlock + (int)threadIdx.x;
+      const int i = base + u * W + tid;
       if (i < te) {
         x[u] = parts4[2 * i];
         if (kSquares) y[u] = parts4[2 * i + 1];
@@ -452,58 +453,58 @@ __global__ __launch_bounds__(kBlock) void nodesum_kernel(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Epilogue: one workgroup per node record of the round.
+// Epilogue: ONE WAVE per node record of the round (no workgroup barrier).
 //   * the node's sums: its own partials (FROM_TOT: the logical node's global
 //     totals from nodesum + allreduce; its own partials then only give the
 //     record's local new-half size);
-//   * thread 0 runs the FP64 update (node_update) -- every record of a
+//   * lane 0 runs the FP64 update (node_update) -- every record of a
 //     logical node runs it on the same totals, so all agree bit for bit;
 //   * a record whose split became final: the partition's per-(tile, wave)
-//     write cursors, and the results written straight to host memory
-//     (NodeResult);
-//   * 2-means launches: every workgroup arrives on the launch's (sharded)
+//     write cursors (a shuffle scan over the lanes' tile chunks), and the
+//     results written straight to host memory (NodeResult);
+//   * 2-means launches: every record arrives on the launch's (sharded)
 //     counter; the last to arrive publishes (round seq, records still
 //     active) to the host, which stops launching iterations once no node is
 //     active.
+constexpr int kEpiBlock = 64;
 template <int KIND, bool FROM_TOT>
-__global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
+__global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
   constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
   DevNode* w = a.nodes + blockIdx.x;
+  const uint32_t lane = threadIdx.x;
   const bool skip = kMeans && w->done_it != 0;   // final in an earlier launch
-  __shared__ uint64_t red[kBlock / 64][8];
-  __shared__ int final_results;
   __shared__ NodeResult sres;
-  if (threadIdx.x == 0) final_results = 0;
+  bool final_results = false;
   if (!skip) {
     const int tb = w->tile_begin, te = w->tile_end;
     uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    sum_record<KIND>(a, w, acc);
+    sum_record<KIND, kEpiBlock>(a, w, acc, (int)lane);
     uint64_t tot[7];
-    block_sum7(acc, red, tot);   // (every thread has read done_it above)
-    if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < F_NUM; ++k) tot[k] = wave_sum_u64(acc[k]);   // in every lane
+    int fin = 0;
+    if (lane == 0) {
       const uint32_t local_new = (uint32_t)tot[F_CNT];
       if (FROM_TOT) {
         const uint64_t* g = a.tot + (size_t)(blockIdx.x / a.nshard) * 8;
         for (int k = 0; k < F_NUM; ++k) tot[k] = g[k];
       }
-      const bool fin = node_update<KIND>(w, &sres, tot, a.fixed_point != 0);
+      fin = node_update<KIND>(w, &sres, tot, a.fixed_point != 0) ? 1 : 0;
       if (fin) {
         for (int c = 0; c < 3; ++c) { sres.tm[c] = w->tm[c]; sres.tv[c] = w->tv[c]; }
         w->n_new_local = local_new;
         sres.n_new_local = local_new;
         sres.done_it = w->done_it;
       }
-      final_results = fin ? 1 : 0;
     }
-    __syncthreads();
+    final_results = __shfl(fin, 0, 64) != 0;
     if (kMeans && final_results) {
       // Partition cursors: for every (tile, wave) of the node, the OLD and
-      // NEW points of the node before its share -- an exclusive scan of the
-      // final pass's per-wave counts, chunked per lane over the tiles.
-      __shared__ uint64_t scan[kBlock];
+      // NEW points of the node before its share -- an exclusive shuffle scan
+      // of the final pass's per-wave counts, chunked per lane over the tiles.
       const int T = te - tb;
-      const int chunk = (T + kBlock - 1) / kBlock;
-      const int c0 = tb + (int)threadIdx.x * chunk;
+      const int chunk = (T + 63) / 64;
+      const int c0 = tb + (int)lane * chunk;
       const int c1 = min(te, c0 + chunk);
       const uint32_t* wp = a.wparts;
       uint64_t local = 0;   // old | new << 32
@@ -512,15 +513,13 @@ __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
           const uint32_t x = wp[i * kTileWaves + ww];
           local += (uint64_t)(x & 0xFFFFu) | ((uint64_t)(x >> 16) << 32);
         }
-      scan[threadIdx.x] = local;
-      __syncthreads();
-      for (int o = 1; o < kBlock; o <<= 1) {
-        const uint64_t v = threadIdx.x >= (uint32_t)o ? scan[threadIdx.x - o] : 0ull;
-        __syncthreads();
-        scan[threadIdx.x] += v;
-        __syncthreads();
+      uint64_t inc = local;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t u = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += u;
       }
-      const uint64_t run0 = scan[threadIdx.x] - local;
+      const uint64_t run0 = inc - local;
       uint32_t ro = (uint32_t)run0, rn = (uint32_t)(run0 >> 32);
       for (int i = c0; i < c1; ++i)
         for (int ww = 0; ww < kTileWaves; ++ww) {
@@ -533,37 +532,37 @@ __global__ __launch_bounds__(kBlock) void epilogue_kernel(RoundArgs a) {
     }
   }
   if (kMeans) {
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // Final results go straight to host-coherent memory: relaxed system-scope
     // 8-B stores, one per lane (no L2 write-back), drained before arriving.
     constexpr int kWords = (int)(sizeof(NodeResult) / 8);
     static_assert(kWords <= 64, "one wave stores the result");
-    if (final_results && threadIdx.x < kWords) {
-      const uint64_t v = reinterpret_cast<const uint64_t*>(&sres)[threadIdx.x];
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.hres + blockIdx.x) + threadIdx.x, v,
+    if (final_results && lane < (uint32_t)kWords) {
+      const uint64_t v = reinterpret_cast<const uint64_t*>(&sres)[lane];
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.hres + blockIdx.x) + lane, v,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (threadIdx.x < 64) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (threadIdx.x == 0) {
-        // 64-bit arrivals (low word = arrived, high = still active) on this
-        // workgroup's shard, then the shard's last arriver on the top word
-        LaunchCtr* c = a.ctr + a.it;
-        const uint32_t sh = blockIdx.x % kArrShards;
-        const uint32_t nsh = min((uint32_t)a.nn, (uint32_t)kArrShards);
-        const uint32_t in_shard = ((uint32_t)a.nn - sh + kArrShards - 1) / kArrShards;
-        const uint64_t mine = 1ull | ((uint64_t)(!skip && !final_results) << 32);
-        const uint64_t old = __hip_atomic_fetch_add(&c->shard[sh].word, mine, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)old == in_shard - 1) {
-          const uint64_t fwd = 1ull | (((old >> 32) + (mine >> 32)) << 32);
-          const uint64_t t = __hip_atomic_fetch_add(&c->top.word, fwd, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-          if ((uint32_t)t == nsh - 1) {
-            const uint64_t act = (t >> 32) + (fwd >> 32);
-            __hip_atomic_store(a.hstat + a.it, (a.seq << 32) | (act << 1) | 1ull,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      // 64-bit arrivals (low word = arrived, high = still active) on this
+      // record's shard, then the shard's last arriver on the top word
+      LaunchCtr* c = a.ctr + a.it;
+      const uint32_t sh = blockIdx.x % kArrShards;
+      const uint32_t nsh = min((uint32_t)a.nn, (uint32_t)kArrShards);
+      const uint32_t in_shard = ((uint32_t)a.nn - sh + kArrShards - 1) / kArrShards;
+      const uint64_t mine = 1ull | ((uint64_t)(!skip && !final_results) << 32);
+      const uint64_t old = __hip_atomic_fetch_add(&c->shard[sh].word, mine, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)old == in_shard - 1) {
+        const uint64_t fwd = 1ull | (((old >> 32) + (mine >> 32)) << 32);
+        const uint64_t t = __hip_atomic_fetch_add(&c->top.word, fwd, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)t == nsh - 1) {
+          const uint64_t act = (t >> 32) + (fwd >> 32);
+          __hip_atomic_store(a.hstat + a.it, (a.seq << 32) | (act << 1) | 1ull,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
     }
@@ -1212,7 +1211,7 @@ void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) {
 void launch_epilogue(int kind, const RoundArgs& a, int nnodes, bool from_totals,
                      hipStream_t stream) {
   if (nnodes <= 0) return;
-  const dim3 g(nnodes), b(kBlock);
+  const dim3 g(nnodes), b(kEpiBlock);
   if (from_totals) {
     switch (kind) {
       case PASS_INIT: epilogue_kernel<PASS_INIT, true><<<g, b, 0, stream>>>(a); break;
