@@ -17,6 +17,8 @@ Device-resident entry points (torch tensors / raw device pointers on HBM):
     quant_device, quant_batch_device, cluster_device, map_device
 Row-tile sharding (one frame over shards / GPUs, RCCL allreduce per pass):
     quant_rows_device, comm_init_torch (comm_unique_id, comm_init, comm_destroy)
+Full-frame block histograms (genHistogramsForBlocks):
+    get_subdivided_colors, gen_histograms_for_blocks, block_hist_device
 """
 import ctypes
 import os
@@ -84,6 +86,11 @@ def lib():
         "dq_hip_stat_name": ([c.c_int], c.c_char_p),
         "dq_hip_set_lanes": ([c.c_int], None),
         "dq_hip_get_lanes": ([], c.c_int),
+        "dq_hip_block_hist": ([vp, c.c_uint32, c.c_uint32, vp, c.c_int, c.c_uint32, c.c_uint32,
+                               c.c_uint32, vp, vp, vp, vp, vp], c.c_int),
+        "dq_hip_block_hist_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, vp, c.c_int, c.c_uint32,
+                                   c.c_uint32, c.c_uint32, vp, vp, vp, vp, vp, vp], c.c_int),
+        "dq_subdivided_colors": ([vp], None),
         "quant_recurse": ([c.c_uint32, vp, vp, u32p, vp, c.c_int], None),
     }
     for name, (args, res) in sigs.items():
@@ -271,6 +278,70 @@ def map_device(t_in, t_out, colortable, device=0, n=None, stream=None):
     if lib().dq_hip_map_dev(device, _dptr(t_in), n, _dptr(t_out), _ptr(ct), ct.size,
                             _stream_ptr(stream)) < 0:
         raise DivQuantError("dq_hip_map_dev: bad arguments")
+
+
+# ---------------------------------------------------------------------------
+# Full-frame fixed-palette map + per-block mode.
+def get_subdivided_colors():
+    """getSubdividedColors (superpixels/OpenCVUtil.cpp:853-897): the 125
+    colours 0xFFRRGGBB of the {0,63,127,191,255}^3 cube (no GPU needed)."""
+    out = np.zeros(125, np.uint32)
+    lib().dq_subdivided_colors(_ptr(out))
+    return out
+
+
+def block_grid(width, height, superpixel_dim=4):
+    """(blockWidth, blockHeight) as clusteringCombine computes them
+    (ClusteringSegmentationMain.cpp:138-149): ceil(W/dim), ceil(H/dim)."""
+    return -(-width // superpixel_dim), -(-height // superpixel_dim)
+
+
+def gen_histograms_for_blocks(frame, superpixel_dim=4, palette=None, tables=False):
+    """genHistogramsForBlocks (ClusteringSegmentation.cpp:365-576) on a frame of
+    0x00RRGGBB words shaped (H, W) (the Vec3BToUID packing of the BGR Mat).
+
+    Returns (block_bgr, region_quant_pixel, quant[, (ndistinct, keys, counts)]):
+    block_bgr (bh, bw, 3) uint8 is the returned blockMat (B, G, R bytes);
+    region_quant_pixel (bh, bw) uint32 is each block's HistogramForBlock::
+    regionQuantPixel; quant (H, W) the map_colors_mps output.  With tables=True
+    also each block's pixelToCountTable in iteration order: ndistinct (bh, bw)
+    and keys/counts (bh, bw, dim*dim), zero past ndistinct."""
+    _require_gpu()
+    fr = _u32(frame)
+    if fr.ndim != 2 or fr.size == 0:
+        raise DivQuantError("frame must be a non-empty (H, W) array")
+    h, w = fr.shape
+    bw, bh = block_grid(w, h, superpixel_dim)
+    pal = get_subdivided_colors() if palette is None else _u32(palette).reshape(-1)
+    quant = np.zeros((h, w), np.uint32)
+    mode = np.zeros((bh, bw), np.uint32)
+    cap = superpixel_dim * superpixel_dim
+    nd = np.zeros((bh, bw), np.uint32) if tables else None
+    keys = np.zeros((bh, bw, cap), np.uint32) if tables else None
+    counts = np.zeros((bh, bw, cap), np.uint32) if tables else None
+    none = ctypes.c_void_p(0)
+    rc = lib().dq_hip_block_hist(_ptr(fr), w, h, _ptr(pal), pal.size, superpixel_dim, bw, bh,
+                                 _ptr(quant), _ptr(mode), _ptr(nd) if tables else none,
+                                 _ptr(keys) if tables else none, _ptr(counts) if tables else none)
+    if rc < 0:
+        raise DivQuantError("dq_hip_block_hist: bad arguments")
+    bgr = np.stack([mode & 0xFF, (mode >> 8) & 0xFF, (mode >> 16) & 0xFF], axis=-1).astype(np.uint8)
+    if tables:
+        return bgr, mode, quant, (nd, keys, counts)
+    return bgr, mode, quant
+
+
+def block_hist_device(t_in, width, height, t_quant, t_mode, palette=None, superpixel_dim=4,
+                      t_ndistinct=None, t_keys=None, t_counts=None, device=0, stream=None):
+    """dq_hip_block_hist_dev on torch tensors / device pointers (asynchronous)."""
+    pal = get_subdivided_colors() if palette is None else _u32(palette).reshape(-1)
+    bw, bh = block_grid(width, height, superpixel_dim)
+    opt = lambda t: _dptr(t) if t is not None else ctypes.c_void_p(0)  # noqa: E731
+    if lib().dq_hip_block_hist_dev(device, _dptr(t_in), width, height, _ptr(pal), pal.size,
+                                   superpixel_dim, bw, bh, _dptr(t_quant), _dptr(t_mode),
+                                   opt(t_ndistinct), opt(t_keys), opt(t_counts),
+                                   _stream_ptr(stream)) < 0:
+        raise DivQuantError("dq_hip_block_hist_dev: bad arguments")
 
 
 def last_centroids(k, device=0):

@@ -104,6 +104,30 @@ int dq_hip_map_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out
   return 0;
 }
 
+static bool block_hist_shape_ok(uint32_t w, uint32_t h, uint32_t dim, uint32_t bw, uint32_t bh) {
+  // every block must hold a pixel (the reference asserts it, :468)
+  return w > 0 && h > 0 && dim >= 1 && dim <= 4 && bw > 0 && bh > 0 &&
+         (uint64_t)(bw - 1) * dim < w && (uint64_t)(bh - 1) * dim < h &&
+         (uint64_t)w * h <= 0xFFFFFFFFull && (uint64_t)bw * bh < 0xFFFFFF00ull;
+}
+
+int dq_hip_block_hist_dev(int device, const uint32_t* d_in, uint32_t width, uint32_t height,
+                          const uint32_t* palette, int npal, uint32_t dim, uint32_t block_w,
+                          uint32_t block_h, uint32_t* d_quant, uint32_t* d_mode,
+                          uint32_t* d_ndistinct, uint32_t* d_keys, uint32_t* d_counts,
+                          void* stream) {
+  if (!d_in || !palette || npal <= 0 || !d_quant || !d_mode || (!d_keys) != (!d_counts) ||
+      !block_hist_shape_ok(width, height, dim, block_w, block_h))
+    return -1;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  e.map(d_in, width * height, d_quant, palette, npal, (hipStream_t)stream);
+  uint32_t* work = e.scratch_words(dq::block_hist_scratch_words(block_w, block_h));
+  dq::BlockHistArgs a{d_quant, width, height, block_w, block_h, d_mode, d_ndistinct, d_keys, d_counts,
+                      work, nullptr, 0};
+  return dq::launch_block_hist(a, (int)dim, (hipStream_t)stream);
+}
+
 int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
                            const uint32_t* n, uint32_t* const* d_out, uint32_t k,
                            uint32_t* ct, uint32_t* k_out, int max_iters, void* stream) {
@@ -274,6 +298,54 @@ int dq_hip_map(const uint32_t* in, uint32_t n, uint32_t* out, const uint32_t* ct
   DQ_HIP(hipMemcpyAsync(out, e.staged_out(), (size_t)n * 4, hipMemcpyDeviceToHost, st));
   DQ_HIP(hipStreamSynchronize(st));
   return 0;
+}
+
+void dq_subdivided_colors(uint32_t* out125) {
+  static const uint32_t v[5] = {0, 63, 127, 191, 255};
+  for (int i = 0; i < 125; ++i)   // R outermost, B innermost, alpha 0xFF (:874-888)
+    out125[i] = 0xFF000000u | (v[i / 25] << 16) | (v[i / 5 % 5] << 8) | v[i % 5];
+}
+
+int dq_hip_block_hist(const uint32_t* in, uint32_t width, uint32_t height, const uint32_t* palette,
+                      int npal, uint32_t dim, uint32_t block_w, uint32_t block_h, uint32_t* quant,
+                      uint32_t* mode, uint32_t* ndistinct, uint32_t* keys, uint32_t* counts) {
+  if (!in || !palette || npal <= 0 || !mode || (!keys) != (!counts) ||
+      !block_hist_shape_ok(width, height, dim, block_w, block_h))
+    return -1;
+  const int dev = current_device();
+  Engine& e = engine_for(dev);
+  hipStream_t st = e.stream();
+  const size_t n = (size_t)width * height, nb = (size_t)block_w * block_h, cap = (size_t)dim * dim;
+  uint32_t *d_mode = nullptr, *d_nd = nullptr, *d_keys = nullptr, *d_counts = nullptr;
+  DQ_HIP(hipMallocAsync((void**)&d_mode, nb * 4, st));
+  if (ndistinct) DQ_HIP(hipMallocAsync((void**)&d_nd, nb * 4, st));
+  if (keys) {
+    DQ_HIP(hipMallocAsync((void**)&d_keys, nb * cap * 4, st));
+    DQ_HIP(hipMallocAsync((void**)&d_counts, nb * cap * 4, st));
+    DQ_HIP(hipMemsetAsync(d_keys, 0, nb * cap * 4, st));
+    DQ_HIP(hipMemsetAsync(d_counts, 0, nb * cap * 4, st));
+  }
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(e.mutex());
+    e.stage_in(in, (uint32_t)n, st);
+    e.map(e.staged_in(), (uint32_t)n, e.staged_out(), palette, npal, st);
+    uint32_t* work = e.scratch_words(dq::block_hist_scratch_words(block_w, block_h));
+    dq::BlockHistArgs a{e.staged_out(), width, height, block_w, block_h, d_mode, d_nd, d_keys, d_counts,
+                        work, nullptr, 0};
+    rc = dq::launch_block_hist(a, (int)dim, st);
+    if (quant) DQ_HIP(hipMemcpyAsync(quant, e.staged_out(), n * 4, hipMemcpyDeviceToHost, st));
+    DQ_HIP(hipMemcpyAsync(mode, d_mode, nb * 4, hipMemcpyDeviceToHost, st));
+    if (ndistinct) DQ_HIP(hipMemcpyAsync(ndistinct, d_nd, nb * 4, hipMemcpyDeviceToHost, st));
+    if (keys) {
+      DQ_HIP(hipMemcpyAsync(keys, d_keys, nb * cap * 4, hipMemcpyDeviceToHost, st));
+      DQ_HIP(hipMemcpyAsync(counts, d_counts, nb * cap * 4, hipMemcpyDeviceToHost, st));
+    }
+    DQ_HIP(hipStreamSynchronize(st));
+  }
+  for (uint32_t* p : {d_mode, d_nd, d_keys, d_counts})
+    if (p) DQ_HIP(hipFree(p));
+  return rc;
 }
 
 int dq_hip_last_centroids(int device, double* means, int64_t* sizes, int k) {

@@ -139,6 +139,18 @@ void Engine::stage_in(const uint32_t* h_in, uint32_t n, hipStream_t stream) {
                         hipMemcpyHostToDevice, stream));
 }
 
+uint32_t* Engine::scratch_words(size_t n) {
+  if (n > cap_scratch_) {
+    if (d_scratch_) {
+      DQ_HIP(hipDeviceSynchronize());
+      DQ_HIP(hipFree(d_scratch_));
+    }
+    DQ_HIP(hipMalloc((void**)&d_scratch_, n * sizeof(uint32_t)));
+    cap_scratch_ = n;
+  }
+  return d_scratch_;
+}
+
 // Device arena for the per-round tables.  Chunks are kept (and reused by the
 // next run); a round's block never moves once written.
 char* Engine::arena_alloc(size_t bytes) {

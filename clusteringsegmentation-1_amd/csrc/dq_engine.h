@@ -119,6 +119,9 @@ class Engine {
   void stage_in(const uint32_t* h_in, uint32_t n, hipStream_t stream);
   const uint32_t* staged_in() const { return d_stage_in_; }
   uint32_t* staged_out() { return d_stage_out_; }
+  // Device scratch of at least n words for stream-ordered helpers (block
+  // histogram queue); growing it waits for the device.
+  uint32_t* scratch_words(size_t n);
 
   hipStream_t stream() const { return stream_; }
 
@@ -205,6 +208,8 @@ class Engine {
   uint32_t* d_stage_in_ = nullptr;
   uint32_t* d_stage_out_ = nullptr;
   size_t cap_stage_ = 0;
+  uint32_t* d_scratch_ = nullptr;
+  size_t cap_scratch_ = 0;
   uint32_t* d_align_ = nullptr;       // aligned copies of misaligned inputs
   size_t cap_align_ = 0;
   uint32_t* d_map_align_ = nullptr;   // map staging for misaligned in/out

@@ -88,4 +88,31 @@ void launch_map(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hi
 constexpr int kMapLdsBlock = 1024;
 void launch_map_lds(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream);
 
+// Block histograms of a mapped frame (genHistogramsForBlocks' block loop,
+// ClusteringSegmentation.cpp:420-563).  Blocks of dim x dim pixels, dim 1..4 (the app: 4);
+// keys/counts (optional, nblocks * dim^2) get each block's histogram in the
+// reference's iteration order.  Requires block_w*dim < width+dim and
+// block_h*dim < height+dim (every block holds a pixel).
+struct BlockHistArgs {
+  const uint32_t* quant;
+  uint32_t width, height, block_w, block_h;
+  uint32_t* mode;
+  uint32_t* ndistinct;
+  uint32_t* keys;
+  uint32_t* counts;
+  uint32_t* work_n;   // block_hist_scratch_words() of device scratch (tie queues)
+  uint32_t* work;     // set by launch_block_hist
+  uint32_t queue_cap; // set by launch_block_hist
+};
+// Tie queues: one per (workgroup % kBhQueues), counters 128 B apart.  Measured
+// per 4K frame (light + rank kernel, us): 1 queue 61+21 (same-address
+// atomics), 8: 15+21, 16: 10+22, 32: 9+93, 64: 10+157 (the ranking kernel
+// degrades with many sparse queues; not understood yet).
+#ifndef DQ_BH_QUEUES
+#define DQ_BH_QUEUES 16
+#endif
+constexpr uint32_t kBhQueues = DQ_BH_QUEUES, kBhQueueStride = 32;
+size_t block_hist_scratch_words(uint32_t block_w, uint32_t block_h);
+int launch_block_hist(const BlockHistArgs& a, int dim, hipStream_t stream);
+
 }  // namespace dq

@@ -28,11 +28,16 @@
 //   map_kernel            map: per pixel argmin over (squared distance, MPS
 //                         visit rank) -- identical to map_colors_mps's pruned
 //                         walk (DivQuantMapColors.cpp:385-527), see DESIGN.md.
+//   block_hist_kernel     genHistogramsForBlocks' per-block mode over a mapped
+//                         frame (ClusteringSegmentation.cpp:420-563): one lane
+//                         per dim x dim block, unordered_map tie-break order
+//                         from stl_order.h.  Reads 4 B per pixel.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
 
 #include "dq_kernels.h"
+#include "stl_order.h"
 
 namespace dq {
 
@@ -1284,6 +1289,199 @@ void launch_map(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hi
     map_kernel<false><<<dim3(nblocks), dim3(kBlock), lds, stream>>>(tasks, ntasks);
   else
     map_kernel<true><<<dim3(nblocks), dim3(kBlock), lds, stream>>>(tasks, ntasks);
+}
+
+// ---------------------------------------------------------------------------
+// Block histograms (genHistogramsForBlocks, ClusteringSegmentation.cpp:420-563)
+// One lane per block: the block's pixels in row-major order (clipped at the
+// frame edge) are slots; a slot is a map key when it is the first occurrence
+// of its colour, its insertion index = number of keys before it.  The mode is
+// the key with the largest count that comes first in the histogram's
+// iteration order (stl_rank_slots).  Lanes of a wave own horizontally
+// adjacent blocks, so each block row is one contiguous 16-B-per-lane load.
+// Two kernels: the light one settles blocks whose largest count is unique (or
+// that hold one colour) and queues the rest; the ranking kernel (O(N^2)
+// compares, ~5x the registers) runs over the queue only.
+template <int DIM>
+__device__ __forceinline__ void block_slots(const BlockHistArgs& a, uint32_t bx, uint32_t by,
+                                            uint32_t* px, int* ins, uint32_t* cnt, int& d) {
+  constexpr int N = DIM * DIM;
+  const uint32_t x0 = bx * DIM, y0 = by * DIM;
+  const uint32_t nx = min((uint32_t)DIM, a.width - x0), ny = min((uint32_t)DIM, a.height - y0);
+  g_cu32* q = (g_cu32*)a.quant;
+  bool valid[N];
+  if (DIM == 4 && nx == 4 && ny == 4 && (a.width & 3) == 0) {
+#pragma unroll
+    for (int r = 0; r < DIM; ++r) {
+      const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(q + (size_t)(y0 + r) * a.width + x0);
+      px[r * DIM + 0] = v.x; px[r * DIM + 1] = v.y; px[r * DIM + 2] = v.z; px[r * DIM + 3] = v.w;
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) valid[r * DIM + c] = true;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < DIM; ++r)
+#pragma unroll
+      for (int c = 0; c < DIM; ++c) {
+        const bool ok = (uint32_t)r < ny && (uint32_t)c < nx;
+        valid[r * DIM + c] = ok;
+        px[r * DIM + c] = ok ? q[(size_t)(y0 + r) * a.width + x0 + c] : 0u;
+      }
+  }
+  // keys: first occurrences in slot order; counts over all valid slots
+  d = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    bool first = valid[i];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const bool same = valid[j] && px[j] == px[i];
+      if (j < i && same) first = false;
+      c += same ? 1u : 0u;
+    }
+    ins[i] = first ? d : -1;
+    d += first ? 1 : 0;
+    cnt[i] = c;
+  }
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void block_hist_kernel(BlockHistArgs a) {
+  constexpr int N = DIM * DIM;
+  const uint32_t b = blockIdx.x * 256u + threadIdx.x;   // nblocks < 2^32 (host check)
+  const bool live = b < a.block_w * a.block_h;
+  bool queue = false;
+  if (live) {
+    const uint32_t by = b / a.block_w, bx = b - by * a.block_w;
+    const uint32_t x0 = bx * DIM, y0 = by * DIM;
+    const uint32_t nx = min((uint32_t)DIM, a.width - x0), ny = min((uint32_t)DIM, a.height - y0);
+    g_cu32* q = (g_cu32*)a.quant;
+    uint32_t px[N];
+    uint32_t vm = 0;   // valid slots
+    if (DIM == 4 && nx == 4 && ny == 4 && (a.width & 3) == 0) {
+#pragma unroll
+      for (int r = 0; r < DIM; ++r) {
+        const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)(q + (size_t)(y0 + r) * a.width + x0);
+        px[r * DIM + 0] = v.x; px[r * DIM + 1] = v.y; px[r * DIM + 2] = v.z; px[r * DIM + 3] = v.w;
+      }
+      vm = (1u << N) - 1u;
+    } else {
+#pragma unroll
+      for (int r = 0; r < DIM; ++r)
+#pragma unroll
+        for (int c = 0; c < DIM; ++c) {
+          const bool ok = (uint32_t)r < ny && (uint32_t)c < nx;
+          vm |= (ok ? 1u : 0u) << (r * DIM + c);
+          px[r * DIM + c] = ok ? q[(size_t)(y0 + r) * a.width + x0 + c] : 0u;
+        }
+    }
+    // one iteration per distinct colour, in first-occurrence order
+    uint32_t rem = vm, best = 0, best_c = 0, nbest = 0, d = 0;
+    while (rem) {
+      const int s0 = __builtin_ctz(rem);
+      uint32_t k = px[0];
+#pragma unroll
+      for (int i = 1; i < N; ++i) k = s0 == i ? px[i] : k;
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 0; i < N; ++i) m |= (px[i] == k ? 1u : 0u) << i;
+      m &= rem;
+      const uint32_t c = (uint32_t)__popc(m);
+      rem &= ~m;
+      ++d;
+      if (c > best_c) {
+        best = k;
+        best_c = c;
+        nbest = 1;
+      } else if (c == best_c) {
+        ++nbest;
+      }
+    }
+    queue = d > 1 && (nbest > 1 || a.keys);   // needs the iteration order
+    if (!queue) {
+      // one colour (the reference's all-same shortcut, :509-520) or a unique maximum
+      a.mode[b] = best;
+      if (a.ndistinct) a.ndistinct[b] = d;
+      if (a.keys) {   // d == 1 here
+        a.keys[(uint64_t)b * N] = best;
+        a.counts[(uint64_t)b * N] = best_c;
+      }
+    }
+  }
+  // one atomic per wave on one of kBhQueues counters (a single counter
+  // serialises ~8K same-address atomics per 4K frame: ~50 us, dq_kernels.h)
+  const uint64_t m = __ballot(queue);
+  if (m == 0) return;
+  const uint32_t lane = __lane_id(), qi = blockIdx.x % kBhQueues;
+  uint32_t base = 0;
+  if (lane == (uint32_t)__builtin_ctzll(m))
+    base = atomicAdd(a.work_n + qi * kBhQueueStride, (uint32_t)__popcll(m));
+  base = __shfl(base, __builtin_ctzll(m));
+  if (queue) a.work[qi * a.queue_cap + base + __popcll(m & ((1ull << lane) - 1))] = b;
+}
+
+template <int DIM>
+__global__ __launch_bounds__(256) void block_rank_kernel(BlockHistArgs a) {
+  constexpr int N = DIM * DIM;
+  const uint32_t w = blockIdx.x * 256u + threadIdx.x, qi = blockIdx.y;
+  if (w >= a.work_n[qi * kBhQueueStride]) return;
+  const uint32_t b = a.work[qi * a.queue_cap + w];
+  const uint32_t by = b / a.block_w, bx = b - by * a.block_w;
+  uint32_t px[N], cnt[N];
+  int ins[N], d, rank[N];
+  block_slots<DIM>(a, bx, by, px, ins, cnt, d);
+  stl_rank_slots<N>(px, ins, d, rank);
+  uint32_t best = px[0], best_c = 0;
+  int best_r = N;
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (ins[i] >= 0 && (cnt[i] > best_c || (cnt[i] == best_c && rank[i] < best_r))) {
+      best = px[i];
+      best_c = cnt[i];
+      best_r = rank[i];
+    }
+  a.mode[b] = best;
+  if (a.ndistinct) a.ndistinct[b] = (uint32_t)d;
+  if (a.keys) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (ins[i] >= 0) {
+        a.keys[(uint64_t)b * N + rank[i]] = px[i];
+        a.counts[(uint64_t)b * N + rank[i]] = cnt[i];
+      }
+  }
+}
+
+template <int DIM>
+static void launch_block_hist_dim(const BlockHistArgs& a, dim3 grid, hipStream_t stream) {
+  block_hist_kernel<DIM><<<grid, dim3(256), 0, stream>>>(a);
+  block_rank_kernel<DIM><<<dim3((a.queue_cap + 255) / 256, kBhQueues), dim3(256), 0, stream>>>(a);
+}
+
+size_t block_hist_scratch_words(uint32_t block_w, uint32_t block_h) {
+  const uint64_t nwg = ((uint64_t)block_w * block_h + 255) / 256;
+  return (size_t)kBhQueues * kBhQueueStride + (size_t)kBhQueues * ((nwg + kBhQueues - 1) / kBhQueues) * 256;
+}
+
+int launch_block_hist(const BlockHistArgs& a0, int dim, hipStream_t stream) {
+  const uint64_t nb = (uint64_t)a0.block_w * a0.block_h;
+  if (nb == 0) return 0;
+  BlockHistArgs a = a0;   // a.work_n: kBhQueues counters, then the queues
+  const uint64_t nwg = (nb + 255) / 256;
+  a.queue_cap = (uint32_t)(((nwg + kBhQueues - 1) / kBhQueues) * 256);
+  a.work = a.work_n + kBhQueues * kBhQueueStride;
+  if (hipMemsetAsync(a.work_n, 0, (size_t)kBhQueues * kBhQueueStride * 4, stream) != hipSuccess)
+    return -2;
+  const dim3 grid((uint32_t)nwg);
+  switch (dim) {
+    case 1: launch_block_hist_dim<1>(a, grid, stream); break;
+    case 2: launch_block_hist_dim<2>(a, grid, stream); break;
+    case 3: launch_block_hist_dim<3>(a, grid, stream); break;
+    case 4: launch_block_hist_dim<4>(a, grid, stream); break;
+    default: return -1;
+  }
+  return 0;
 }
 
 }  // namespace dq

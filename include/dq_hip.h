@@ -37,6 +37,26 @@ int dq_hip_quant(const uint32_t *in, uint32_t n, uint32_t *out, uint32_t *k,
 int dq_hip_map(const uint32_t *in, uint32_t n, uint32_t *out,
                const uint32_t *ct, int k);
 
+/* genHistogramsForBlocks (ClusteringSegmentation.cpp:365-576) without the
+ * OpenCV Mats: map the W x H frame `in` (0x00RRGGBB, Vec3BToUID packing,
+ * OpenCVUtil.h:19-27) onto `palette` (npal colours; the app passes
+ * getSubdividedColors, see dq_subdivided_colors) with map_colors_mps, then per
+ * block of dim x dim pixels (block_w x block_h blocks, row-major) the most
+ * frequent mapped colour, ties broken by the reference's unordered_map
+ * iteration order.  mode: block_w*block_h words = HistogramForBlock::
+ * regionQuantPixel (and the BGR of blockMat).  Optional (NULL to skip):
+ * quant (W*H mapped frame), ndistinct (per block table size), keys/counts
+ * (block_w*block_h*dim*dim words: each block's pixelToCountTable in iteration
+ * order).  dim 1..4 (the app uses 4, ClusteringSegmentationMain.cpp:138);
+ * every block must hold a pixel.  Returns 0 or < 0. */
+int dq_hip_block_hist(const uint32_t *in, uint32_t width, uint32_t height,
+                      const uint32_t *palette, int npal, uint32_t dim,
+                      uint32_t block_w, uint32_t block_h, uint32_t *quant,
+                      uint32_t *mode, uint32_t *ndistinct, uint32_t *keys,
+                      uint32_t *counts);
+/* getSubdividedColors (superpixels/OpenCVUtil.cpp:853-897): 125 colours. */
+void dq_subdivided_colors(uint32_t *out125);
+
 /* ---- device-pointer entry points (inputs already resident in HBM) --------
  * d_in/d_out: device pointers on `device`; k/ct: host.  Synchronous with
  * respect to the host on return (ct and *k are final). */
@@ -51,6 +71,15 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t *const *d_in,
                            const uint32_t *n, uint32_t *const *d_out, uint32_t k,
                            uint32_t *ct, uint32_t *k_out, int max_iters,
                            void *stream);
+/* dq_hip_block_hist on device pointers (in, quant, mode, ndistinct, keys,
+ * counts; quant is required: the mapped frame); palette is host memory.
+ * Asynchronous on `stream`. */
+int dq_hip_block_hist_dev(int device, const uint32_t *d_in, uint32_t width,
+                          uint32_t height, const uint32_t *palette, int npal,
+                          uint32_t dim, uint32_t block_w, uint32_t block_h,
+                          uint32_t *d_quant, uint32_t *d_mode,
+                          uint32_t *d_ndistinct, uint32_t *d_keys,
+                          uint32_t *d_counts, void *stream);
 /* Row-tile sharding.  Frame i's rows are d_in[i] (n[i] points,
  * width[i] per row; width NULL or 0: shard boundaries on 4-point multiples).
  * Inside this process the rows are split into nshard (1..8) row ranges that

@@ -34,6 +34,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -337,6 +338,61 @@ int dqo_quant_recurse(uint32_t n, const uint32_t* in, uint32_t* out,
   *k_inout = m;
   dqo_map(in, n, out, ct, (int)m);
   return empty;
+}
+
+// getSubdividedColors restated (superpixels/OpenCVUtil.cpp:853-897): the 5^3
+// cube {0,63,127,191,255}, R outermost, B innermost, alpha 0xFF.
+void dqo_subdivided_colors(uint32_t* out125) {
+  static const uint32_t v[5] = {0, 63, 127, 191, 255};
+  int i = 0;
+  for (int r = 0; r < 5; ++r)
+    for (int g = 0; g < 5; ++g)
+      for (int b = 0; b < 5; ++b)
+        out125[i++] = 0xFF000000u | (v[r] << 16) | (v[g] << 8) | v[b];
+}
+
+// genHistogramsForBlocks' block loop restated (ClusteringSegmentation.cpp:
+// 420-563) over an already mapped frame `quant` (W*H, 0x00RRGGBB): per block
+// of dim x dim pixels (clipped at the right/bottom edge, row-major inside the
+// block) a std::unordered_map<uint32_t,uint32_t> histogram, filled in pixel
+// order, then the FIRST entry in the map's iteration order with the largest
+// count wins (strict '>' from maxCount 0).  The same container type is used on
+// purpose: the tie-break is its (libstdc++) iteration order.  keys/counts
+// (optional, [nblocks*dim*dim]) receive the table in iteration order,
+// ndistinct (optional) its size.
+void dqo_block_hist(const uint32_t* quant, uint32_t width, uint32_t height,
+                    uint32_t block_w, uint32_t block_h, uint32_t dim, uint32_t* mode,
+                    uint32_t* ndistinct, uint32_t* keys, uint32_t* counts) {
+  const uint32_t cap = dim * dim;
+  for (uint32_t by = 0; by < block_h; ++by)
+    for (uint32_t bx = 0; bx < block_w; ++bx) {
+      const uint64_t b = (uint64_t)by * block_w + bx;
+      std::vector<uint32_t> px;
+      for (uint32_t y = by * dim; y < by * dim + dim; ++y)
+        for (uint32_t x = bx * dim; x < bx * dim + dim; ++x)
+          if (x < width && y < height) px.push_back(quant[(size_t)y * width + x]);
+      std::unordered_map<uint32_t, uint32_t> table;
+      bool same = true;
+      for (uint32_t p : px) same = same && p == px[0];
+      if (same) {
+        table[px[0]] = (uint32_t)px.size();  // the reference's all-same shortcut (:509-520)
+      } else {
+        for (uint32_t p : px) table[p] += 1;
+      }
+      uint32_t best = 0, best_n = 0, i = 0;
+      for (const auto& kv : table) {
+        if (kv.second > best_n) {
+          best_n = kv.second;
+          best = kv.first;
+        }
+        if (keys) keys[b * cap + i] = kv.first;
+        if (counts) counts[b * cap + i] = kv.second;
+        ++i;
+      }
+      if (same) best = px[0];
+      mode[b] = best;
+      if (ndistinct) ndistinct[b] = i;
+    }
 }
 
 }  // extern "C"
