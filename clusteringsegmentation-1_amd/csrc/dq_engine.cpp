@@ -203,7 +203,7 @@ void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t s
   // before any of these buffers moves.
   const bool grow = staging_bytes > cap_stage_tab_ || nnodes > cap_res_ ||
                     (size_t)max_iters > cap_stat_ || ntiles > cap_parts_ ||
-                    nptiles > cap_sparts_ || ntiles * kTileWaves > cap_wparts_ || !h_stage_ || !h_res_ || !h_stat_ || !d_parts_ ||
+                    2 * nptiles > cap_sparts_ || ntiles * kTileWaves > cap_wparts_ || !h_stage_ || !h_res_ || !h_stat_ || !d_parts_ ||
                     !d_sparts_;
   if (!grow) return;
   DQ_HIP(hipStreamSynchronize(stream));
@@ -217,7 +217,7 @@ void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t s
   grow_coherent(&h_stat_, &d_stat_, &cap_stat_, (size_t)max_iters);
   grow_device(&d_parts_, &cap_parts_, ntiles);
   grow_device(&d_wparts_, &cap_wparts_, ntiles * kTileWaves);
-  grow_device(&d_sparts_, &cap_sparts_, std::max<size_t>(nptiles, 1));
+  grow_device(&d_sparts_, &cap_sparts_, std::max<size_t>(2 * nptiles, 2));
 }
 
 // Wait for the status word of 2-means iteration `it` of round `seq`; returns
@@ -333,8 +333,9 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   const size_t o_tiles = al(nr * sizeof(DevNode));
   const size_t o_pt = o_tiles + al(ntiles * sizeof(Tile));
   const size_t o_ctr = o_pt + al(nptiles * sizeof(PartTile));
-  const size_t bytes = o_ctr + al((size_t)max_iters * sizeof(LaunchCtr));
-  ensure_round(nr, ntiles, nptiles, bytes, max_iters, stream);
+  // (LaunchCtr and status word max_iters: the split epilogue's)
+  const size_t bytes = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
+  ensure_round(nr, ntiles, nptiles, bytes, max_iters + 1, stream);
   if (sharded && (size_t)nl * 8 > cap_tot_) {
     DQ_HIP(hipStreamSynchronize(stream));
     if (d_tot_) DQ_HIP(hipFree(d_tot_));
@@ -375,6 +376,8 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       thr = split_threshold(cut);
       shift = 16 - 8 * axis;
     }
+    nodes_[order[a]].axis = (int16_t)((16 - shift) >> 3);
+    nodes_[order[a]].thr = (int16_t)thr;
     for (int sh = 0; sh < S; ++sh) {
       DevNode& d = hn[a * S + sh];
       d.src = buf_ptr(n.buf, fs, sh);
@@ -395,8 +398,10 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       for (int c = 0; c < 3; ++c) { d.tm[c] = n.mean[c]; d.tv[c] = n.var[c]; }
       d.prm.thr = thr;
       d.prm.shift = shift;
+      for (int c = 0; c < 3; ++c) { d.box_lo[c] = n.lo[c]; d.box_hi[c] = n.hi[c]; }
       d.tile_begin = t;
       const uint64_t tln = tile_len(sg.len);
+      d.tile_len = (uint32_t)tln;
       for (uint64_t o = 0; o == 0 || o < sg.len; o += tln) {
         Tile& tt = ht[t++];
         tt.node = a * S + sh;
@@ -427,6 +432,10 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
           pt.thr[1] = thr[1];
           pt.shift[0] = shift[0];
           pt.shift[1] = shift[1];
+          for (int c = 0; c < 2; ++c) {
+            const int sl = slot_of_[ch[c]];
+            pt.child[c] = sl >= 0 ? sl * S + sh : -1;
+          }
         }
       }
     }
@@ -483,17 +492,23 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     pass(PASS_INIT, ST_INIT, -1, nt, bytes_all);
     epilogue(PASS_INIT, -1);
   }
+  // the split pass's per-(tile, wave) counts: own split passes store theirs,
+  // partsplit adds the fused children's up
+  if (nptiles > 0) DQ_HIP(hipMemsetAsync(d_wparts_, 0, ntiles * kTileWaves * sizeof(uint32_t), stream));
   pass(PASS_SPLIT, ST_SPLIT, -1, (int)nt_own, 4.0 * (double)own_total);
   if (nptiles > 0) {
     timed_begin(stream);
     launch_partsplit(ra, (int)nptiles, stream);
     timed_end(ST_PARTITION, 8.0 * (double)parent_total, stream);
   }
-  epilogue(PASS_SPLIT, -1);
+  epilogue(PASS_SPLIT, max_iters);
+  // Splits the epilogue proved final (cut_is_fixed_point) need no 2-means
+  // pass: when that is all of them, the round ends here.
+  const bool all_proven = fixed_point_ && wait_status(max_iters, seq, stream) == 0;
   // 2-means iterations, `lookahead_` launched past the one whose status the
   // host waits for; stop as soon as every node is final.
   int launched = 0, known = 0;
-  while (true) {
+  while (!all_proven) {
     while (launched < max_iters && launched <= known + lookahead_) {
       const bool last = launched == max_iters - 1;
       pass(last ? PASS_KLAST : PASS_KMEANS, last ? ST_KLAST : ST_KMEANS, launched, nt, bytes_all);
@@ -513,7 +528,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     uint64_t px = 0;
     for (int a = 0; a < nl; ++a) {
       const int di = h_res_[a * S].done_it;
-      if (di <= 0 || it < di)
+      if (!h_res_[a * S].proven && (di <= 0 || it < di))
         for (int sh = 0; sh < S; ++sh) px += seg(order[a], sh).len;
     }
     return px;
@@ -533,6 +548,13 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     const NodeResult& r = h_res_[a * S];   // global results: every record agrees
     if (root_round) {
       for (int c = 0; c < 3; ++c) { nodes_[id].mean[c] = r.tm[c]; nodes_[id].var[c] = r.tv[c]; }
+      // the cut the INIT epilogue chose on the device, same comparisons
+      double maxv = r.tv[0], cut = r.tm[0];
+      int axis = 0;
+      if (maxv < r.tv[1]) { maxv = r.tv[1]; axis = 1; cut = r.tm[1]; }
+      if (maxv < r.tv[2]) { axis = 2; cut = r.tm[2]; }
+      nodes_[id].axis = (int16_t)axis;
+      nodes_[id].thr = (int16_t)split_threshold(cut);
     }
     Node co, cn;
     const int io = (int)nodes_.size();
@@ -553,6 +575,14 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       cn.glen = r.n_new;
       co.glen = p.glen - r.n_new;
       co.buf = cn.buf = child_buf(p.buf);
+      for (int c = 0; c < 3; ++c) {
+        co.lo[c] = cn.lo[c] = p.lo[c];
+        co.hi[c] = cn.hi[c] = p.hi[c];
+      }
+      if (r.proven) {   // the halves are the cut's: v_axis < thr | >= thr
+        co.hi[p.axis] = (int16_t)std::min<int>(p.hi[p.axis], p.thr - 1);
+        cn.lo[p.axis] = (int16_t)std::max<int>(p.lo[p.axis], p.thr);
+      }
     }
     nodes_.push_back(co);
     nodes_.push_back(cn);

@@ -54,6 +54,11 @@ struct Node {
   double var[3] = {0, 0, 0};         // var[]      (:314)
   double tse = 0.0;                  // tse[]      (:304)
   uint64_t glen = 0;                 // size[] of the cluster (all shards, all processes)
+  // a box holding every point (channel R, G, B): the cube for a root, the
+  // parent's for a child, clipped at the parent's cut when the parent's
+  // halves are proven to be the cut's (DevNode::box_lo)
+  int16_t lo[3] = {0, 0, 0}, hi[3] = {255, 255, 255};
+  int16_t axis = 0, thr = 0;         // the split's cut, once run (for the children's boxes)
 };
 
 // A node's local segment in one shard, and -- once the node has been split --

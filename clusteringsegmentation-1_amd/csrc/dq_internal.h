@@ -74,7 +74,12 @@ struct alignas(16) DevNode {
   uint32_t n_new_local;     // final new-half size in this shard (partition)
   int32_t iter;             // 2-means iterations completed (epilogue count)
   int32_t done_it;          // 0: active; else 1 + the iteration found at the fixed point
-  int32_t pad1;
+  uint32_t tile_len;        // this record's tiles: [off + k*tile_len, ...) (last one shorter)
+  // --- a box holding every point of the node (channel c: R, G, B), from the
+  //     host: the root's is the cube, a child's is its parent's, clipped at
+  //     the parent's cut when the parent's halves are proven to be the cut's
+  //     (split epilogue, cut_is_fixed_point)
+  int32_t box_lo[3], box_hi[3];
 };
 
 // The split's results, written by the finalising epilogue straight into
@@ -88,12 +93,14 @@ struct alignas(16) NodeResult {
   uint64_t n_new;           // new_size (:820-821), global
   uint32_t n_new_local;     // new half in this shard
   int32_t done_it;          // see DevNode
+  int32_t proven;           // 1: final at the split epilogue -- the halves are the cut's
+  int32_t pad;
 };
 
 // One workgroup's share of a pass.  Inside a tile, wave w of the workgroup
-// owns the points vs + 4*(j*kBlock + w*64 + lane) + e of every sweep vs (the
-// same in every kernel), so the final pass's per-wave counts let each wave
-// of the partition write its points with no block-level synchronisation.
+// owns a contiguous range of it (dq_kernels.hip, wave_range: the same in
+// every kernel), so the final pass's per-wave counts let each wave of the
+// partition write its points with no block-level synchronisation.
 constexpr int kTileWaves = 4;
 struct alignas(16) Tile {
   int32_t node;             // index into the round's DevNode array
@@ -108,11 +115,17 @@ struct alignas(16) Tile {
 // parent node split in an EARLIER round.  Its points are written to the two
 // children's segments (replaying the parent's final decision) and each
 // child's split-pass statistics (:438-559) are accumulated on the way.
+// Besides the children's split sums (count, sums, sums of squares of each
+// child's new side: 2 x TilePartial per PartTile) it adds each child's
+// per-(tile, wave) counts of its split-pass halves into Tile-wave words of
+// RoundArgs::wparts (old | new << 16, zeroed for the round): the partition
+// cursors of a child whose split turns out final at its split epilogue.
 struct alignas(32) PartTile {
   const Tile* tile;         // the parent's tile (cursors final)
   const DevNode* parent;    // the parent's record
   int32_t thr[2];           // children's split thresholds (256: child not split this round)
   int32_t shift[2];
+  int32_t child[2];         // the children's records in this round (-1: not split in it)
 };
 
 // Per-launch completion counters of the round's 2-means epilogues (device

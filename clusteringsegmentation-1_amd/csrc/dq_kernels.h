@@ -12,7 +12,8 @@ namespace dq {
 
 constexpr int kBlock = 64 * kTileWaves;          // 4 wave64 per workgroup
 constexpr int kVecPerThread = 4;                // uint4 loads per lane per sweep
-constexpr int kSweep = kBlock * kVecPerThread * 4;   // 4096 points per sweep
+constexpr int kSweep = kBlock * kVecPerThread * 4;   // 4096 points: tile lengths are multiples
+constexpr int kWaveSweep = 64 * kVecPerThread * 4;   // 1024 points: one wave's sweep
 constexpr uint32_t kMaxTilePx = 16 * kSweep;    // keeps packed 16-bit lane sums exact
 
 // Map (nearest palette entry) cell grid: 32 cells of 8 values per channel.
@@ -28,15 +29,17 @@ struct RoundArgs {
   Tile* tiles;              // the round's tiles (kept: a later round partitions through them)
   DevNode* nodes;           // the round's node records (kept, as tiles)
   TilePartial* parts;       // one per tile, rewritten by every pass
-  uint32_t* wparts;         // per (tile, wave): old | new << 16 of the last 2-means pass
+  uint32_t* wparts;         // per (tile, wave): old | new << 16 of the last pass (the
+                            //   split pass's: own split pass, or added up by partsplit)
   const PartTile* ptiles;   // fused partition + split work of this round
-  TilePartial* sparts;      // one per PartTile
+  TilePartial* sparts;      // two per PartTile (old child, new child)
   NodeResult* hres;         // host-coherent pinned: final results per node
-  LaunchCtr* ctr;           // per 2-means iteration
-  uint64_t* hstat;          // host-coherent pinned: status word per 2-means iteration
+  LaunchCtr* ctr;           // per 2-means iteration, then one for the split epilogue
+  uint64_t* hstat;          // host-coherent pinned: status word per 2-means iteration,
+                            //   then the split epilogue's (index max_iters)
   uint64_t seq;             // round sequence number (tags the status words)
   int32_t fixed_point;      // epilogues finalise nodes at a 2-means fixed point
-  int32_t it;               // 2-means iteration of an epilogue launch
+  int32_t it;               // 2-means iteration of an epilogue launch (split: max_iters)
   int32_t nn;               // node records in the round (logical nodes x shards)
   // sharded rounds (a frame split into row ranges, one record per shard):
   uint64_t* tot;            // per logical node: 8 u64 totals (nodesum, then allreduce)

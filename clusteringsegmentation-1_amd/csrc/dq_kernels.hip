@@ -55,7 +55,8 @@ __device__ __forceinline__ g_cu32* as_g(const uint32_t* p) { return (g_cu32*)p; 
 __device__ __forceinline__ g_u32* as_gw(uint32_t* p) { return (g_u32*)p; }
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ uint32_t wave_id() { return threadIdx.x >> 6; }
+// (readfirstlane: provably wave-uniform, so values derived from it stay scalar)
+__device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -149,16 +150,30 @@ __device__ __forceinline__ bool stays_old(uint32_t p, const Params& q) {
 
 __device__ __forceinline__ uint32_t vec_elem(const u32x4& v, int e) { return v[e]; }
 
-// This lane's kVecPerThread uint4 of the sweep starting at vs (16-B aligned).
-// FULL: the whole sweep lies inside the tile.  Otherwise vectors starting at
-// or past `end` are not loaded; a vector straddling `end` is loaded whole --
-// every working buffer keeps >= 3 readable words of slack past each frame.
+// Wave w of a workgroup owns the contiguous range [ws, we) of its tile
+// [start, end): four ranges of q = ceil(len / 4096) * 1024 points (the last
+// ones cut at `end`, possibly empty).  Every kernel sweeping tiles, and the
+// partition's per-(tile, wave) cursors, use this ownership.  A wave sweeps
+// its range in sweeps of kWaveSweep points from ws & ~3; lane l holds the
+// uint4 at vs + 4 * (j * 64 + l), j < kVecPerThread.
+__device__ __forceinline__ void wave_range(uint32_t start, uint32_t end, uint32_t w,
+                                           uint32_t& ws, uint32_t& we) {
+  const uint32_t q = ((end - start + kSweep - 1) / kSweep) * kWaveSweep;
+  ws = min(start + w * q, end);
+  we = min(ws + q, end);
+}
+
+// This lane's kVecPerThread uint4 of the wave sweep starting at vs (16-B
+// aligned).  FULL: the whole sweep lies inside the range.  Otherwise vectors
+// starting at or past `end` are not loaded; a vector straddling `end` is
+// loaded whole -- every working buffer keeps >= 3 readable words of slack
+// past each frame.
 template <bool FULL>
 __device__ __forceinline__ void load_sweep(g_cu4* src4, uint32_t vs, uint32_t end,
                                            u32x4 v[kVecPerThread]) {
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
-    const uint32_t i = vs + 4u * (j * kBlock + threadIdx.x);
+    const uint32_t i = vs + 4u * (j * 64 + lane_id());
     if (FULL || i < end) v[j] = src4[i >> 2];
     else v[j] = (u32x4){0u, 0u, 0u, 0u};
   }
@@ -197,9 +212,10 @@ __device__ __forceinline__ void add4(const uint32_t m[4], LaneSums& s) {
   s.qb = __builtin_amdgcn_udot4(bq, bq, s.qb, false);
 }
 
-// The split pass needs only the new side's count and sums (:438-559).
+// The split pass's new side: count, sums (:438-559) and sums of squares (the
+// results of a split proven final at its epilogue, cut_is_fixed_point).
 struct SplitSums {
-  uint32_t cnt = 0, sr = 0, sg = 0, sb = 0;
+  uint32_t cnt = 0, sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
 };
 
 __device__ __forceinline__ void add4_sums(const uint32_t m[4], SplitSums& s) {
@@ -212,6 +228,9 @@ __device__ __forceinline__ void add4_sums(const uint32_t m[4], SplitSums& s) {
   s.sr = __builtin_amdgcn_udot4(rq, 0x01010101u, s.sr, false);
   s.sg = __builtin_amdgcn_udot4(gq, 0x01010101u, s.sg, false);
   s.sb = __builtin_amdgcn_udot4(bq, 0x01010101u, s.sb, false);
+  s.qr = __builtin_amdgcn_udot4(rq, rq, s.qr, false);
+  s.qg = __builtin_amdgcn_udot4(gq, gq, s.qg, false);
+  s.qb = __builtin_amdgcn_udot4(bq, bq, s.qb, false);
 }
 
 template <int KIND, bool FULL>
@@ -221,7 +240,7 @@ __device__ __forceinline__ void sweep_sums(const u32x4 v[kVecPerThread], uint32_
   if (FULL) s.vcnt += kVecPerThread * 4;
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
-    const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
+    const uint32_t i0 = vs + 4u * (j * 64 + lane_id());
     uint32_t m[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -267,6 +286,39 @@ __device__ void node_results(NodeResult* r, const DevNode* w, const uint64_t t[F
   r->n_new = t[F_CNT];
 }
 
+// Is the first 2-means iteration after the split a fixed point, for every
+// point the node can hold?  p is that iteration's decision (old iff lhs <
+// rr*R + rg*G + rb*B, :683), the split sent v_axis >= thr new (:438-559).
+// On the node's box (w->box_lo/hi) the decision is checked at the corners of
+// both halves of the cut: every point with v_axis >= thr must go new (max of
+// the linear form <= lhs - margin) and every other point must stay old (min
+// >= lhs + margin).  The margin 1e-12*M dwarfs the FP64 evaluation's error
+// (< 4*2^-53*M, decision_from_means), so each point's exact outcome equals
+// the cut's.  Then the iteration's halves -- hence its exact integer sums --
+// are the split's, the next decision is p again, and the results are what
+// the first 2-means epilogue would publish as a fixed point.
+__device__ bool cut_is_fixed_point(const DevNode* w, const Params& p) {
+  const double M = (fabs(p.rr) + fabs(p.rg) + fabs(p.rb)) * 255.0 + fabs(p.lhs);
+  if (!(M > 1e-30 && M < 1e30)) return false;
+  const double mg = 1e-12 * M;
+  const double c[3] = {p.rr, p.rg, p.rb};
+  const int axis = (16 - p.shift) >> 3;
+  for (int side = 0; side < 2; ++side) {   // 0: the cut's old half, 1: its new half
+    int lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) { lo[k] = w->box_lo[k]; hi[k] = w->box_hi[k]; }
+    if (side) lo[axis] = max(lo[axis], p.thr);
+    else hi[axis] = min(hi[axis], p.thr - 1);
+    if (lo[axis] > hi[axis]) continue;   // the box holds no point of this half
+    double ext = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const double a = c[k] * (double)lo[k], b = c[k] * (double)hi[k];
+      ext += side ? fmax(a, b) : fmin(a, b);
+    }
+    if (side ? !(ext <= p.lhs - mg) : !(ext >= p.lhs + mg)) return false;
+  }
+  return true;
+}
+
 // The FP64 update after pass KIND from the node's total sums t[] (exact
 // integers).  Publishes the next pass's Params, or -- when the results are
 // final (PASS_KLAST, or a PASS_KMEANS at a fixed point: prm then already
@@ -310,12 +362,21 @@ __device__ bool node_update(DevNode* w, NodeResult* r, const uint64_t t[F_NUM], 
   if (final) {
     node_results(r, w, t, om, nm, nw, ow);
     w->done_it = KIND == PASS_KMEANS ? w->iter : -1;
+    r->proven = 0;
     return true;
   }
   for (int c = 0; c < 4; ++c) w->prev[c] = t[F_CNT + c];
   Params p = w->prm;
   decision_from_means(om, nm, &p);
   w->prm = p;
+  if (KIND == PASS_SPLIT && fixed_point && t[F_CNT] != 0 && ow > 0.0 && cut_is_fixed_point(w, p)) {
+    // exactly the first 2-means epilogue's fixed-point branch on sums t
+    w->iter = 1;
+    node_results(r, w, t, om, nm, nw, ow);
+    w->done_it = 1;
+    r->proven = 1;
+    return true;
+  }
   return false;
 }
 
@@ -338,20 +399,22 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
   __shared__ uint32_t red[kBlock / 64][8];
   LaneSums s;
   u32x4 v[kVecPerThread];
-  for (uint32_t vs = t.start & ~3u; vs < t.end; vs += kSweep) {
-    if (vs >= t.start && vs + kSweep <= t.end) {   // wave-uniform
-      load_sweep<true>(src4, vs, t.end, v);
-      sweep_sums<KIND, true>(v, vs, t.start, t.end, q, s);
+  uint32_t ws, we;
+  wave_range(t.start, t.end, wave_id(), ws, we);
+  for (uint32_t vs = ws & ~3u; vs < we; vs += kWaveSweep) {
+    if (vs >= ws && vs + kWaveSweep <= we) {   // wave-uniform
+      load_sweep<true>(src4, vs, we, v);
+      sweep_sums<KIND, true>(v, vs, ws, we, q, s);
     } else {
-      load_sweep<false>(src4, vs, t.end, v);
-      sweep_sums<KIND, false>(v, vs, t.start, t.end, q, s);
+      load_sweep<false>(src4, vs, we, v);
+      sweep_sums<KIND, false>(v, vs, ws, we, q, s);
     }
   }
 
   uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
 #pragma unroll
   for (int k = 0; k < kNF; ++k) f[k] = wave_sum_u32(f[k]);
-  if (KIND == PASS_KMEANS || KIND == PASS_KLAST) {
+  if (KIND != PASS_INIT) {
     // this wave's (old, new) counts: the partition cursors if this pass is final
     const uint32_t vsum = wave_sum_u32(s.vcnt);
     if (lane_id() == 0) a.wparts[blockIdx.x * kTileWaves + wave_id()] = (vsum - f[F_CNT]) | (f[F_CNT] << 16);
@@ -377,21 +440,24 @@ template <int KIND, int W = kBlock>
 __device__ __forceinline__ void sum_record(const RoundArgs& a, const DevNode* w, uint64_t acc[7],
                                            int tid = (int)threadIdx.x) {
   if (KIND == PASS_SPLIT && w->split_pb >= 0) {
-    // children's (cnt, sums) of the fused pass: [0..3] old half, [4..7] new half
+    // the fused pass's partials of this half: TilePartial 2 * i + side
     const g_cu4* sp4 = (const g_cu4*)a.sparts;
     const int side = w->split_side;
     for (int i = w->split_pb + tid; i < w->split_pe; i += W) {
-      const u32x4 x = sp4[2 * i + side];
+      const u32x4 x = sp4[4 * i + 2 * side], y = sp4[4 * i + 2 * side + 1];
       acc[0] += x[0];
       acc[1] += x[1];
       acc[2] += x[2];
       acc[3] += x[3];
+      acc[4] += y[0];
+      acc[5] += y[1];
+      acc[6] += y[2];
     }
     return;
   }
   const int tb = w->tile_begin, te = w->tile_end;
   const g_cu4* parts4 = (const g_cu4*)a.parts;
-  constexpr bool kSquares = KIND != PASS_SPLIT;
+  constexpr bool kSquares = true;   // (the split pass's: results of a proven split)
   for (int base = tb; base < te; base += 4 * W) {
     u32x4 x[4], y[4];
 #pragma unroll
@@ -467,10 +533,11 @@ __global__ __launch_bounds__(kBlock) void nodesum_kernel(RoundArgs a) {
 //   * a record whose split became final: the partition's per-(tile, wave)
 //     write cursors (a shuffle scan over the lanes' tile chunks), and the
 //     results written straight to host memory (NodeResult);
-//   * 2-means launches: every record arrives on the launch's (sharded)
-//     counter; the last to arrive publishes (round seq, records still
-//     active) to the host, which stops launching iterations once no node is
-//     active.
+//   * 2-means and split launches: every record arrives on the launch's
+//     (sharded) counter; the last to arrive publishes (round seq, records
+//     still active) to the host, which stops launching iterations once no
+//     node is active (after the split: nodes proven final by
+//     cut_is_fixed_point need no 2-means pass at all).
 constexpr int kEpiBlock = 64;
 template <int KIND, bool FROM_TOT>
 __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
@@ -503,7 +570,7 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
       }
     }
     final_results = __shfl(fin, 0, 64) != 0;
-    if (kMeans && final_results) {
+    if ((kMeans || KIND == PASS_SPLIT) && final_results) {
       // Partition cursors: for every (tile, wave) of the node, the OLD and
       // NEW points of the node before its share -- an exclusive shuffle scan
       // of the final pass's per-wave counts, chunked per lane over the tiles.
@@ -536,7 +603,7 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
         }
     }
   }
-  if (kMeans) {
+  if (kMeans || KIND == PASS_SPLIT) {   // (split: proven fixed points, status slot max_iters)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -591,7 +658,7 @@ __device__ __forceinline__ void decide_sweep(const u32x4 v[kVecPerThread], uint3
   const uint32_t epsb = __float_as_uint(q.eps);
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
-    const uint32_t i0 = vs + 4u * (j * kBlock + threadIdx.x);
+    const uint32_t i0 = vs + 4u * (j * 64 + lane_id());
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int sidx = j * 4 + e;
@@ -640,20 +707,158 @@ __device__ __forceinline__ void decide_sweep(const u32x4 v[kVecPerThread], uint3
 // points into the old or the new run (each store instruction covers at most
 // two contiguous runs of the child buffer), with the next sweep's loads in
 // flight.  No LDS and no barrier until the final reduction of the sums.
-// One 32-B partial per tile: [0..3] old child, [4..7] new child.
+// Two 32-B partials per tile: the old child's (count, sums, sums of squares),
+// then the new child's; the children's per-(tile, wave) split counts go to
+// wparts (chunk_run).
+// A child's split-pass (old, new) counts per (tile, wave) of the CHILD's
+// tiling, from the runs of the child buffer one partsplit wave writes in
+// order.  A "chunk" is one wave range of a child tile (wave_range): at least
+// 1024 points, except the segment's last non-empty one, which ends where the
+// segment does -- so a run (<= 64 points) crosses at most one chunk end.  The
+// wave keeps the chunk it is in (wave-uniform) and adds one packed word per
+// chunk (old | new << 16) with one atomic when it leaves it.
+struct ChunkAcc {
+  bool on;                // the child is split this round
+  uint32_t off, len, tl;  // its segment and tile length
+  uint32_t* w0;           // its first tile's wave words in wparts
+  uint32_t k, t0, tend, q;// current child tile, its range, its wave range size
+  uint32_t w, end;        // current wave range and its end (0: none yet)
+  uint32_t acc;
+  uint32_t lnew;          // per LANE: new points of fast sweeps not yet in acc
+};
+
+// (plain pointers: a `const RoundArgs&` parameter made the kernel argument
+// addressable and cost partsplit ~80 VGPRs)
+__device__ __forceinline__ void chunk_init(ChunkAcc& c, const DevNode* nodes, uint32_t* wparts, int rec) {
+  c.on = rec >= 0;
+  const DevNode* ch = nodes + (rec >= 0 ? rec : 0);
+  c.off = ch->off;
+  c.len = ch->len;
+  c.tl = ch->tile_len;
+  c.w0 = wparts + (size_t)ch->tile_begin * kTileWaves;
+  c.k = c.t0 = c.tend = c.q = c.w = c.end = c.acc = c.lnew = 0;
+}
+
+// Fold the lanes' fast-sweep new counts into acc (fast sweeps added all
+// their points as old).
+__device__ __forceinline__ void chunk_reduce(ChunkAcc& c) {
+  const uint32_t nn = wave_sum_u32(c.lnew);
+  c.acc += (nn << 16) - nn;
+  c.lnew = 0;
+}
+
+__device__ __forceinline__ void chunk_flush(ChunkAcc& c) {
+  if (c.acc != 0 && lane_id() == 0) atomicAdd(c.w0 + c.k * kTileWaves + c.w, c.acc);
+  c.acc = 0;
+}
+
+__device__ __forceinline__ void chunk_tile(ChunkAcc& c) {
+  c.t0 = c.off + c.k * c.tl;
+  c.tend = min(c.t0 + c.tl, c.off + c.len);
+  c.q = ((c.tend - c.t0 + kSweep - 1) / kSweep) * kWaveSweep;
+}
+
+// Enter the chunk starting at position p (the first: the one holding p).
+__device__ __forceinline__ void chunk_enter(ChunkAcc& c, uint32_t p) {
+  if (c.end == 0) {
+    c.k = (p - c.off) / c.tl;
+    chunk_tile(c);
+    c.w = (p - c.t0) / c.q;
+  } else if (c.end == c.tend) {   // next tile
+    c.k += 1;
+    chunk_tile(c);
+    c.w = 0;
+  } else {
+    c.w += 1;
+  }
+  c.end = min(c.t0 + (c.w + 1u) * c.q, c.tend);
+}
+
+// Run [run0, run0 + cnt) of this child written by the current slot; newb =
+// ballot of its lanes whose point is new for the child's split; rank = the
+// lane's position in the run (valid where in_run).
+__device__ __forceinline__ void chunk_run(ChunkAcc& c, uint32_t run0, uint32_t cnt, uint64_t newb,
+                                          uint32_t rank, bool in_run) {
+  if (!c.on || cnt == 0) return;
+  if (c.end == 0) chunk_enter(c, run0);
+  const uint32_t nn = (uint32_t)__popcll(newb);
+  if (run0 + cnt <= c.end) {   // common: inside the current chunk
+    c.acc += (cnt - nn) | (nn << 16);
+    return;
+  }
+  // the first `cut` points close the current chunk, the rest open the next
+  const uint32_t cut = c.end > run0 ? c.end - run0 : 0u;
+  const uint32_t n1 = (uint32_t)__popcll(newb & __ballot(in_run && rank < cut));
+  c.acc += (cut - n1) | (n1 << 16);
+  chunk_flush(c);
+  chunk_enter(c, c.end);
+  c.acc += ((cnt - cut) - (nn - n1)) | ((nn - n1) << 16);
+}
+
 #ifndef DQ_PS_WAVES
 #define DQ_PS_WAVES 1
 #endif
 #ifndef DQ_PS_PREFETCH
 #define DQ_PS_PREFETCH 1
 #endif
+// This wave's points of one sweep, slot by slot, ranked by ballot; raw
+// buffer stores (SGPR descriptor + 32-bit offset).  In a full sweep every
+// slot is valid: a lane's rank among the new points is its lane id minus
+// its rank among the old ones (one ballot, one mbcnt pair).  Partial sweeps:
+// out-of-range offsets are dropped by the buffer bounds check, so invalid
+// slots get one.  CHUNKS: split every run over the children's chunks.
+template <bool CHUNKS>
+__device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32_t oldm, uint32_t newm,
+                                            bool full, __amdgpu_buffer_rsrc_t drs, uint32_t l,
+                                            uint32_t xcut, uint32_t ycut, uint32_t& oc, uint32_t& nc,
+                                            ChunkAcc& cx, ChunkAcc& cy) {
+  constexpr int kSlots = kVecPerThread * 4;
+  if (full) {
+#pragma unroll
+    for (int sidx = 0; sidx < kSlots; ++sidx) {
+      const bool o = (oldm >> sidx) & 1u;
+      const uint64_t bo = __ballot(o);
+      const uint32_t ro = mbcnt64(bo);
+      const uint32_t idx = o ? oc + ro : nc + (l - ro);
+      __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
+                                            (int)(idx * 4u), 0, 0);
+      const uint32_t co = (uint32_t)__popcll(bo);
+      if (CHUNKS) {
+        chunk_run(cx, oc, co, __ballot((xcut >> sidx) & 1u), ro, o);
+        chunk_run(cy, nc, 64u - co, __ballot((ycut >> sidx) & 1u), l - ro, !o);
+      }
+      oc += co;
+      nc += 64u - co;
+    }
+  } else {
+#pragma unroll
+    for (int sidx = 0; sidx < kSlots; ++sidx) {
+      const bool o = (oldm >> sidx) & 1u, n = (newm >> sidx) & 1u;
+      const uint64_t bo = __ballot(o), bn = __ballot(n);
+      const uint32_t ro = mbcnt64(bo), rn = mbcnt64(bn);
+      uint32_t idx = o ? oc + ro : nc + rn;
+      idx = (o || n) ? idx : 0x3FFFFFFFu;
+      __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
+                                            (int)(idx * 4u), 0, 0);
+      const uint32_t co = (uint32_t)__popcll(bo), cn = (uint32_t)__popcll(bn);
+      if (CHUNKS) {
+        chunk_run(cx, oc, co, __ballot((xcut >> sidx) & 1u), ro, o);
+        chunk_run(cy, nc, cn, __ballot((ycut >> sidx) & 1u), rn, n);
+      }
+      oc += co;
+      nc += cn;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArgs a) {
   constexpr int kSlots = kVecPerThread * 4;
   const PartTile pt = a.ptiles[blockIdx.x];
   const Tile* tp = pt.tile;
   const DevNode& nd = *pt.parent;
   const uint32_t w = wave_id(), l = lane_id();
-  const uint32_t start = tp->start, end = tp->end;
+  uint32_t start, end;   // this wave's range of the parent tile
+  wave_range(tp->start, tp->end, w, start, end);
   g_cu4* src4 = as_g4(nd.src);
   // child buffer of the frame shard: every index < off + len < 2^30
   const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
@@ -666,10 +871,15 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
   const uint32_t sh0 = (uint32_t)pt.shift[0], sh1 = (uint32_t)pt.shift[1];
   const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
   SplitSums so, sn;
+  ChunkAcc cx, cy;
+  chunk_init(cx, a.nodes, a.wparts, pt.child[0]);
+  chunk_init(cy, a.nodes, a.wparts, pt.child[1]);
+  if (cx.on) chunk_enter(cx, oc);
+  if (cy.on) chunk_enter(cy, nc);
 
   u32x4 v[kVecPerThread];
   uint32_t vs = start & ~3u;
-  bool full = vs >= start && vs + kSweep <= end;
+  bool full = vs >= start && vs + kWaveSweep <= end;
   if (vs < end) {
     if (full) load_sweep<true>(src4, vs, end, v);
     else load_sweep<false>(src4, vs, end, v);
@@ -681,6 +891,7 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
     const uint32_t newm = validm & ~oldm;
     // --- the children's split pass on the same registers: bit arithmetic,
     //     (byte - thr) >> 31 == 0  <=>  byte >= thr  <=>  cut_pos < byte
+    uint32_t xcut = 0, ycut = 0;   // slots new for the old / new child's split
 #pragma unroll
     for (int j = 0; j < kVecPerThread; ++j) {
       uint32_t mo[4], mn[4];
@@ -696,13 +907,15 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
         mn[e] = p & (0u - (sn_new & 1u));
         so.cnt += so_new & 1u;
         sn.cnt += sn_new & 1u;
+        xcut |= (so_new & 1u) << sidx;
+        ycut |= (sn_new & 1u) << sidx;
       }
       add4_sums(mo, so);
       add4_sums(mn, sn);
     }
     // --- next sweep's loads in flight during the stores
-    const uint32_t nvs = vs + kSweep;
-    const bool nfull = nvs >= start && nvs + kSweep <= end;
+    const uint32_t nvs = vs + kWaveSweep;
+    const bool nfull = nvs >= start && nvs + kWaveSweep <= end;
 #if DQ_PS_PREFETCH
     u32x4 vn[kVecPerThread];
     if (nvs < end) {
@@ -710,37 +923,21 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
       else load_sweep<false>(src4, nvs, end, vn);
     }
 #endif
-    // --- this wave's points, slot by slot, ranked by ballot; raw buffer
-    //     stores (SGPR descriptor + 32-bit offset).  In a full sweep every
-    //     slot is valid: a lane's rank among the new points is its lane id
-    //     minus its rank among the old ones (one ballot, one mbcnt pair).
-    //     Partial sweeps: out-of-range offsets are dropped by the buffer
-    //     bounds check, so invalid slots get one.
-    if (full) {
-#pragma unroll
-      for (int sidx = 0; sidx < kSlots; ++sidx) {
-        const bool o = (oldm >> sidx) & 1u;
-        const uint64_t bo = __ballot(o);
-        const uint32_t ro = mbcnt64(bo);
-        const uint32_t idx = o ? oc + ro : nc + (l - ro);
-        __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
-                                              (int)(idx * 4u), 0, 0);
-        const uint32_t co = (uint32_t)__popcll(bo);
-        oc += co;
-        nc += 64u - co;
-      }
+    // --- this wave's points (store_sweep).  A sweep writes at most kWaveSweep points to each child: when neither
+    // child's current chunk can end inside it (fast sweep), only the lanes'
+    // new counts are kept; otherwise every slot's run is split exactly.
+    const bool fast = (!cx.on || oc + kWaveSweep <= cx.end) && (!cy.on || nc + kWaveSweep <= cy.end);
+    if (fast) {
+      const uint32_t oc0 = oc, nc0 = nc;
+      store_sweep<false>(v, oldm, newm, full, drs, l, xcut, ycut, oc, nc, cx, cy);
+      cx.acc += oc - oc0;
+      cy.acc += nc - nc0;
+      cx.lnew += (uint32_t)__builtin_popcount(xcut);
+      cy.lnew += (uint32_t)__builtin_popcount(ycut);
     } else {
-#pragma unroll
-      for (int sidx = 0; sidx < kSlots; ++sidx) {
-        const bool o = (oldm >> sidx) & 1u, n = (newm >> sidx) & 1u;
-        const uint64_t bo = __ballot(o), bn = __ballot(n);
-        uint32_t idx = o ? oc + mbcnt64(bo) : nc + mbcnt64(bn);
-        idx = (o || n) ? idx : 0x3FFFFFFFu;
-        __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
-                                              (int)(idx * 4u), 0, 0);
-        oc += (uint32_t)__popcll(bo);
-        nc += (uint32_t)__popcll(bn);
-      }
+      if (cx.on) chunk_reduce(cx);
+      if (cy.on) chunk_reduce(cy);
+      store_sweep<true>(v, oldm, newm, full, drs, l, xcut, ycut, oc, nc, cx, cy);
     }
 #if DQ_PS_PREFETCH
 #pragma unroll
@@ -755,20 +952,24 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
     full = nfull;
   }
 
-  __shared__ uint32_t red[kTileWaves][8];
-  uint32_t f[8] = {so.cnt, so.sr, so.sg, so.sb, sn.cnt, sn.sr, sn.sg, sn.sb};
+  if (cx.on) { chunk_reduce(cx); chunk_flush(cx); }
+  if (cy.on) { chunk_reduce(cy); chunk_flush(cy); }
+
+  __shared__ uint32_t red[kTileWaves][16];
+  uint32_t f[16] = {so.cnt, so.sr, so.sg, so.sb, so.qr, so.qg, so.qb, 0u,
+                    sn.cnt, sn.sr, sn.sg, sn.sb, sn.qr, sn.qg, sn.qb, 0u};
 #pragma unroll
-  for (int k = 0; k < 8; ++k) f[k] = wave_sum_u32(f[k]);
+  for (int k = 0; k < 16; ++k) f[k] = (k & 7) == 7 ? 0u : wave_sum_u32(f[k]);
   if (l == 0) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) red[w][k] = f[k];
+    for (int k = 0; k < 16; ++k) red[w][k] = f[k];
   }
   __syncthreads();
-  if (threadIdx.x < 8) {
+  if (threadIdx.x < 16) {
     uint32_t x = 0;
 #pragma unroll
     for (int ww = 0; ww < kTileWaves; ++ww) x += red[ww][threadIdx.x];
-    as_gw(a.sparts[blockIdx.x].f)[threadIdx.x] = x;
+    as_gw(a.sparts[2 * blockIdx.x].f)[threadIdx.x] = x;   // (2 TilePartials: 16 words)
   }
 }
 
