@@ -57,6 +57,8 @@ Engine::Engine(int device) : device_(device) {
   if (const char* v = getenv("DQ_HIP_LDS_MAP")) use_lds_map_ = v[0] != '0';
   const char* la = getenv("DQ_HIP_LOOKAHEAD");
   if (la && la[0]) lookahead_ = std::max(0, std::min(8, atoi(la)));
+  const char* sp = std::getenv("DQ_HIP_SPEC_IT0");
+  if (sp && sp[0]) spec_it0_env_ = atoi(sp) != 0 ? 1 : 0;
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
 }
@@ -503,11 +505,21 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   }
   epilogue(PASS_SPLIT, max_iters);
   // Splits the epilogue proved final (cut_is_fixed_point) need no 2-means
-  // pass: when that is all of them, the round ends here.
-  const bool all_proven = fixed_point_ && wait_status(max_iters, seq, stream) == 0;
+  // pass: when that is all of them, the round ends here (latency mode: after
+  // the first iteration, queued meanwhile -- a no-op for proven nodes).
+  int launched = 0, known = 0;
+  bool all_proven = false;
+  if (fixed_point_) {
+    if (spec_it0_) {
+      pass(max_iters == 1 ? PASS_KLAST : PASS_KMEANS, max_iters == 1 ? ST_KLAST : ST_KMEANS, 0, nt,
+           bytes_all);
+      epilogue(max_iters == 1 ? PASS_KLAST : PASS_KMEANS, 0);
+      launched = 1;
+    }
+    all_proven = wait_status(max_iters, seq, stream) == 0;
+  }
   // 2-means iterations, `lookahead_` launched past the one whose status the
   // host waits for; stop as soon as every node is final.
-  int launched = 0, known = 0;
   while (!all_proven) {
     while (launched < max_iters && launched <= known + lookahead_) {
       const bool last = launched == max_iters - 1;
@@ -725,6 +737,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   last_points_full = 0;
   nshard_ = jobs[0].nshard;
   DQ_CHECK(nshard_ >= 1 && nshard_ <= kMaxShard, "shards per frame must be in [1, 8]");
+  spec_it0_ = spec_it0_env_ >= 0 ? spec_it0_env_ == 1 : nframes == 1;
   const int S = nshard_;
   size_t total = 0, align_need = 0;
   for (int i = 0; i < nframes; ++i) {

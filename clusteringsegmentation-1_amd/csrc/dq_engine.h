@@ -242,6 +242,12 @@ class Engine {
   size_t cap_stat_ = 0;
   uint64_t seq_ = 0;                  // round sequence number
   int lookahead_ = 1;                 // 2-means iterations queued past the one awaited
+  // Latency mode (one frame per call, nothing else to overlap the host's
+  // waits): queue the first 2-means iteration before knowing whether the
+  // split epilogue proved every node final (then it is a no-op) instead of
+  // waiting for that status.  DQ_HIP_SPEC_IT0=0/1 forces it off/on.
+  int spec_it0_env_ = -1;
+  bool spec_it0_ = false;
   int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TILES)
   int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_NODE_TILES)
   uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TILE_MAX)

@@ -711,46 +711,23 @@ __device__ __forceinline__ void decide_sweep(const u32x4 v[kVecPerThread], uint3
 // then the new child's; the children's per-(tile, wave) split counts go to
 // wparts (chunk_run).
 // A child's split-pass (old, new) counts per (tile, wave) of the CHILD's
-// tiling, from the runs of the child buffer one partsplit wave writes in
-// order.  A "chunk" is one wave range of a child tile (wave_range): at least
-// 1024 points, except the segment's last non-empty one, which ends where the
-// segment does -- so a run (<= 64 points) crosses at most one chunk end.  The
-// wave keeps the chunk it is in (wave-uniform) and adds one packed word per
-// chunk (old | new << 16) with one atomic when it leaves it.
+// tiling, from the run of the child buffer one partsplit wave writes (its
+// positions only grow, sweep after sweep).  A "chunk" is one wave range of a
+// child tile (wave_range): at least kWaveSweep points, except the segment's
+// last non-empty one, which ends where the segment does -- so the <= 1024
+// points a sweep writes to a child cross at most one chunk end.  The wave
+// keeps the chunk it is in (wave-uniform), counts its points as old in
+// `acc` (old | new << 16) and the new ones per lane in `lnew`, and adds acc
+// with one atomic when it leaves the chunk.
 struct ChunkAcc {
   bool on;                // the child is split this round
   uint32_t off, len, tl;  // its segment and tile length
   uint32_t* w0;           // its first tile's wave words in wparts
   uint32_t k, t0, tend, q;// current child tile, its range, its wave range size
-  uint32_t w, end;        // current wave range and its end (0: none yet)
+  uint32_t w, end;        // current wave range and its end
   uint32_t acc;
-  uint32_t lnew;          // per LANE: new points of fast sweeps not yet in acc
+  uint32_t lnew;          // per LANE: new points of the chunk not yet in acc
 };
-
-// (plain pointers: a `const RoundArgs&` parameter made the kernel argument
-// addressable and cost partsplit ~80 VGPRs)
-__device__ __forceinline__ void chunk_init(ChunkAcc& c, const DevNode* nodes, uint32_t* wparts, int rec) {
-  c.on = rec >= 0;
-  const DevNode* ch = nodes + (rec >= 0 ? rec : 0);
-  c.off = ch->off;
-  c.len = ch->len;
-  c.tl = ch->tile_len;
-  c.w0 = wparts + (size_t)ch->tile_begin * kTileWaves;
-  c.k = c.t0 = c.tend = c.q = c.w = c.end = c.acc = c.lnew = 0;
-}
-
-// Fold the lanes' fast-sweep new counts into acc (fast sweeps added all
-// their points as old).
-__device__ __forceinline__ void chunk_reduce(ChunkAcc& c) {
-  const uint32_t nn = wave_sum_u32(c.lnew);
-  c.acc += (nn << 16) - nn;
-  c.lnew = 0;
-}
-
-__device__ __forceinline__ void chunk_flush(ChunkAcc& c) {
-  if (c.acc != 0 && lane_id() == 0) atomicAdd(c.w0 + c.k * kTileWaves + c.w, c.acc);
-  c.acc = 0;
-}
 
 __device__ __forceinline__ void chunk_tile(ChunkAcc& c) {
   c.t0 = c.off + c.k * c.tl;
@@ -758,13 +735,38 @@ __device__ __forceinline__ void chunk_tile(ChunkAcc& c) {
   c.q = ((c.tend - c.t0 + kSweep - 1) / kSweep) * kWaveSweep;
 }
 
-// Enter the chunk starting at position p (the first: the one holding p).
-__device__ __forceinline__ void chunk_enter(ChunkAcc& c, uint32_t p) {
-  if (c.end == 0) {
+// (plain pointers: a `const RoundArgs&` parameter made the kernel argument
+// addressable and cost partsplit ~80 VGPRs).  Enters the chunk holding p,
+// the wave's first position in the child.
+__device__ __forceinline__ void chunk_init(ChunkAcc& c, const DevNode* nodes, uint32_t* wparts, int rec,
+                                           uint32_t p) {
+  c.on = rec >= 0;
+  const DevNode* ch = nodes + (rec >= 0 ? rec : 0);
+  c.off = ch->off;
+  c.len = ch->len;
+  c.tl = ch->tile_len;
+  c.w0 = wparts + (size_t)ch->tile_begin * kTileWaves;
+  c.acc = c.lnew = 0;
+  c.k = c.w = 0;
+  if (c.on && p < c.off + c.len) {
     c.k = (p - c.off) / c.tl;
     chunk_tile(c);
     c.w = (p - c.t0) / c.q;
-  } else if (c.end == c.tend) {   // next tile
+    c.end = min(c.t0 + (c.w + 1u) * c.q, c.tend);
+  } else {
+    c.end = 0xFFFFFFFFu;   // writes nothing to this child
+  }
+}
+
+// Leave the chunk: fold the lanes' new counts into acc, add acc, step to
+// the next chunk (next wave range, or the next tile's first).
+__device__ __forceinline__ void chunk_next(ChunkAcc& c) {
+  const uint32_t nn = wave_sum_u32(c.lnew);
+  const uint32_t v = c.acc + (nn << 16) - nn;
+  if (v != 0 && lane_id() == 0) atomicAdd(c.w0 + c.k * kTileWaves + c.w, v);
+  c.acc = 0;
+  c.lnew = 0;
+  if (c.end == c.tend) {
     c.k += 1;
     chunk_tile(c);
     c.w = 0;
@@ -774,25 +776,29 @@ __device__ __forceinline__ void chunk_enter(ChunkAcc& c, uint32_t p) {
   c.end = min(c.t0 + (c.w + 1u) * c.q, c.tend);
 }
 
-// Run [run0, run0 + cnt) of this child written by the current slot; newb =
-// ballot of its lanes whose point is new for the child's split; rank = the
-// lane's position in the run (valid where in_run).
-__device__ __forceinline__ void chunk_run(ChunkAcc& c, uint32_t run0, uint32_t cnt, uint64_t newb,
-                                          uint32_t rank, bool in_run) {
-  if (!c.on || cnt == 0) return;
-  if (c.end == 0) chunk_enter(c, run0);
-  const uint32_t nn = (uint32_t)__popcll(newb);
-  if (run0 + cnt <= c.end) {   // common: inside the current chunk
-    c.acc += (cnt - nn) | (nn << 16);
+// Book one sweep's points [p0, p1) of this child: lanecnt = the lane's new
+// points among them, lanepre = those below the chunk end (slow sweeps).
+__device__ __forceinline__ void chunk_sweep(ChunkAcc& c, uint32_t p0, uint32_t p1, uint32_t lanecnt,
+                                            uint32_t lanepre) {
+  if (!c.on) return;
+  if (p1 <= c.end) {
+    c.acc += p1 - p0;
+    c.lnew += lanecnt;
     return;
   }
-  // the first `cut` points close the current chunk, the rest open the next
-  const uint32_t cut = c.end > run0 ? c.end - run0 : 0u;
-  const uint32_t n1 = (uint32_t)__popcll(newb & __ballot(in_run && rank < cut));
-  c.acc += (cut - n1) | (n1 << 16);
-  chunk_flush(c);
-  chunk_enter(c, c.end);
-  c.acc += ((cnt - cut) - (nn - n1)) | ((nn - n1) << 16);
+  const uint32_t before = c.end - p0;
+  c.acc += before;
+  c.lnew += lanepre;
+  chunk_next(c);
+  c.acc = (p1 - p0) - before;
+  c.lnew = lanecnt - lanepre;
+}
+
+__device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
+  if (!c.on) return;
+  const uint32_t nn = wave_sum_u32(c.lnew);
+  const uint32_t v = c.acc + (nn << 16) - nn;
+  if (v != 0 && lane_id() == 0) atomicAdd(c.w0 + c.k * kTileWaves + c.w, v);
 }
 
 #ifndef DQ_PS_WAVES
@@ -806,12 +812,13 @@ __device__ __forceinline__ void chunk_run(ChunkAcc& c, uint32_t run0, uint32_t c
 // slot is valid: a lane's rank among the new points is its lane id minus
 // its rank among the old ones (one ballot, one mbcnt pair).  Partial sweeps:
 // out-of-range offsets are dropped by the buffer bounds check, so invalid
-// slots get one.  CHUNKS: split every run over the children's chunks.
-template <bool CHUNKS>
+// slots get one.  PRE: also count, per lane, the children's split-new points
+// written below the child's chunk end (ex / ey).
+template <bool PRE>
 __device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32_t oldm, uint32_t newm,
                                             bool full, __amdgpu_buffer_rsrc_t drs, uint32_t l,
                                             uint32_t xcut, uint32_t ycut, uint32_t& oc, uint32_t& nc,
-                                            ChunkAcc& cx, ChunkAcc& cy) {
+                                            uint32_t ex, uint32_t ey, uint32_t& ax, uint32_t& ay) {
   constexpr int kSlots = kVecPerThread * 4;
   if (full) {
 #pragma unroll
@@ -822,11 +829,11 @@ __device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32
       const uint32_t idx = o ? oc + ro : nc + (l - ro);
       __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
                                             (int)(idx * 4u), 0, 0);
-      const uint32_t co = (uint32_t)__popcll(bo);
-      if (CHUNKS) {
-        chunk_run(cx, oc, co, __ballot((xcut >> sidx) & 1u), ro, o);
-        chunk_run(cy, nc, 64u - co, __ballot((ycut >> sidx) & 1u), l - ro, !o);
+      if (PRE) {
+        ax += (xcut >> sidx) & (uint32_t)(idx < ex);
+        ay += (ycut >> sidx) & (uint32_t)(idx < ey) & 1u;
       }
+      const uint32_t co = (uint32_t)__popcll(bo);
       oc += co;
       nc += 64u - co;
     }
@@ -835,18 +842,16 @@ __device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32
     for (int sidx = 0; sidx < kSlots; ++sidx) {
       const bool o = (oldm >> sidx) & 1u, n = (newm >> sidx) & 1u;
       const uint64_t bo = __ballot(o), bn = __ballot(n);
-      const uint32_t ro = mbcnt64(bo), rn = mbcnt64(bn);
-      uint32_t idx = o ? oc + ro : nc + rn;
+      uint32_t idx = o ? oc + mbcnt64(bo) : nc + mbcnt64(bn);
       idx = (o || n) ? idx : 0x3FFFFFFFu;
       __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
                                             (int)(idx * 4u), 0, 0);
-      const uint32_t co = (uint32_t)__popcll(bo), cn = (uint32_t)__popcll(bn);
-      if (CHUNKS) {
-        chunk_run(cx, oc, co, __ballot((xcut >> sidx) & 1u), ro, o);
-        chunk_run(cy, nc, cn, __ballot((ycut >> sidx) & 1u), rn, n);
+      if (PRE) {
+        ax += (xcut >> sidx) & (uint32_t)(idx < ex);
+        ay += (ycut >> sidx) & (uint32_t)(idx < ey) & 1u;
       }
-      oc += co;
-      nc += cn;
+      oc += (uint32_t)__popcll(bo);
+      nc += (uint32_t)__popcll(bn);
     }
   }
 }
@@ -872,10 +877,8 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
   const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
   SplitSums so, sn;
   ChunkAcc cx, cy;
-  chunk_init(cx, a.nodes, a.wparts, pt.child[0]);
-  chunk_init(cy, a.nodes, a.wparts, pt.child[1]);
-  if (cx.on) chunk_enter(cx, oc);
-  if (cy.on) chunk_enter(cy, nc);
+  chunk_init(cx, a.nodes, a.wparts, pt.child[0], oc);
+  chunk_init(cy, a.nodes, a.wparts, pt.child[1], nc);
 
   u32x4 v[kVecPerThread];
   uint32_t vs = start & ~3u;
@@ -926,19 +929,13 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
     // --- this wave's points (store_sweep).  A sweep writes at most kWaveSweep points to each child: when neither
     // child's current chunk can end inside it (fast sweep), only the lanes'
     // new counts are kept; otherwise every slot's run is split exactly.
-    const bool fast = (!cx.on || oc + kWaveSweep <= cx.end) && (!cy.on || nc + kWaveSweep <= cy.end);
-    if (fast) {
-      const uint32_t oc0 = oc, nc0 = nc;
-      store_sweep<false>(v, oldm, newm, full, drs, l, xcut, ycut, oc, nc, cx, cy);
-      cx.acc += oc - oc0;
-      cy.acc += nc - nc0;
-      cx.lnew += (uint32_t)__builtin_popcount(xcut);
-      cy.lnew += (uint32_t)__builtin_popcount(ycut);
-    } else {
-      if (cx.on) chunk_reduce(cx);
-      if (cy.on) chunk_reduce(cy);
-      store_sweep<true>(v, oldm, newm, full, drs, l, xcut, ycut, oc, nc, cx, cy);
-    }
+    const bool fast = oc + kWaveSweep <= cx.end && nc + kWaveSweep <= cy.end;
+    const uint32_t oc0 = oc, nc0 = nc;
+    uint32_t ax = 0, ay = 0;
+    if (fast) store_sweep<false>(v, oldm, newm, full, drs, l, xcut, ycut, oc, nc, 0u, 0u, ax, ay);
+    else store_sweep<true>(v, oldm, newm, full, drs, l, xcut, ycut, oc, nc, cx.end, cy.end, ax, ay);
+    chunk_sweep(cx, oc0, oc, (uint32_t)__builtin_popcount(xcut), ax);
+    chunk_sweep(cy, nc0, nc, (uint32_t)__builtin_popcount(ycut), ay);
 #if DQ_PS_PREFETCH
 #pragma unroll
     for (int j = 0; j < kVecPerThread; ++j) v[j] = vn[j];
@@ -952,8 +949,8 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
     full = nfull;
   }
 
-  if (cx.on) { chunk_reduce(cx); chunk_flush(cx); }
-  if (cy.on) { chunk_reduce(cy); chunk_flush(cy); }
+  chunk_finish(cx);
+  chunk_finish(cy);
 
   __shared__ uint32_t red[kTileWaves][16];
   uint32_t f[16] = {so.cnt, so.sr, so.sg, so.sb, so.qr, so.qg, so.qb, 0u,
