@@ -75,6 +75,9 @@ struct alignas(16) DevNode {
   int32_t iter;             // 2-means iterations completed (epilogue count)
   int32_t done_it;          // 0: active; else 1 + the iteration found at the fixed point
   uint32_t tile_len;        // this record's tiles: [off + k*tile_len, ...) (last one shorter)
+  int32_t proven;           // set by the split epilogue: the final halves are the cut's
+                            //   (a later partition replays the cut, prm.thr / prm.shift)
+  int32_t pad2[3];
   // --- a box holding every point of the node (channel c: R, G, B), from the
   //     host: the root's is the cube, a child's is its parent's, clipped at
   //     the parent's cut when the parent's halves are proven to be the cut's

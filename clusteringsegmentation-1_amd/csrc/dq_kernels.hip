@@ -374,6 +374,7 @@ __device__ bool node_update(DevNode* w, NodeResult* r, const uint64_t t[F_NUM], 
     w->iter = 1;
     node_results(r, w, t, om, nm, nw, ow);
     w->done_it = 1;
+    w->proven = 1;
     r->proven = 1;
     return true;
   }
@@ -690,6 +691,28 @@ __device__ __forceinline__ void decide_sweep(const u32x4 v[kVecPerThread], uint3
   validm = vm;
 }
 
+// The same masks for a node whose final decision is its cut (DevNode::
+// proven): OLD iff byte < thr.
+template <bool FULL>
+__device__ __forceinline__ void cut_sweep(const u32x4 v[kVecPerThread], uint32_t vs, uint32_t start,
+                                          uint32_t end, uint32_t shift, int32_t thr,
+                                          uint32_t& oldm, uint32_t& validm) {
+  uint32_t om = 0, vm = FULL ? 0xFFFFu : 0u;
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    const uint32_t i0 = vs + 4u * (j * 64 + lane_id());
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int sidx = j * 4 + e;
+      const uint32_t b = (vec_elem(v[j], e) >> shift) & 0xFFu;
+      om |= ((uint32_t)((int32_t)b - thr) >> 31) << sidx;
+      if (!FULL) vm |= ((uint32_t)((i0 + e - start) < (end - start))) << sidx;
+    }
+  }
+  oldm = om & vm;
+  validm = vm;
+}
+
 // ---------------------------------------------------------------------------
 // Fused partition + split pass over the tiles of parents split in an earlier
 // round (replaces the reference's per-split O(N) member[] gather, :894-1026,
@@ -801,11 +824,15 @@ __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
   if (v != 0 && lane_id() == 0) atomicAdd(c.w0 + c.k * kTileWaves + c.w, v);
 }
 
+// Occupancy / double-buffering of partsplit (measured per 8 x 4K round,
+// tools/prof_variants.sh): 3 waves/SIMD with the next sweep's loads in
+// flight 137.8 us; 4 waves/SIMD (<= 128 VGPRs) with prefetch 126.7 us,
+// without 124.1 us; 5 waves spills VGPRs (182 us).
 #ifndef DQ_PS_WAVES
-#define DQ_PS_WAVES 1
+#define DQ_PS_WAVES 4
 #endif
 #ifndef DQ_PS_PREFETCH
-#define DQ_PS_PREFETCH 1
+#define DQ_PS_PREFETCH 0
 #endif
 // This wave's points of one sweep, slot by slot, ranked by ballot; raw
 // buffer stores (SGPR descriptor + 32-bit offset).  In a full sweep every
@@ -873,6 +900,7 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
   uint32_t oc = nd.off + tp->old_base[w];
   uint32_t nc = nd.off + n_old + tp->new_base[w];
   const bool exact_all = !(q.eps < __builtin_inff());   // FP32 filter off for this node
+  const bool cut = nd.proven != 0;
   const uint32_t sh0 = (uint32_t)pt.shift[0], sh1 = (uint32_t)pt.shift[1];
   const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
   SplitSums so, sn;
@@ -889,8 +917,13 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
   }
   while (vs < end) {
     uint32_t oldm, validm;
-    if (full) decide_sweep<true>(v, vs, start, end, q, exact_all, oldm, validm);
-    else decide_sweep<false>(v, vs, start, end, q, exact_all, oldm, validm);
+    if (cut) {   // proven parent: its final halves are the cut's
+      if (full) cut_sweep<true>(v, vs, start, end, (uint32_t)q.shift, q.thr, oldm, validm);
+      else cut_sweep<false>(v, vs, start, end, (uint32_t)q.shift, q.thr, oldm, validm);
+    } else {
+      if (full) decide_sweep<true>(v, vs, start, end, q, exact_all, oldm, validm);
+      else decide_sweep<false>(v, vs, start, end, q, exact_all, oldm, validm);
+    }
     const uint32_t newm = validm & ~oldm;
     // --- the children's split pass on the same registers: bit arithmetic,
     //     (byte - thr) >> 31 == 0  <=>  byte >= thr  <=>  cut_pos < byte
