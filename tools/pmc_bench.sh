@@ -10,7 +10,7 @@ TAG=${1:-pmc}; shift || true
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-timing --no-c3 $*"
-K="--kernel-include-regex (partsplit|pass_kernel|map_kernel|epilogue)"
+K="--kernel-include-regex (partsplit|pass_kernel|map_|epilogue|build_cells)"
 cd /tmp
 run() {   # name counters...
   local name=$1; shift

@@ -8,7 +8,7 @@ TAG=${1:-pmcv}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-timing --no-c3 --lanes 1"
-K="--kernel-include-regex (partsplit|pass_kernel)"
+K="--kernel-include-regex (partsplit|pass_kernel|map_lds|build_cells)"
 cd /tmp
 timeout -s KILL 120 rocprofv3 $K --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/mix -o mix -- python3 $R/bench.py $ARGS > $O/mix.log 2>&1
 python3 - "$O/mix" <<'PY'
