@@ -1029,37 +1029,83 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
 __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __restrict__ tasks) {
   const MapTask tk = tasks[blockIdx.y];
   const int k = tk.k;
-  extern __shared__ uint32_t spal_c[];   // k colours
+  extern __shared__ uint32_t spal_c[];   // k colours, then k region-list entries (u16)
+  uint16_t* slist = reinterpret_cast<uint16_t*>(spal_c + k);
   __shared__ uint32_t scand[kCellCap * kBlock];   // [i][thread]
+  __shared__ int sred[kBlock / 64];
+  __shared__ uint32_t swoff[kBlock / 64 + 1];
   for (int i = threadIdx.x; i < k; i += kBlock) spal_c[i] = as_g(tk.pal)[i];
-  __syncthreads();
-  const uint32_t tid = threadIdx.x;
-  const uint32_t cell = blockIdx.x * kBlock + tid;
-  const int cw = 1 << (8 - kCellBits);
-  const int lo0 = (int)(cell >> (2 * kCellBits)) * cw;
-  const int lo1 = (int)((cell >> kCellBits) & ((1 << kCellBits) - 1)) * cw;
-  const int lo2 = (int)(cell & ((1 << kCellBits) - 1)) * cw;
-  const int hi0 = lo0 + cw - 1, hi1 = lo1 + cw - 1, hi2 = lo2 + cw - 1;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   auto far2 = [](int v, int lo, int hi) { const int x = max(v - lo, hi - v); return x * x; };
   auto near2 = [](int v, int lo, int hi) {
     const int x = max(max(lo - v, v - hi), 0);
     return x * x;
   };
-  int bound = 0x7FFFFFFF;
-#pragma unroll 8
-  for (int e = 0; e < k; ++e) {
+  // This workgroup's cells: a 4 x 8 x 8 block of the 32^3 grid (R x G x B),
+  // so that one region list serves all of them.  For a cell C inside the
+  // region R, C's candidates {e : near2(e,C) <= min_f far2(f,C)} are
+  // candidates of R (near2(e,R) <= near2(e,C), far2(f,C) <= far2(f,R)), and
+  // C's minimiser of far2 is one too: scanning R's list (palette order)
+  // gives exactly the bound and the candidates of a scan over the palette.
+  static_assert(kCellBits == 5 && kBlock == 256, "4 x 8 x 8 cells per workgroup");
+  const uint32_t bb = blockIdx.x & 3u, bg = (blockIdx.x >> 2) & 3u, br = blockIdx.x >> 4;
+  const uint32_t c0 = br * 4 + (tid >> 6), c1 = bg * 8 + ((tid >> 3) & 7u), c2 = bb * 8 + (tid & 7u);
+  const uint32_t cell = (c0 << (2 * kCellBits)) | (c1 << kCellBits) | c2;
+  const int cw = 1 << (8 - kCellBits);
+  const int rlo0 = (int)br * 4 * cw, rlo1 = (int)bg * 8 * cw, rlo2 = (int)bb * 8 * cw;
+  const int rhi0 = rlo0 + 4 * cw - 1, rhi1 = rlo1 + 8 * cw - 1, rhi2 = rlo2 + 8 * cw - 1;
+  __syncthreads();
+  // region bound: min over entries of the max distance to the region
+  int rb = 0x7FFFFFFF;
+  for (int e = (int)tid; e < k; e += kBlock) {
     const uint32_t q = spal_c[e];
+    rb = min(rb, far2((q >> 16) & 0xFF, rlo0, rhi0) + far2((q >> 8) & 0xFF, rlo1, rhi1) +
+                     far2(q & 0xFF, rlo2, rhi2));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) rb = min(rb, __shfl_xor(rb, o, 64));
+  if (lane == 0) sred[wv] = rb;
+  __syncthreads();
+  rb = sred[0];
+#pragma unroll
+  for (int w = 1; w < kBlock / 64; ++w) rb = min(rb, sred[w]);
+  // region list in palette order: chunks of kBlock entries, ballot-ranked
+  uint32_t nlist = 0;
+  for (int base = 0; base < k; base += kBlock) {
+    const int e = base + (int)tid;
+    bool in = false;
+    if (e < k) {
+      const uint32_t q = spal_c[e];
+      in = near2((q >> 16) & 0xFF, rlo0, rhi0) + near2((q >> 8) & 0xFF, rlo1, rhi1) +
+               near2(q & 0xFF, rlo2, rhi2) <= rb;
+    }
+    const uint64_t m = __ballot(in);
+    if (lane == 0) swoff[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = nlist;
+    for (uint32_t w = 0; w < wv; ++w) off += swoff[w];
+    if (in) slist[off + mbcnt64(m)] = (uint16_t)e;
+    for (int w = 0; w < kBlock / 64; ++w) nlist += swoff[w];
+    __syncthreads();
+  }
+  const int lo0 = (int)c0 * cw, lo1 = (int)c1 * cw, lo2 = (int)c2 * cw;
+  const int hi0 = lo0 + cw - 1, hi1 = lo1 + cw - 1, hi2 = lo2 + cw - 1;
+  int bound = 0x7FFFFFFF;
+#pragma unroll 4
+  for (uint32_t i = 0; i < nlist; ++i) {
+    const uint32_t q = spal_c[slist[i]];
     bound = min(bound, far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) +
                            far2(q & 0xFF, lo2, hi2));
   }
   // (a) loose candidates, palette order
   uint32_t count = 0;
-#pragma unroll 8
-  for (int e = 0; e < k; ++e) {
+#pragma unroll 4
+  for (uint32_t i = 0; i < nlist; ++i) {
+    const uint32_t e = slist[i];
     const uint32_t q = spal_c[e];
     const bool cand = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
                           near2(q & 0xFF, lo2, hi2) <= bound;
-    if (cand && count < (uint32_t)kCellCap) scand[count * kBlock + tid] = (uint32_t)e;
+    if (cand && count < (uint32_t)kCellCap) scand[count * kBlock + tid] = e;
     count += cand ? 1u : 0u;
   }
   // (b) dominance by the 4 candidates with the smallest max distance (as
@@ -1485,12 +1531,12 @@ void launch_build_cells(const MapTask* tasks, int ntasks, int kmax, hipStream_t 
   static_assert(kCells % kBlock == 0, "whole cells per workgroup");
   if (ntasks <= 0) return;
   static bool attr = false;
-  if (!attr) {   // palettes up to 16384 entries: up to 64 KB of dynamic LDS beside 32 KB static
+  if (!attr) {   // palettes up to 16384 entries: up to 96 KB of dynamic LDS beside 32 KB static
     (void)hipFuncSetAttribute((const void*)build_cells_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
     attr = true;
   }
-  build_cells_kernel<<<dim3(kCells / kBlock, ntasks), dim3(kBlock), (size_t)kmax * 4,
+  build_cells_kernel<<<dim3(kCells / kBlock, ntasks), dim3(kBlock), (size_t)kmax * 6 + 16,
                        stream>>>(tasks);
 }
 
