@@ -205,7 +205,7 @@ void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t s
   // before any of these buffers moves.
   const bool grow = staging_bytes > cap_stage_tab_ || nnodes > cap_res_ ||
                     (size_t)max_iters > cap_stat_ || ntiles > cap_parts_ ||
-                    2 * nptiles > cap_sparts_ || ntiles * kTileWaves > cap_wparts_ || !h_stage_ || !h_res_ || !h_stat_ || !d_parts_ ||
+                    2 * nptiles > cap_sparts_ || !h_stage_ || !h_res_ || !h_stat_ || !d_parts_ ||
                     !d_sparts_;
   if (!grow) return;
   DQ_HIP(hipStreamSynchronize(stream));
@@ -218,7 +218,6 @@ void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t s
   grow_coherent(&h_res_, &d_res_, &cap_res_, nnodes);
   grow_coherent(&h_stat_, &d_stat_, &cap_stat_, (size_t)max_iters);
   grow_device(&d_parts_, &cap_parts_, ntiles);
-  grow_device(&d_wparts_, &cap_wparts_, ntiles * kTileWaves);
   grow_device(&d_sparts_, &cap_sparts_, std::max<size_t>(2 * nptiles, 2));
 }
 
@@ -330,13 +329,16 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   for (int p : parents)
     for (int sh = 0; sh < S; ++sh) nptiles += seg(p, sh).ntiles;
 
-  // the round's block: [DevNode nr | Tile ntiles | PartTile nptiles | LaunchCtr max_iters]
+  // the round's block: [DevNode nr | Tile ntiles | PartTile nptiles | LaunchCtr max_iters+1 | wparts]
   auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
   const size_t o_tiles = al(nr * sizeof(DevNode));
   const size_t o_pt = o_tiles + al(ntiles * sizeof(Tile));
   const size_t o_ctr = o_pt + al(nptiles * sizeof(PartTile));
-  // (LaunchCtr and status word max_iters: the split epilogue's)
-  const size_t bytes = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
+  // (LaunchCtr and status word max_iters: the split epilogue's); then the
+  // per-(tile, wave) counts, zero from the staging memset (partsplit adds
+  // the fused children's up)
+  const size_t o_wp = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
+  const size_t bytes = o_wp + al(ntiles * kTileWaves * sizeof(uint32_t));
   ensure_round(nr, ntiles, nptiles, bytes, max_iters + 1, stream);
   if (sharded && (size_t)nl * 8 > cap_tot_) {
     DQ_HIP(hipStreamSynchronize(stream));
@@ -453,7 +455,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   ra.tiles = dt;
   ra.nodes = dn;
   ra.parts = d_parts_;
-  ra.wparts = d_wparts_;
+  ra.wparts = reinterpret_cast<uint32_t*>(dblk + o_wp);
   ra.ptiles = reinterpret_cast<const PartTile*>(dblk + o_pt);
   ra.sparts = d_sparts_;
   ra.hres = d_res_;
@@ -494,9 +496,6 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     pass(PASS_INIT, ST_INIT, -1, nt, bytes_all);
     epilogue(PASS_INIT, -1);
   }
-  // the split pass's per-(tile, wave) counts: own split passes store theirs,
-  // partsplit adds the fused children's up
-  if (nptiles > 0) DQ_HIP(hipMemsetAsync(d_wparts_, 0, ntiles * kTileWaves * sizeof(uint32_t), stream));
   pass(PASS_SPLIT, ST_SPLIT, -1, (int)nt_own, 4.0 * (double)own_total);
   if (nptiles > 0) {
     timed_begin(stream);
