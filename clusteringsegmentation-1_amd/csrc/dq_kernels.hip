@@ -218,20 +218,6 @@ struct SplitSums {
   uint32_t cnt = 0, sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
 };
 
-__device__ __forceinline__ void add4_sums(const uint32_t m[4], SplitSums& s) {
-  const uint32_t u01 = __builtin_amdgcn_perm(m[1], m[0], 0x05010400u);  // B0 B1 G0 G1
-  const uint32_t u23 = __builtin_amdgcn_perm(m[3], m[2], 0x05010400u);  // B2 B3 G2 G3
-  const uint32_t bq = __builtin_amdgcn_perm(u23, u01, 0x05040100u);     // B0 B1 B2 B3
-  const uint32_t gq = __builtin_amdgcn_perm(u23, u01, 0x07060302u);     // G0 G1 G2 G3
-  const uint32_t rq = __builtin_amdgcn_perm(m[1], m[0], 0x0C0C0602u) |  // R0 R1 0 0
-                      __builtin_amdgcn_perm(m[3], m[2], 0x06020C0Cu);   // 0 0 R2 R3
-  s.sr = __builtin_amdgcn_udot4(rq, 0x01010101u, s.sr, false);
-  s.sg = __builtin_amdgcn_udot4(gq, 0x01010101u, s.sg, false);
-  s.sb = __builtin_amdgcn_udot4(bq, 0x01010101u, s.sb, false);
-  s.qr = __builtin_amdgcn_udot4(rq, rq, s.qr, false);
-  s.qg = __builtin_amdgcn_udot4(gq, gq, s.qg, false);
-  s.qb = __builtin_amdgcn_udot4(bq, bq, s.qb, false);
-}
 
 template <int KIND, bool FULL>
 __device__ __forceinline__ void sweep_sums(const u32x4 v[kVecPerThread], uint32_t vs,
@@ -925,29 +911,49 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
       else decide_sweep<false>(v, vs, start, end, q, exact_all, oldm, validm);
     }
     const uint32_t newm = validm & ~oldm;
-    // --- the children's split pass on the same registers: bit arithmetic,
-    //     (byte - thr) >> 31 == 0  <=>  byte >= thr  <=>  cut_pos < byte
-    uint32_t xcut = 0, ycut = 0;   // slots new for the old / new child's split
+    // --- the children's split pass on the same registers (cut_pos < v_axis
+    //     <=> v_axis >= thr): per lane, a bit per slot below each child's
+    //     threshold, then the children's new-side slots as masks; counts by
+    //     popcount, sums by v_dot4 against byte weights spread from 4 mask
+    //     bits (b * 0x204081 puts bit i at bit 8i), the byte transposes shared
+    //     by both children
+    uint32_t lt0 = 0, lt1 = 0;
 #pragma unroll
-    for (int j = 0; j < kVecPerThread; ++j) {
-      uint32_t mo[4], mn[4];
+    for (int j = 0; j < kVecPerThread; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int sidx = j * 4 + e;
         const uint32_t p = vec_elem(v[j], e);
-        const uint32_t b0 = ((uint32_t)((int32_t)((p >> sh0) & 0xFF) - thr0) >> 31) ^ 1u;
-        const uint32_t b1 = ((uint32_t)((int32_t)((p >> sh1) & 0xFF) - thr1) >> 31) ^ 1u;
-        const uint32_t so_new = b0 & (oldm >> sidx);
-        const uint32_t sn_new = b1 & (newm >> sidx);
-        mo[e] = p & (0u - (so_new & 1u));
-        mn[e] = p & (0u - (sn_new & 1u));
-        so.cnt += so_new & 1u;
-        sn.cnt += sn_new & 1u;
-        xcut |= (so_new & 1u) << sidx;
-        ycut |= (sn_new & 1u) << sidx;
+        lt0 |= ((uint32_t)((int32_t)((p >> sh0) & 0xFF) - thr0) >> 31) << sidx;
+        lt1 |= ((uint32_t)((int32_t)((p >> sh1) & 0xFF) - thr1) >> 31) << sidx;
       }
-      add4_sums(mo, so);
-      add4_sums(mn, sn);
+    const uint32_t xcut = oldm & ~lt0, ycut = newm & ~lt1;   // slots new for the old / new child
+    so.cnt += (uint32_t)__builtin_popcount(xcut);
+    sn.cnt += (uint32_t)__builtin_popcount(ycut);
+#pragma unroll
+    for (int j = 0; j < kVecPerThread; ++j) {
+      const u32x4 x = v[j];
+      const uint32_t u01 = __builtin_amdgcn_perm(x[1], x[0], 0x05010400u);  // B0 B1 G0 G1
+      const uint32_t u23 = __builtin_amdgcn_perm(x[3], x[2], 0x05010400u);  // B2 B3 G2 G3
+      const uint32_t bq = __builtin_amdgcn_perm(u23, u01, 0x05040100u);     // B0 B1 B2 B3
+      const uint32_t gq = __builtin_amdgcn_perm(u23, u01, 0x07060302u);     // G0 G1 G2 G3
+      const uint32_t rq = __builtin_amdgcn_perm(x[1], x[0], 0x0C0C0602u) |  // R0 R1 0 0
+                          __builtin_amdgcn_perm(x[3], x[2], 0x06020C0Cu);   // 0 0 R2 R3
+      const uint32_t wx = (((xcut >> (4 * j)) & 0xFu) * 0x204081u) & 0x01010101u;
+      const uint32_t wy = (((ycut >> (4 * j)) & 0xFu) * 0x204081u) & 0x01010101u;
+      const uint32_t mx = wx * 0xFFu, my = wy * 0xFFu;
+      so.sr = __builtin_amdgcn_udot4(rq, wx, so.sr, false);
+      so.sg = __builtin_amdgcn_udot4(gq, wx, so.sg, false);
+      so.sb = __builtin_amdgcn_udot4(bq, wx, so.sb, false);
+      so.qr = __builtin_amdgcn_udot4(rq & mx, rq, so.qr, false);
+      so.qg = __builtin_amdgcn_udot4(gq & mx, gq, so.qg, false);
+      so.qb = __builtin_amdgcn_udot4(bq & mx, bq, so.qb, false);
+      sn.sr = __builtin_amdgcn_udot4(rq, wy, sn.sr, false);
+      sn.sg = __builtin_amdgcn_udot4(gq, wy, sn.sg, false);
+      sn.sb = __builtin_amdgcn_udot4(bq, wy, sn.sb, false);
+      sn.qr = __builtin_amdgcn_udot4(rq & my, rq, sn.qr, false);
+      sn.qg = __builtin_amdgcn_udot4(gq & my, gq, sn.qg, false);
+      sn.qb = __builtin_amdgcn_udot4(bq & my, bq, sn.qb, false);
     }
     // --- next sweep's loads in flight during the stores
     const uint32_t nvs = vs + kWaveSweep;
