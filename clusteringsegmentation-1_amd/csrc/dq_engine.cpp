@@ -338,7 +338,9 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   // per-(tile, wave) counts, zero from the staging memset (partsplit adds
   // the fused children's up)
   const size_t o_wp = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
-  const size_t bytes = o_wp + al(ntiles * kTileWaves * sizeof(uint32_t));
+  // then the fused 2-means passes' arrival words, per (iteration, record)
+  const size_t o_rd = o_wp + al(ntiles * kTileWaves * sizeof(uint32_t));
+  const size_t bytes = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
   ensure_round(nr, ntiles, nptiles, bytes, max_iters + 1, stream);
   if (sharded && (size_t)nl * 8 > cap_tot_) {
     DQ_HIP(hipStreamSynchronize(stream));
@@ -468,6 +470,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   ra.tot = d_tot_;
   ra.nshard = S;
   ra.pad = 0;
+  ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
   const double bytes_all = 4.0 * (double)total;
   const int nt = (int)ntiles;
   // 2-means passes (iteration index) whose timing entry gets its swept bytes
@@ -492,6 +495,22 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     launch_epilogue(kind, ra, nr, sharded, stream);
     timed_end(ST_EPILOGUE, 0.0, stream);
   };
+  // 2-means iteration `it`: pass + epilogue, one launch when unsharded
+  auto kmeans_iter = [&](int it) {
+    const bool last = it == max_iters - 1;
+    const int kind = last ? PASS_KLAST : PASS_KMEANS;
+    const int st = last ? ST_KLAST : ST_KMEANS;
+    if (sharded) {
+      pass(kind, st, it, nt, bytes_all);
+      epilogue(kind, it);
+      return;
+    }
+    ra.it = it;
+    timed_begin(stream);
+    launch_kpass(kind, ra, nt, stream);
+    timed_end(st, bytes_all, stream);
+    if (timing_) km_events.push_back({pending_.size() - 1, it});
+  };
   if (root_round) {
     pass(PASS_INIT, ST_INIT, -1, nt, bytes_all);
     epilogue(PASS_INIT, -1);
@@ -510,9 +529,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   bool all_proven = false;
   if (fixed_point_) {
     if (spec_it0_) {
-      pass(max_iters == 1 ? PASS_KLAST : PASS_KMEANS, max_iters == 1 ? ST_KLAST : ST_KMEANS, 0, nt,
-           bytes_all);
-      epilogue(max_iters == 1 ? PASS_KLAST : PASS_KMEANS, 0);
+      kmeans_iter(0);
       launched = 1;
     }
     all_proven = wait_status(max_iters, seq, stream) == 0;
@@ -521,9 +538,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   // host waits for; stop as soon as every node is final.
   while (!all_proven) {
     while (launched < max_iters && launched <= known + lookahead_) {
-      const bool last = launched == max_iters - 1;
-      pass(last ? PASS_KLAST : PASS_KMEANS, last ? ST_KLAST : ST_KMEANS, launched, nt, bytes_all);
-      epilogue(last ? PASS_KLAST : PASS_KMEANS, launched);
+      kmeans_iter(launched);
       ++launched;
     }
     const uint32_t act = wait_status(known, seq, stream);

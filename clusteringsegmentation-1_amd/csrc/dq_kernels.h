@@ -45,10 +45,13 @@ struct RoundArgs {
   uint64_t* tot;            // per logical node: 8 u64 totals (nodesum, then allreduce)
   int32_t nshard;           // records per logical node (record r = node * nshard + shard)
   int32_t pad;
+  uint32_t* rdone;          // per (2-means iteration, record): kpass workgroups finished
 };
 
 // One statistics pass over tiles [0, ntiles) of the round (one workgroup per tile).
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
+// A 2-means pass with its epilogue fused (unsharded rounds; kpass_kernel).
+void launch_kpass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
 // The FP64 update after a pass, one workgroup per node record: sums the
 // node's tile partials (from_totals: reads the node's global totals instead)
 // and publishes the next pass's decision (or the split's results).

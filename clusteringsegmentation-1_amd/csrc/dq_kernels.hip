@@ -511,6 +511,87 @@ __global__ __launch_bounds__(kBlock) void nodesum_kernel(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Finalisation steps of a node record, one wave (epilogue_kernel and the
+// fused 2-means pass, kpass_kernel).
+//
+// Partition cursors: for every (tile, wave) of the record, the OLD and NEW
+// points before its share -- an exclusive shuffle scan of the final pass's
+// per-wave counts, chunked per lane over the tiles [tb, te).  COHERENT: the
+// counts were written by other workgroups of the running kernel
+// (agent-scope loads).
+template <bool COHERENT = false>
+__device__ __forceinline__ void record_cursors(Tile* tiles, const uint32_t* wp, int tb, int te,
+                                               uint32_t lane) {
+  const int T = te - tb;
+  const int chunk = (T + 63) / 64;
+  const int c0 = tb + (int)lane * chunk;
+  const int c1 = min(te, c0 + chunk);
+  auto ld = [&](int i) -> uint32_t {
+    if (COHERENT) return __hip_atomic_load(wp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return wp[i];
+  };
+  uint64_t local = 0;   // old | new << 32
+  for (int i = c0; i < c1; ++i)
+    for (int ww = 0; ww < kTileWaves; ++ww) {
+      const uint32_t x = ld(i * kTileWaves + ww);
+      local += (uint64_t)(x & 0xFFFFu) | ((uint64_t)(x >> 16) << 32);
+    }
+  uint64_t inc = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t u = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += u;
+  }
+  const uint64_t run0 = inc - local;
+  uint32_t ro = (uint32_t)run0, rn = (uint32_t)(run0 >> 32);
+  for (int i = c0; i < c1; ++i)
+    for (int ww = 0; ww < kTileWaves; ++ww) {
+      const uint32_t x = ld(i * kTileWaves + ww);
+      tiles[i].old_base[ww] = ro;
+      tiles[i].new_base[ww] = rn;
+      ro += x & 0xFFFFu;
+      rn += x >> 16;
+    }
+}
+
+// Final results go straight to host-coherent memory: relaxed system-scope
+// 8-B stores, one per lane (no L2 write-back); the caller drains them
+// (s_waitcnt vmcnt(0)) before arriving.
+__device__ __forceinline__ void store_result(NodeResult* dst, const NodeResult& r, uint32_t lane) {
+  constexpr int kWords = (int)(sizeof(NodeResult) / 8);
+  static_assert(kWords <= 64, "one wave stores the result");
+  if (lane < (uint32_t)kWords) {
+    const uint64_t v = reinterpret_cast<const uint64_t*>(&r)[lane];
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + lane, v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// One record's arrival on a launch's counters (lane 0): 64-bit words (low =
+// arrived, high = still active) on the record's shard; the shard's last
+// arriver forwards to `top`, whose last arriver publishes the status word
+// (seq << 32) | (active << 1) | 1 to host memory.
+__device__ __forceinline__ void arrive(LaunchCtr* c, uint32_t rec, uint32_t nn, bool active,
+                                       uint64_t* hstat, uint64_t seq) {
+  const uint32_t sh = rec % kArrShards;
+  const uint32_t nsh = min(nn, (uint32_t)kArrShards);
+  const uint32_t in_shard = (nn - sh + kArrShards - 1) / kArrShards;
+  const uint64_t mine = 1ull | ((uint64_t)active << 32);
+  const uint64_t old = __hip_atomic_fetch_add(&c->shard[sh].word, mine, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+  if ((uint32_t)old == in_shard - 1) {
+    const uint64_t fwd = 1ull | (((old >> 32) + (mine >> 32)) << 32);
+    const uint64_t t = __hip_atomic_fetch_add(&c->top.word, fwd, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)t == nsh - 1) {
+      const uint64_t act = (t >> 32) + (fwd >> 32);
+      __hip_atomic_store(hstat, (seq << 32) | (act << 1) | 1ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Epilogue: ONE WAVE per node record of the round (no workgroup barrier).
 //   * the node's sums: its own partials (FROM_TOT: the logical node's global
 //     totals from nodesum + allreduce; its own partials then only give the
@@ -557,75 +638,113 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
       }
     }
     final_results = __shfl(fin, 0, 64) != 0;
-    if ((kMeans || KIND == PASS_SPLIT) && final_results) {
-      // Partition cursors: for every (tile, wave) of the node, the OLD and
-      // NEW points of the node before its share -- an exclusive shuffle scan
-      // of the final pass's per-wave counts, chunked per lane over the tiles.
-      const int T = te - tb;
-      const int chunk = (T + 63) / 64;
-      const int c0 = tb + (int)lane * chunk;
-      const int c1 = min(te, c0 + chunk);
-      const uint32_t* wp = a.wparts;
-      uint64_t local = 0;   // old | new << 32
-      for (int i = c0; i < c1; ++i)
-        for (int ww = 0; ww < kTileWaves; ++ww) {
-          const uint32_t x = wp[i * kTileWaves + ww];
-          local += (uint64_t)(x & 0xFFFFu) | ((uint64_t)(x >> 16) << 32);
-        }
-      uint64_t inc = local;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t u = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc += u;
-      }
-      const uint64_t run0 = inc - local;
-      uint32_t ro = (uint32_t)run0, rn = (uint32_t)(run0 >> 32);
-      for (int i = c0; i < c1; ++i)
-        for (int ww = 0; ww < kTileWaves; ++ww) {
-          const uint32_t x = wp[i * kTileWaves + ww];
-          a.tiles[i].old_base[ww] = ro;
-          a.tiles[i].new_base[ww] = rn;
-          ro += x & 0xFFFFu;
-          rn += x >> 16;
-        }
-    }
+    if ((kMeans || KIND == PASS_SPLIT) && final_results) record_cursors(a.tiles, a.wparts, tb, te, lane);
   }
   if (kMeans || KIND == PASS_SPLIT) {   // (split: proven fixed points, status slot max_iters)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // Final results go straight to host-coherent memory: relaxed system-scope
-    // 8-B stores, one per lane (no L2 write-back), drained before arriving.
-    constexpr int kWords = (int)(sizeof(NodeResult) / 8);
-    static_assert(kWords <= 64, "one wave stores the result");
-    if (final_results && lane < (uint32_t)kWords) {
-      const uint64_t v = reinterpret_cast<const uint64_t*>(&sres)[lane];
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(a.hres + blockIdx.x) + lane, v,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (final_results) store_result(a.hres + blockIdx.x, sres, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      // 64-bit arrivals (low word = arrived, high = still active) on this
-      // record's shard, then the shard's last arriver on the top word
-      LaunchCtr* c = a.ctr + a.it;
-      const uint32_t sh = blockIdx.x % kArrShards;
-      const uint32_t nsh = min((uint32_t)a.nn, (uint32_t)kArrShards);
-      const uint32_t in_shard = ((uint32_t)a.nn - sh + kArrShards - 1) / kArrShards;
-      const uint64_t mine = 1ull | ((uint64_t)(!skip && !final_results) << 32);
-      const uint64_t old = __hip_atomic_fetch_add(&c->shard[sh].word, mine, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      if ((uint32_t)old == in_shard - 1) {
-        const uint64_t fwd = 1ull | (((old >> 32) + (mine >> 32)) << 32);
-        const uint64_t t = __hip_atomic_fetch_add(&c->top.word, fwd, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)t == nsh - 1) {
-          const uint64_t act = (t >> 32) + (fwd >> 32);
-          __hip_atomic_store(a.hstat + a.it, (a.seq << 32) | (act << 1) | 1ull,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
+    if (lane == 0)
+      arrive(a.ctr + a.it, blockIdx.x, (uint32_t)a.nn, !skip && !final_results, a.hstat + a.it, a.seq);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 2-means pass with its epilogue fused (unsharded rounds): pass_kernel's
+// sweep, then the record's LAST workgroup to finish runs the record's
+// epilogue (one wave; exactly epilogue_kernel<KIND, false>).  Partials and
+// per-wave counts are stored at agent scope and read back at agent scope
+// (the XCDs' L2s are not coherent with each other); every workgroup drains
+// its stores (barrier: vmcnt(0)) before counting itself in.  A record final
+// in an earlier launch arrives through its first tile's workgroup.
+template <int KIND>
+__device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int rec, NodeResult* sres) {
+  DevNode* w = a.nodes + rec;
+  const uint32_t lane = lane_id();
+  const int tb = w->tile_begin, te = w->tile_end;
+  uint64_t acc[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
+  const uint32_t* pp = reinterpret_cast<const uint32_t*>(a.parts);
+  for (int i = tb + (int)lane; i < te; i += 64)
+#pragma unroll
+    for (int k = 0; k < F_NUM; ++k)
+      acc[k] += __hip_atomic_load(pp + (size_t)i * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t tot[F_NUM];
+#pragma unroll
+  for (int k = 0; k < F_NUM; ++k) tot[k] = wave_sum_u64(acc[k]);
+  int fin = 0;
+  if (lane == 0) {
+    fin = node_update<KIND>(w, sres, tot, a.fixed_point != 0) ? 1 : 0;
+    if (fin) {
+      for (int c = 0; c < 3; ++c) { sres->tm[c] = w->tm[c]; sres->tv[c] = w->tv[c]; }
+      w->n_new_local = (uint32_t)tot[F_CNT];
+      sres->n_new_local = (uint32_t)tot[F_CNT];
+      sres->done_it = w->done_it;
     }
   }
+  const bool final_results = __shfl(fin, 0, 64) != 0;
+  if (final_results) record_cursors<true>(a.tiles, a.wparts, tb, te, lane);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (final_results) store_result(a.hres + rec, *sres, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0)
+    arrive(a.ctr + a.it, (uint32_t)rec, (uint32_t)a.nn, !final_results, a.hstat + a.it, a.seq);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kBlock) void kpass_kernel(RoundArgs a) {
+  const Tile t = a.tiles[blockIdx.x];
+  const int rec = t.node;
+  const DevNode& nd = a.nodes[rec];
+  if (nd.done_it != 0) {   // final in an earlier launch: its first tile arrives for it
+    if ((int)blockIdx.x == nd.tile_begin && threadIdx.x == 0)
+      arrive(a.ctr + a.it, (uint32_t)rec, (uint32_t)a.nn, false, a.hstat + a.it, a.seq);
+    return;
+  }
+  g_cu4* src4 = as_g4(nd.src);
+  const Params q = nd.prm;
+  __shared__ uint32_t red[kBlock / 64][8];
+  __shared__ int slast;
+  __shared__ NodeResult sres;
+  LaneSums s;
+  u32x4 v[kVecPerThread];
+  uint32_t ws, we;
+  wave_range(t.start, t.end, wave_id(), ws, we);
+  for (uint32_t vs = ws & ~3u; vs < we; vs += kWaveSweep) {
+    if (vs >= ws && vs + kWaveSweep <= we) {   // wave-uniform
+      load_sweep<true>(src4, vs, we, v);
+      sweep_sums<KIND, true>(v, vs, ws, we, q, s);
+    } else {
+      load_sweep<false>(src4, vs, we, v);
+      sweep_sums<KIND, false>(v, vs, ws, we, q, s);
+    }
+  }
+  uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
+#pragma unroll
+  for (int k = 0; k < F_NUM; ++k) f[k] = wave_sum_u32(f[k]);
+  const uint32_t vsum = wave_sum_u32(s.vcnt);
+  if (lane_id() == 0) {
+    __hip_atomic_store(a.wparts + blockIdx.x * kTileWaves + wave_id(),
+                       (vsum - f[F_CNT]) | (f[F_CNT] << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[wave_id()][k] = k < F_NUM ? f[k] : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) x += red[w][threadIdx.x];
+    __hip_atomic_store(a.parts[blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();   // (every wave's stores drained)
+  if (threadIdx.x == 0)
+    slast = __hip_atomic_fetch_add(a.rdone + (size_t)a.it * a.nn + rec, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(nd.tile_end - nd.tile_begin) - 1;
+  __syncthreads();
+  if (slast && wave_id() == 0) kmeans_epilogue_wave<KIND>(a, rec, &sres);
 }
 
 // The 2-means decisions of one sweep as lane bit masks: bit s of oldm = slot
@@ -870,7 +989,6 @@ __device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32
 }
 
 __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArgs a) {
-  constexpr int kSlots = kVecPerThread * 4;
   const PartTile pt = a.ptiles[blockIdx.x];
   const Tile* tp = pt.tile;
   const DevNode& nd = *pt.parent;
@@ -1494,6 +1612,13 @@ void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) {
     case PASS_KMEANS: pass_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a); break;
     default: pass_kernel<PASS_KLAST><<<g, b, 0, stream>>>(a); break;
   }
+}
+
+void launch_kpass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) {
+  if (ntiles <= 0) return;
+  const dim3 g(ntiles), b(kBlock);
+  if (kind == PASS_KLAST) kpass_kernel<PASS_KLAST><<<g, b, 0, stream>>>(a);
+  else kpass_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a);
 }
 
 void launch_epilogue(int kind, const RoundArgs& a, int nnodes, bool from_totals,
