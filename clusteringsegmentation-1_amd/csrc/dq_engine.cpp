@@ -240,6 +240,7 @@ uint32_t Engine::wait_status(int it, uint64_t seq, hipStream_t stream) {
   uint32_t act = 0;
   for (uint64_t spin = 0;; ++spin) {
     if (ready(&act)) return act;
+    __builtin_ia32_pause();   // (spinning lane threads share cores)
     if ((spin & 0x3FFF) == 0x3FFF) {
       const hipError_t e = hipStreamQuery(stream);
       if (e == hipSuccess) {
