@@ -34,8 +34,16 @@ def _named(funcs, part):
     return got
 
 
+def _is_fused_epilogue(name):
+    # kpass_kernel: the record's last workgroup runs the 2-means epilogue
+    # (FP64 update with divisions), checked like the epilogues below
+    return "kpass_kernel" in name
+
+
 def test_no_fp64_contraction_in_decisions(kernels):
     for name, body in list(_named(kernels, "pass_kernel").items()) + list(_named(kernels, "partsplit_kernel").items()):
+        if _is_fused_epilogue(name):
+            continue
         assert "v_fma_f64" not in body and "v_fmac_f64" not in body, name
 
 
@@ -59,7 +67,7 @@ def test_epilogue_fma_only_in_divisions(kernels, tmp_path):
                           stderr=subprocess.DEVNULL)
     fast = _fma_counts(fast_s.read_text())
     for name, (nfma, ndiv) in prod.items():
-        if "epilogue_kernel" not in name:
+        if "epilogue_kernel" not in name and not _is_fused_epilogue(name):
             continue
         assert nfma <= 5 * ndiv, (name, nfma, ndiv)
         if ndiv:
