@@ -19,6 +19,8 @@ Row-tile sharding (one frame over shards / GPUs, RCCL allreduce per pass):
     quant_rows_device, comm_init_torch (comm_unique_id, comm_init, comm_destroy)
 Full-frame block histograms (genHistogramsForBlocks):
     get_subdivided_colors, gen_histograms_for_blocks, block_hist_device
+BGR24 (OpenCV CV_8UC3) ingestion / output on the GPU (Vec3BToUID / PixelToVec3b):
+    pack_bgr24_device, unpack_bgr24_device, gather_bgr24_device
 """
 import ctypes
 import os
@@ -91,6 +93,10 @@ def lib():
         "dq_hip_block_hist_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, vp, c.c_int, c.c_uint32,
                                    c.c_uint32, c.c_uint32, vp, vp, vp, vp, vp, vp], c.c_int),
         "dq_subdivided_colors": ([vp], None),
+        "dq_hip_pack_bgr24_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp, vp], c.c_int),
+        "dq_hip_unpack_bgr24_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp, vp],
+                                    c.c_int),
+        "dq_hip_gather_bgr24_dev": ([c.c_int, vp, c.c_uint32, vp, c.c_uint32, vp, vp], c.c_int),
         "quant_recurse": ([c.c_uint32, vp, vp, u32p, vp, c.c_int], None),
     }
     for name, (args, res) in sigs.items():
@@ -278,6 +284,33 @@ def map_device(t_in, t_out, colortable, device=0, n=None, stream=None):
     if lib().dq_hip_map_dev(device, _dptr(t_in), n, _dptr(t_out), _ptr(ct), ct.size,
                             _stream_ptr(stream)) < 0:
         raise DivQuantError("dq_hip_map_dev: bad arguments")
+
+
+# ---------------------------------------------------------------------------
+# BGR24 frames.  `t_bgr`: uint8 device tensor (or pointer)
+# holding a CV_8UC3 frame, `stride` bytes per row (default 3 * width).
+def pack_bgr24_device(t_bgr, width, height, t_out, stride=None, device=0, stream=None):
+    """t_out[y*width+x] = Vec3BToUID(img(y, x)) (OpenCVUtil.h:19-27), asynchronous."""
+    stride = 3 * width if stride is None else stride
+    if lib().dq_hip_pack_bgr24_dev(device, _dptr(t_bgr), width, height, stride, _dptr(t_out),
+                                   _stream_ptr(stream)) < 0:
+        raise DivQuantError("dq_hip_pack_bgr24_dev: bad arguments")
+
+
+def unpack_bgr24_device(t_in, width, height, t_bgr, stride=None, device=0, stream=None):
+    """img(y, x) = PixelToVec3b(t_in[y*width+x]) (OpenCVUtil.h:53-59), asynchronous."""
+    stride = 3 * width if stride is None else stride
+    if lib().dq_hip_unpack_bgr24_dev(device, _dptr(t_in), width, height, stride, _dptr(t_bgr),
+                                     _stream_ptr(stream)) < 0:
+        raise DivQuantError("dq_hip_unpack_bgr24_dev: bad arguments")
+
+
+def gather_bgr24_device(t_bgr, stride, t_coords, n, t_out, device=0, stream=None):
+    """t_out[i] = Vec3BToUID(img(c.y, c.x)) for Coord words c = x | y << 16
+    (Coord.h:30-33; ClusteringSegmentation.cpp:1795-1800), asynchronous."""
+    if lib().dq_hip_gather_bgr24_dev(device, _dptr(t_bgr), stride, _dptr(t_coords), n,
+                                     _dptr(t_out), _stream_ptr(stream)) < 0:
+        raise DivQuantError("dq_hip_gather_bgr24_dev: bad arguments")
 
 
 # ---------------------------------------------------------------------------

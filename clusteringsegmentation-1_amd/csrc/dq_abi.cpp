@@ -128,6 +128,42 @@ int dq_hip_block_hist_dev(int device, const uint32_t* d_in, uint32_t width, uint
   return dq::launch_block_hist(a, (int)dim, (hipStream_t)stream);
 }
 
+static bool bgr24_shape_ok(uint32_t width, uint32_t height, uint32_t stride) {
+  return width > 0 && height > 0 && width <= 0xFFFFFFFFu / 3u && stride >= 3u * width &&
+         (uint64_t)width * height <= 0xFFFFFFFFull;
+}
+
+static hipStream_t engine_stream(int device, void* stream) {
+  Engine& e = engine_for(device);
+  DQ_HIP(hipSetDevice(device));
+  return stream ? (hipStream_t)stream : e.stream();
+}
+
+int dq_hip_pack_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t width, uint32_t height,
+                          uint32_t stride, uint32_t* d_out, void* stream) {
+  if (!d_bgr || !d_out || !bgr24_shape_ok(width, height, stride)) return -1;
+  dq::launch_bgr24_pack(d_bgr, width, height, stride, d_out, engine_stream(device, stream));
+  DQ_HIP(hipGetLastError());
+  return 0;
+}
+
+int dq_hip_unpack_bgr24_dev(int device, const uint32_t* d_in, uint32_t width, uint32_t height,
+                            uint32_t stride, uint8_t* d_bgr, void* stream) {
+  if (!d_in || !d_bgr || !bgr24_shape_ok(width, height, stride)) return -1;
+  dq::launch_bgr24_unpack(d_in, width, height, stride, d_bgr, engine_stream(device, stream));
+  DQ_HIP(hipGetLastError());
+  return 0;
+}
+
+int dq_hip_gather_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t stride,
+                            const uint32_t* d_coords, uint32_t n, uint32_t* d_out, void* stream) {
+  if (!d_bgr || !d_coords || !d_out || stride < 3u) return -1;
+  if (n == 0) return 0;
+  dq::launch_bgr24_gather(d_bgr, stride, d_coords, n, d_out, engine_stream(device, stream));
+  DQ_HIP(hipGetLastError());
+  return 0;
+}
+
 int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
                            const uint32_t* n, uint32_t* const* d_out, uint32_t k,
                            uint32_t* ct, uint32_t* k_out, int max_iters, void* stream) {

@@ -121,4 +121,14 @@ constexpr uint32_t kBhQueues = DQ_BH_QUEUES, kBhQueueStride = 32;
 size_t block_hist_scratch_words(uint32_t block_w, uint32_t block_h);
 int launch_block_hist(const BlockHistArgs& a, int dim, hipStream_t stream);
 
+// BGR24 (OpenCV CV_8UC3, `stride` bytes per row) <-> packed 0x00RRGGBB
+// frames: Vec3BToUID / PixelToVec3b (superpixels/OpenCVUtil.h:19-27, 53-59)
+// over a whole frame, and the Coord-list gather of ClusteringSegmentation.cpp:1795-1800.
+void launch_bgr24_pack(const uint8_t* bgr, uint32_t width, uint32_t height, uint32_t stride,
+                       uint32_t* out, hipStream_t stream);
+void launch_bgr24_unpack(const uint32_t* in, uint32_t width, uint32_t height, uint32_t stride,
+                         uint8_t* bgr, hipStream_t stream);
+void launch_bgr24_gather(const uint8_t* bgr, uint32_t stride, const uint32_t* coords, uint32_t n,
+                         uint32_t* out, hipStream_t stream);
+
 }  // namespace dq

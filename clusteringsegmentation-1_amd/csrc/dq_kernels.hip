@@ -1892,4 +1892,153 @@ int launch_block_hist(const BlockHistArgs& a0, int dim, hipStream_t stream) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// BGR24 ingestion and output.  The app builds the u32
+// frame on the CPU, pixel by pixel, from an OpenCV CV_8UC3 Mat
+// (Vec3BToUID, superpixels/OpenCVUtil.h:19-27, loops at
+// ClusteringSegmentation.cpp:381-395 and the region gather :1795-1800), and
+// writes mapped colours back with PixelToVec3b (OpenCVUtil.h:53-59,
+// ClusteringSegmentation.cpp:1812-1817).  Memory bytes of a BGR pixel are
+// B, G, R; the packed word 0x00RRGGBB has the same three bytes in the same
+// little-endian order plus a zero, so packing is a byte shuffle.
+// Fast path (row stride, width and base 4-B aligned, output 16-B aligned):
+// one lane per 4 pixels of a row, 12 B read as three dwords, 16 B written.
+// HBM-bound: 7 B per pixel.  Rows are blockIdx.y (+ gridDim.y strides).
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+#ifndef DQ_BGR_NT
+#define DQ_BGR_NT 1       // nontemporal (streaming) frame accesses: pack 12.8 -> 10.9 us per 4K frame
+#endif
+#ifndef DQ_BGR_NTU
+#define DQ_BGR_NTU 0      // nontemporal BGR stores in unpack
+#endif
+#ifndef DQ_BGR_ROWCAP
+#define DQ_BGR_ROWCAP 65535u   // grid rows; a workgroup strides over the rest (a cap
+                               // of 270 or 540 rows measured slower)
+#endif
+
+__device__ __forceinline__ u32x4 bgr12_to_px4(uint32_t w0, uint32_t w1, uint32_t w2) {
+  u32x4 o;
+  o.x = w0 & 0x00FFFFFFu;
+  o.y = __builtin_amdgcn_perm(w1, w0, 0x0C050403u);   // b3 b4 b5 0
+  o.z = __builtin_amdgcn_perm(w2, w1, 0x0C040302u);   // b6 b7 b8 0
+  o.w = w2 >> 8;                                       // b9 b10 b11 0
+  return o;
+}
+
+__device__ __forceinline__ void px4_to_bgr12(u32x4 p, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
+  w0 = __builtin_amdgcn_perm(p.y, p.x, 0x04020100u);   // B0 G0 R0 B1
+  w1 = __builtin_amdgcn_perm(p.z, p.y, 0x05040201u);   // G1 R1 B2 G2
+  w2 = __builtin_amdgcn_perm(p.w, p.z, 0x06050402u);   // R2 B3 G3 R3
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(256) void bgr24_pack_kernel(const uint8_t* __restrict__ bgr,
+                                                         uint32_t width, uint32_t height,
+                                                         uint32_t stride, uint32_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;   // pixel quad (FAST) or pixel
+  for (uint32_t y = blockIdx.y; y < height; y += gridDim.y) {
+    const uint8_t* row = bgr + (size_t)y * stride;
+    if (FAST) {
+      if (4u * i >= width) return;
+#if DQ_BGR_NT
+      const __attribute__((address_space(1))) uint32_t* r =
+          (const __attribute__((address_space(1))) uint32_t*)(row + 12u * i);
+      const u32x3 w = {__builtin_nontemporal_load(r), __builtin_nontemporal_load(r + 1),
+                       __builtin_nontemporal_load(r + 2)};
+      __builtin_nontemporal_store(bgr12_to_px4(w.x, w.y, w.z),
+                                  (__attribute__((address_space(1))) u32x4*)(out + (size_t)y * width + 4u * i));
+#else
+      const u32x3 w = *(const __attribute__((address_space(1))) u32x3*)(row + 12u * i);
+      *(__attribute__((address_space(1))) u32x4*)(out + (size_t)y * width + 4u * i) =
+          bgr12_to_px4(w.x, w.y, w.z);
+#endif
+    } else {
+      if (i >= width) return;
+      const uint8_t* q = row + 3u * i;
+      out[(size_t)y * width + i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+    }
+  }
+}
+
+template <bool FAST>
+__global__ __launch_bounds__(256) void bgr24_unpack_kernel(const uint32_t* __restrict__ in,
+                                                           uint32_t width, uint32_t height,
+                                                           uint32_t stride, uint8_t* __restrict__ bgr) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  for (uint32_t y = blockIdx.y; y < height; y += gridDim.y) {
+    uint8_t* row = bgr + (size_t)y * stride;
+    if (FAST) {
+      if (4u * i >= width) return;
+#if DQ_BGR_NT
+      const u32x4 p = __builtin_nontemporal_load(
+          (const __attribute__((address_space(1))) u32x4*)(in + (size_t)y * width + 4u * i));
+#else
+      const u32x4 p = *(const __attribute__((address_space(1))) u32x4*)(in + (size_t)y * width + 4u * i);
+#endif
+      uint32_t w0, w1, w2;
+      px4_to_bgr12(p, w0, w1, w2);
+      const u32x3 w = {w0, w1, w2};
+#if DQ_BGR_NTU
+      __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x3*)(row + 12u * i));
+#else
+      *(__attribute__((address_space(1))) u32x3*)(row + 12u * i) = w;
+#endif
+    } else {
+      if (i >= width) return;
+      const uint32_t p = in[(size_t)y * width + i];
+      uint8_t* q = row + 3u * i;
+      q[0] = (uint8_t)p;
+      q[1] = (uint8_t)(p >> 8);
+      q[2] = (uint8_t)(p >> 16);
+    }
+  }
+}
+
+// Region gather: out[i] = Vec3BToUID(img.at<Vec3b>(c.y, c.x)) for the i-th
+// Coord {uint16 x, uint16 y} (superpixels/Coord.h:30-33: one 32-bit word,
+// x in the low half).
+__global__ __launch_bounds__(256) void bgr24_gather_kernel(const uint8_t* __restrict__ bgr,
+                                                           uint32_t stride,
+                                                           const uint32_t* __restrict__ coords,
+                                                           uint32_t n, uint32_t* __restrict__ out) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const uint32_t c = coords[i];
+    const uint8_t* q = bgr + (size_t)(c >> 16) * stride + 3u * (c & 0xFFFFu);
+    out[i] = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+  }
+}
+
+static bool bgr24_fast(const void* bgr, uint32_t width, uint32_t stride, const void* px) {
+  return (width & 3u) == 0 && (stride & 3u) == 0 && ((uintptr_t)bgr & 3u) == 0 &&
+         ((uintptr_t)px & 15u) == 0;
+}
+
+static dim3 bgr24_grid(uint32_t width, uint32_t height, bool fast) {
+  const uint32_t per_row = fast ? width / 4u : width;
+  return dim3((per_row + 255u) / 256u, height < DQ_BGR_ROWCAP ? height : DQ_BGR_ROWCAP);
+}
+
+void launch_bgr24_pack(const uint8_t* bgr, uint32_t width, uint32_t height, uint32_t stride,
+                       uint32_t* out, hipStream_t stream) {
+  const bool fast = bgr24_fast(bgr, width, stride, out);
+  const dim3 g = bgr24_grid(width, height, fast);
+  if (fast) bgr24_pack_kernel<true><<<g, dim3(256), 0, stream>>>(bgr, width, height, stride, out);
+  else bgr24_pack_kernel<false><<<g, dim3(256), 0, stream>>>(bgr, width, height, stride, out);
+}
+
+void launch_bgr24_unpack(const uint32_t* in, uint32_t width, uint32_t height, uint32_t stride,
+                         uint8_t* bgr, hipStream_t stream) {
+  const bool fast = bgr24_fast(bgr, width, stride, in);
+  const dim3 g = bgr24_grid(width, height, fast);
+  if (fast) bgr24_unpack_kernel<true><<<g, dim3(256), 0, stream>>>(in, width, height, stride, bgr);
+  else bgr24_unpack_kernel<false><<<g, dim3(256), 0, stream>>>(in, width, height, stride, bgr);
+}
+
+void launch_bgr24_gather(const uint8_t* bgr, uint32_t stride, const uint32_t* coords, uint32_t n,
+                         uint32_t* out, hipStream_t stream) {
+  uint32_t nwg = (n + 255u) / 256u;
+  if (nwg > 65536u) nwg = 65536u;
+  bgr24_gather_kernel<<<dim3(nwg), dim3(256), 0, stream>>>(bgr, stride, coords, n, out);
+}
+
 }  // namespace dq

@@ -80,6 +80,28 @@ int dq_hip_block_hist_dev(int device, const uint32_t *d_in, uint32_t width,
                           uint32_t *d_quant, uint32_t *d_mode,
                           uint32_t *d_ndistinct, uint32_t *d_keys,
                           uint32_t *d_counts, void *stream);
+/* BGR24 ingestion / output, device pointers, asynchronous
+ * on `stream` (NULL: the library's stream of `device`).  d_bgr: an OpenCV
+ * CV_8UC3 frame, `stride` bytes per row (>= 3*width; 3*width when
+ * continuous).  Fast path when width, stride and d_bgr are 4-B aligned and
+ * the u32 frame is 16-B aligned; any other layout is handled per pixel.
+ * Return 0 or -1 on bad arguments.
+ *   pack:   d_out[y*width+x] = Vec3BToUID(img(y,x))   (superpixels/OpenCVUtil.h:19-27;
+ *           the loop at ClusteringSegmentation.cpp:381-395)
+ *   unpack: img(y,x) = PixelToVec3b(d_in[y*width+x])  (OpenCVUtil.h:53-59;
+ *           ClusteringSegmentation.cpp:1812-1817); bits 24-31 are dropped
+ *   gather: d_out[i] = Vec3BToUID(img(c.y, c.x)) for the i-th Coord, passed
+ *           as its 32-bit layout (x | y << 16, superpixels/Coord.h:30-33);
+ *           ClusteringSegmentation.cpp:1795-1800.  Coords are not range-checked. */
+int dq_hip_pack_bgr24_dev(int device, const uint8_t *d_bgr, uint32_t width,
+                          uint32_t height, uint32_t stride, uint32_t *d_out,
+                          void *stream);
+int dq_hip_unpack_bgr24_dev(int device, const uint32_t *d_in, uint32_t width,
+                            uint32_t height, uint32_t stride, uint8_t *d_bgr,
+                            void *stream);
+int dq_hip_gather_bgr24_dev(int device, const uint8_t *d_bgr, uint32_t stride,
+                            const uint32_t *d_coords, uint32_t n, uint32_t *d_out,
+                            void *stream);
 /* Row-tile sharding.  Frame i's rows are d_in[i] (n[i] points,
  * width[i] per row; width NULL or 0: shard boundaries on 4-point multiples).
  * Inside this process the rows are split into nshard (1..8) row ranges that

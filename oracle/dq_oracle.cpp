@@ -395,6 +395,42 @@ void dqo_block_hist(const uint32_t* quant, uint32_t width, uint32_t height,
     }
 }
 
+// ---- BGR24 <-> packed frames ----------------------------
+// Vec3BToUID (superpixels/OpenCVUtil.h:19-27) over a CV_8UC3 frame, row by
+// row as the loop at ClusteringSegmentation.cpp:381-395 visits it.
+void dqo_pack_bgr24(const uint8_t* bgr, uint32_t width, uint32_t height, uint32_t stride,
+                    uint32_t* out) {
+  for (uint32_t y = 0; y < height; ++y)
+    for (uint32_t x = 0; x < width; ++x) {
+      const uint8_t* v = bgr + (size_t)y * stride + 3u * x;   // v[0]=B v[1]=G v[2]=R
+      out[(size_t)y * width + x] = ((uint32_t)v[2] << 16) | ((uint32_t)v[1] << 8) | (uint32_t)v[0];
+    }
+}
+
+// PixelToVec3b (OpenCVUtil.h:53-59): B = bits 0-7, G = 8-15, R = 16-23.
+void dqo_unpack_bgr24(const uint32_t* in, uint32_t width, uint32_t height, uint32_t stride,
+                      uint8_t* bgr) {
+  for (uint32_t y = 0; y < height; ++y)
+    for (uint32_t x = 0; x < width; ++x) {
+      const uint32_t p = in[(size_t)y * width + x];
+      uint8_t* v = bgr + (size_t)y * stride + 3u * x;
+      v[0] = (uint8_t)(p & 0xFF);
+      v[1] = (uint8_t)((p >> 8) & 0xFF);
+      v[2] = (uint8_t)((p >> 16) & 0xFF);
+    }
+}
+
+// Region gather (ClusteringSegmentation.cpp:1795-1800): Coord {uint16 x, y}
+// (superpixels/Coord.h:30-33) as one word x | y << 16.
+void dqo_gather_bgr24(const uint8_t* bgr, uint32_t stride, const uint32_t* coords, uint32_t n,
+                      uint32_t* out) {
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t cx = coords[i] & 0xFFFFu, cy = coords[i] >> 16;
+    const uint8_t* v = bgr + (size_t)cy * stride + 3u * cx;
+    out[i] = ((uint32_t)v[2] << 16) | ((uint32_t)v[1] << 8) | (uint32_t)v[0];
+  }
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
