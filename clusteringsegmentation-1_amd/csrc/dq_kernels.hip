@@ -168,13 +168,13 @@ __device__ __forceinline__ void wave_range(uint32_t start, uint32_t end, uint32_
 // starting at or past `end` are not loaded; a vector straddling `end` is
 // loaded whole -- every working buffer keeps >= 3 readable words of slack
 // past each frame.
-template <bool FULL>
+template <bool FULL, bool NT = false>
 __device__ __forceinline__ void load_sweep(g_cu4* src4, uint32_t vs, uint32_t end,
                                            u32x4 v[kVecPerThread]) {
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
     const uint32_t i = vs + 4u * (j * 64 + lane_id());
-    if (FULL || i < end) v[j] = src4[i >> 2];
+    if (FULL || i < end) v[j] = NT ? __builtin_nontemporal_load(src4 + (i >> 2)) : src4[i >> 2];
     else v[j] = (u32x4){0u, 0u, 0u, 0u};
   }
 }
@@ -939,6 +939,14 @@ __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
 #ifndef DQ_PS_PREFETCH
 #define DQ_PS_PREFETCH 0
 #endif
+// Cache policy of partsplit's streams (a parent's points are read once, its
+// children's written once): nontemporal loads, store cache-policy bits
+#ifndef DQ_PS_NTLOAD
+#define DQ_PS_NTLOAD 0
+#endif
+#ifndef DQ_PS_STORE_AUX
+#define DQ_PS_STORE_AUX 0
+#endif
 // This wave's points of one sweep, slot by slot, ranked by ballot; raw
 // buffer stores (SGPR descriptor + 32-bit offset).  In a full sweep every
 // slot is valid: a lane's rank among the new points is its lane id minus
@@ -960,7 +968,7 @@ __device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32
       const uint32_t ro = mbcnt64(bo);
       const uint32_t idx = o ? oc + ro : nc + (l - ro);
       __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
-                                            (int)(idx * 4u), 0, 0);
+                                            (int)(idx * 4u), 0, DQ_PS_STORE_AUX);
       if (PRE) {
         ax += (xcut >> sidx) & (uint32_t)(idx < ex);
         ay += (ycut >> sidx) & (uint32_t)(idx < ey) & 1u;
@@ -977,7 +985,7 @@ __device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32
       uint32_t idx = o ? oc + mbcnt64(bo) : nc + mbcnt64(bn);
       idx = (o || n) ? idx : 0x3FFFFFFFu;
       __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
-                                            (int)(idx * 4u), 0, 0);
+                                            (int)(idx * 4u), 0, DQ_PS_STORE_AUX);
       if (PRE) {
         ax += (xcut >> sidx) & (uint32_t)(idx < ex);
         ay += (ycut >> sidx) & (uint32_t)(idx < ey) & 1u;
@@ -1016,8 +1024,8 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
   uint32_t vs = start & ~3u;
   bool full = vs >= start && vs + kWaveSweep <= end;
   if (vs < end) {
-    if (full) load_sweep<true>(src4, vs, end, v);
-    else load_sweep<false>(src4, vs, end, v);
+    if (full) load_sweep<true, DQ_PS_NTLOAD>(src4, vs, end, v);
+    else load_sweep<false, DQ_PS_NTLOAD>(src4, vs, end, v);
   }
   while (vs < end) {
     uint32_t oldm, validm;
@@ -1079,8 +1087,8 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
 #if DQ_PS_PREFETCH
     u32x4 vn[kVecPerThread];
     if (nvs < end) {
-      if (nfull) load_sweep<true>(src4, nvs, end, vn);
-      else load_sweep<false>(src4, nvs, end, vn);
+      if (nfull) load_sweep<true, DQ_PS_NTLOAD>(src4, nvs, end, vn);
+      else load_sweep<false, DQ_PS_NTLOAD>(src4, nvs, end, vn);
     }
 #endif
     // --- this wave's points (store_sweep).  A sweep writes at most kWaveSweep points to each child: when neither
@@ -1098,8 +1106,8 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
     for (int j = 0; j < kVecPerThread; ++j) v[j] = vn[j];
 #else
     if (nvs < end) {
-      if (nfull) load_sweep<true>(src4, nvs, end, v);
-      else load_sweep<false>(src4, nvs, end, v);
+      if (nfull) load_sweep<true, DQ_PS_NTLOAD>(src4, nvs, end, v);
+      else load_sweep<false, DQ_PS_NTLOAD>(src4, nvs, end, v);
     }
 #endif
     vs = nvs;
