@@ -1484,7 +1484,7 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
     for (int i = threadIdx.x; i <= k; i += kMapLdsBlock) {
       const uint32_t q = i < k ? gpal[i] : 0u;
       const uint32_t c2 = i < k ? __builtin_amdgcn_udot4(q, q, 0u, false) + (1u << 19) : 0xFFFFFu;
-      spal[i] = make_uint2(q, c2);
+      spal[i] = make_uint2(q, c2 << 12);   // c2 < 2^20: the key's distance field, pre-shifted
     }
     g_cu16* glut = (g_cu16*)tk.lut;
     for (int i = threadIdx.x; i < 766; i += kMapLdsBlock) slut[i] = glut[i];
@@ -1498,11 +1498,13 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   typedef __attribute__((address_space(1))) u32x4 g_u4;
   g_u4* out4 = (g_u4*)as_gw(tk.out);
 
+  // (c2 - 2 dot) << 12 | sad, as (c2 << 12) - (dot << 13) + sad: the low 12
+  // bits of the first two terms are zero and sad < 4096, so the OR is an add
+  // and folds into v_sad_u16's accumulator (same 32-bit key as map_kernel)
   auto key = [&](uint32_t p, uint32_t S, uint32_t j) -> uint32_t {
     const uint2 en = spal[j];
-    const uint32_t d = (uint32_t)((int32_t)en.y - 2 * (int32_t)__builtin_amdgcn_udot4(p, en.x, 0u, false));
-    const uint32_t sad = __builtin_amdgcn_sad_u16(4u * j, S, 0u);
-    return (d << 12) | sad;
+    const uint32_t hi = en.y - (__builtin_amdgcn_udot4(p, en.x, 0u, false) << 13);
+    return __builtin_amdgcn_sad_u16(4u * j, S, hi);
   };
   auto answer = [&](uint32_t S, uint32_t best) -> uint32_t {
     return spal[entry_from_sad<false>(S, best & 0xFFFu)].x;
@@ -1512,8 +1514,8 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
            (((p >> (16 - kCellBits)) & ((1u << kCellBits) - 1)) << kCellBits) |
            ((p >> (8 - kCellBits)) & ((1u << kCellBits) - 1));
   };
-  auto start_of = [&](uint32_t p) -> uint32_t {
-    return 4u * slut[((p >> 16) & 0xFF) + ((p >> 8) & 0xFF) + (p & 0xFF)] + 1u;
+  auto start_of = [&](uint32_t p) -> uint32_t {   // p < 2^24: R + G + B in one dot4
+    return 4u * slut[__builtin_amdgcn_udot4(p, 0x00010101u, 0u, false)] + 1u;
   };
   // the exact answer for a pixel of an overflow cell (record r)
   auto resolve = [&](uint32_t p, uint32_t S, uint32_t r) -> uint32_t {
