@@ -1509,10 +1509,13 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   auto answer = [&](uint32_t S, uint32_t best) -> uint32_t {
     return spal[entry_from_sad<false>(S, best & 0xFFFu)].x;
   };
-  auto cell_of = [](uint32_t p) -> uint32_t {
-    return ((p >> (24 - kCellBits)) << (2 * kCellBits)) |
-           (((p >> (16 - kCellBits)) & ((1u << kCellBits) - 1)) << kCellBits) |
-           ((p >> (8 - kCellBits)) & ((1u << kCellBits) - 1));
+  // the record of p's cell: byte offset 4 * cell = (R'' << 10) + (G'' << 5) + B''
+  // with X'' = (X >> 3) << 2, the bytes of m = (p >> 1) & 0x7C7C7C
+  static_assert(kCellBits == 5, "cell record offset assumes 5 bits per channel");
+  auto cell_rec = [&](uint32_t p) -> uint32_t {
+    const uint32_t m = (p >> 1) & 0x7C7C7Cu;
+    const uint32_t off = ((m >> 16) << 10) + __builtin_amdgcn_udot4(m, 0x00002001u, 0u, false);
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(stab) + off);
   };
   auto start_of = [&](uint32_t p) -> uint32_t {   // p < 2^24: R + G + B in one dot4
     return 4u * slut[__builtin_amdgcn_udot4(p, 0x00010101u, 0u, false)] + 1u;
@@ -1553,7 +1556,7 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
     uint32_t res[kMapPx], rec[kMapPx], Ss[kMapPx];
 #pragma unroll
     for (int e = 0; e < kMapPx; ++e) {
-      rec[e] = stab[cell_of(px[e])];
+      rec[e] = cell_rec(px[e]);
       Ss[e] = start_of(px[e]);
     }
 #pragma unroll
@@ -1582,7 +1585,7 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (lane < min(qn, (uint32_t)kMapQ)) {
         const uint32_t p = wq[lane];
-        wq[lane] = resolve(p, start_of(p), stab[cell_of(p)]);
+        wq[lane] = resolve(p, start_of(p), cell_rec(p));
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
