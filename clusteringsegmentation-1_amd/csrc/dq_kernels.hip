@@ -1561,11 +1561,14 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
     }
 #pragma unroll
     for (int e = 0; e < kMapPx; ++e) {
+      // keys of distinct entries differ (the tie field is |4j - S|, S odd), so
+      // the answer is the winning candidate's own entry: no second palette read
       const uint32_t p = px[e], S = Ss[e], r = rec[e];
-      uint32_t best = key(p, S, r & 0x3FFu);
-      best = min(best, key(p, S, (r >> 10) & 0x3FFu));
-      best = min(best, key(p, S, (r >> 20) & 0x3FFu));
-      res[e] = answer(S, best);
+      const uint32_t j0 = r & 0x3FFu, j1 = (r >> 10) & 0x3FFu, j2 = (r >> 20) & 0x3FFu;
+      const uint32_t q0 = spal[j0].x, q1 = spal[j1].x, q2 = spal[j2].x;
+      const uint32_t k0 = key(p, S, j0), k1 = key(p, S, j1), k2 = key(p, S, j2);
+      const uint32_t best = min(k0, min(k1, k2));
+      res[e] = best == k0 ? q0 : (best == k1 ? q1 : q2);
     }
     // overflow cells: queue (slot order), resolve cooperatively, read back
     uint32_t qpos[kMapPx];
