@@ -7,27 +7,33 @@
 Workload (BASELINE.json metric "Mpixels/sec DivQuant K=256 on 4K RGB"):
 
 * --mode frames (default): one step = quant_recurse (K=256, max_iters=10,
-  cluster + colortable dedup + map) on each of the F synthetic uniform-random
-  24-bit 3840x2160 frames this rank owns, already resident in HBM, in ONE
-  batched call (every pass of a split round is one launch over all F frames).
+  cluster + colortable dedup + map) on each of the F synthetic 3840x2160
+  frames this rank owns, already resident in HBM, in ONE batched call.
   Default F = 8: C4's per-GPU share (C4 = 64 4K frames over 8 GPUs, so
   --gpus 8 is exactly C4).  Frames are independent objects: no data-path
-  collective, "scaling": "weak".  The single-frame latency of C3 (one 4K
-  frame per call) is measured in the same run and reported in detail.c3.
-* --mode rows: ONE frame of the config (e.g. --config c5: the 16384x16384
-  K=1024 gigapixel tile) row-tile sharded over the N ranks; every pass's
-  integer node totals are allreduced with RCCL over xGMI ("scaling":
-  "strong": the total work is fixed).
+  collective, "scaling": "weak".  The same run also measures C3 (one 4K
+  frame per call: detail.c3) and C4's row-tile variant (all 64 frames, each
+  row-sharded over the N ranks, one RCCL allreduce of every frame's node
+  totals per pass: detail.c4_rowtile).
+* --mode rows: F frames of the config (default 1; --config c5: the
+  16384x16384 K=1024 gigapixel tile) row-tile sharded over the N ranks; every
+  pass's integer node totals of all frames are allreduced in one RCCL call
+  ("scaling": "strong": the total work is fixed).
+
+Frames are the SURVEY 8c/8d generator (xorshift64, frame f = seed + f); the
+outputs of the timed work are checked against the reference build's golden
+fixtures (tests/golden/c4.json, big.json) after the timed region and the run
+FAILS on a mismatch ("verified" field).
 
 N>1 is launched by torch.distributed.run, one rank per GPU.  Prints ONE JSON
 line on rank 0.  `roofline` is the kernel with the largest measured time in
 the step, timed live on the library's stream with HIP events around every
-launch, against the 8 TB/s HBM peak; `traffic` comes from the committed
-rocprofv3 PMC counters of the same command (profiles/pmc_traffic.json, see
-tools/pmc_bench.sh) when they exist.  `cpu_baseline` times the reference
-DivQuant (oracle/_ref, built from the unmodified reference sources) -- or,
-if that build is absent, the oracle's restatement -- on one 4K frame, one
-host core, rank 0 at N=1 only.
+launch, against the 8 TB/s HBM peak, with its bytes from the engine work
+model; `traffic` comes from the committed rocprofv3 PMC
+counters of the same command (profiles/pmc_traffic.json).  `cpu_baseline`
+times the reference DivQuant (oracle/_ref, built from the unmodified
+reference sources) -- or, if that build is absent, the oracle's restatement --
+on one 4K frame, one host core, rank 0 at N=1 only.
 """
 import argparse
 import ctypes
@@ -41,11 +47,11 @@ import numpy as np
 # The engine overlaps frames on two lanes (HIP streams); with HIP's default
 # of 4 hardware queues per process the lanes' streams and torch's sometimes
 # share a queue and serialise (measured: ~1 run in 5 at the one-lane speed).
-# 8 queues keep them apart; set before HIP initialises (torch import).
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 CONFIGS = {   # BASELINE.json configs (C4 = 64 x c3 frames; C5 = c5 row-sharded)
     "c1": (256, 256, 16),
@@ -54,11 +60,16 @@ CONFIGS = {   # BASELINE.json configs (C4 = 64 x c3 frames; C5 = c5 row-sharded)
     "c5": (16384, 16384, 1024),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# algorithmic bytes of the kernel kinds the roofline may name (bytes per point
-# the engine attributes to each launch: 4 read, +4 written for the partition)
-ROOF_KERNELS = {"pass_kmeans": "pass_kernel<PASS_KMEANS>", "partition": "partsplit_kernel",
-                "pass_split": "pass_kernel<PASS_SPLIT>", "pass_init": "pass_kernel<PASS_INIT>",
-                "map": "map_kernel"}
+# kernel kinds the roofline may name -> (kernel symbol, engine-model bytes per
+# point, SURVEY 8(d)-model bytes per point).  Engine model:
+# every statistics pass reads 4 B per swept point, the fused partition +
+# split pass reads 4 B and writes 4 B per parent point, the map reads 4 B and
+# writes 4 B per pixel.  SURVEY 8(d) counts the partition's write as overhead.
+ROOF_KERNELS = {"pass_kmeans": ("kpass_kernel<PASS_KMEANS>", 4, 4),
+                "partition": ("partsplit_kernel", 8, 4),
+                "pass_split": ("pass_kernel<PASS_SPLIT>", 4, 4),
+                "pass_init": ("pass_kernel<PASS_INIT>", 4, 4),
+                "map": ("map_lds_kernel", 8, 8)}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -67,15 +78,24 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: c3 (frames mode), c5 (rows mode)")
     ap.add_argument("--mode", default="frames", choices=["frames", "rows"])
-    ap.add_argument("--frames", type=int, default=8, help="frames per rank per step (frames mode)")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="frames per rank per step (frames mode, default 8) / frames per step (rows, default 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline region")
     ap.add_argument("--no-c3", action="store_true", help="skip the single-frame C3 measurement")
+    ap.add_argument("--no-rowtile", action="store_true", help="skip the C4 row-tile measurement")
+    ap.add_argument("--no-verify", action="store_true", help="skip the golden-fixture check")
     ap.add_argument("--lanes", type=int, default=0,
                     help="engine lanes per batch (0: library default); the roofline region always uses 1")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config is None:
+        a.config = "c5" if a.mode == "rows" else "c3"
+    if a.frames is None:
+        a.frames = 8 if a.mode == "frames" else 1
+    return a
 
 
 def cpu_baseline(w, h, k):
@@ -112,8 +132,8 @@ def cpu_baseline(w, h, k):
         os.close(saved)
         os.close(devnull)
     return {"value": round(w * h / dt / 1e6, 4), "unit": "Mpix/s", "cores": 1, "kind": kind,
-            "sample": "one %dx%d frame, K=%d, quant_recurse(allPixelsUnique=1), %.2f s, single thread "
-                      "(host has %d cores)" % (w, h, k, dt, os.cpu_count() or 0)}
+            "sample": "one %dx%d frame (synthetic frame 0), K=%d, quant_recurse(allPixelsUnique=1), "
+                      "%.2f s, single thread (host has %d cores)" % (w, h, k, dt, os.cpu_count() or 0)}
 
 
 def init_dist():
@@ -129,9 +149,10 @@ def init_dist():
     return rank, world, local
 
 
-def frame_seed(rank, frame):
-    """Each rank owns its own frames (weak scaling, no data-path collective)."""
-    return 0x5EED + 1000 * rank + frame
+def frame_id(rank, i, nf):
+    """Weak scaling: rank r owns frames [r*nf, (r+1)*nf) of the global batch
+    (at N=8, nf=8: C4's 64 frames, each rank a distinct eighth)."""
+    return rank * nf + i
 
 
 def row_range(h, rank, world):
@@ -164,6 +185,63 @@ def max_over_ranks(dt, world, device="cpu"):
     return float(t.item())
 
 
+def all_ranks_ok(ok, world, device):
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return ok
+    t = torch.tensor([0 if ok else 1], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item()) == 0
+
+
+# ---------------------------------------------------------------------------
+# Golden-fixture checks (the reference build's outputs, tests/golden/).
+_fix_cache = {}
+
+
+def fixture(name):
+    if name not in _fix_cache:
+        path = os.path.join(GOLDEN, name)
+        _fix_cache[name] = json.load(open(path)) if os.path.exists(path) else {}
+    return _fix_cache[name]
+
+
+def frame_fixture(w, h, k, f):
+    """The reference's (out_fnv, ct, band_fnv) of synthetic frame f, or None."""
+    if (w, h, k) == (3840, 2160, 256):
+        return fixture("c4.json").get("f%02d" % f)
+    if f == 0:
+        return fixture("big.json").get("%dx%d_k%d" % (w, h, k))
+    return None
+
+
+def check_frame(pkg, out_t, ct, fix, rows=None, h=None, world=1, rank=0):
+    """Compare one frame's output (whole frame, or this rank's row band) and
+    colortable with the fixture.  Returns True / False / None (no fixture)."""
+    if fix is None:
+        return None
+    if [int(v) for v in ct] != fix["ct"]:
+        return False
+    out = out_t.cpu().numpy().view(np.uint32)
+    if rows is None:
+        return "%016x" % pkg.fnv1a64(out) == fix["out_fnv"]
+    bands = fix.get("band_fnv")
+    if world == 1:
+        return "%016x" % pkg.fnv1a64(out) == fix["out_fnv"]
+    if not bands or 8 % world != 0:
+        return None
+    per = 8 // world   # this rank's rows = bands [rank*per, (rank+1)*per)
+    bh = h // 8
+    w = out.size // (rows[1] - rows[0])
+    for j in range(per):
+        b = rank * per + j
+        lo = (b * bh - rows[0]) * w
+        if "%016x" % pkg.fnv1a64(out[lo:lo + bh * w]) != bands[b]:
+            return False
+    return True
+
+
 def pick_roofline(stats, pmc_key):
     """The roofline object of the kernel kind with the largest measured time."""
     cand = {k: v for k, v in stats.items() if k in ROOF_KERNELS and v[0] > 0 and v[1] > 0 and v[2] > 0}
@@ -171,24 +249,39 @@ def pick_roofline(stats, pmc_key):
         return None
     kind = max(cand, key=lambda k: cand[k][1])
     launches, ms, alg = cand[kind]
+    sym, b_eng, b_survey = ROOF_KERNELS[kind]
     gbs = alg / (ms / 1e3) / 1e9
     roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": ROOF_KERNELS[kind], "launches": launches,
+            "kernel": sym, "launches": launches,
             "avg_launch_us": round(ms * 1e3 / launches, 2),
             "alg_bytes_per_launch": round(alg / launches),
+            "alg_model": "engine work model (DESIGN.md 5): %d B per point of this kernel" % b_eng,
+            "frac_survey_model": round(gbs * b_survey / b_eng / HBM_PEAK_GBS, 4),
+            "survey_model": "SURVEY 8(d): %d B per point (a partition's write is overhead)" % b_survey,
             "share_of_step_kernel_time": round(ms / sum(v[1] for v in stats.values() if v[1] > 0), 3),
             "measured": "HIP events around every launch on the engine's stream, one engine lane "
                         "(kernels not overlapped), same workload as the timed region"}
     if os.path.exists(PMC_FILE):
         try:
-            pmc = json.load(open(PMC_FILE)).get(pmc_key, {}).get(ROOF_KERNELS[kind])
+            pmc = json.load(open(PMC_FILE)).get(pmc_key, {}).get(sym)
         except ValueError:
             pmc = None
         if pmc:
             roof["traffic"] = round(pmc["hbm_bytes_per_launch"])
             roof["traffic_source"] = pmc["source"]
     return roof
+
+
+def upload_frames(torch, pkg, dev, w, h, ids, rows=None):
+    """Synthetic frames `ids` on the device (whole, or rows [r0, r1) of each)."""
+    ts = []
+    for f in ids:
+        px = pkg.synth_frame(w * h, f)
+        if rows is not None:
+            px = px[rows[0] * w:rows[1] * w]
+        ts.append(torch.from_numpy(px.view(np.int32)).to(dev))
+    return ts
 
 
 def main():
@@ -201,23 +294,25 @@ def main():
     dev = torch.device("cuda", local)
     pkg = load_package()
     stream = torch.cuda.current_stream(dev)
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
 
     w, h, k = CONFIGS[a.config]
     n = w * h
+    nf = a.frames
+    verify = []   # (name, out tensor, colortable getter, fixture, rows)
     if a.mode == "frames":
-        nf = a.frames
-        frames = []
-        for f in range(nf):
-            g = torch.Generator(device=dev)
-            g.manual_seed(frame_seed(rank, f))
-            frames.append(torch.randint(0, 1 << 24, (n,), dtype=torch.int32, device=dev, generator=g))
+        ids = [frame_id(rank, i, nf) for i in range(nf)]
+        frames = upload_frames(torch, pkg, dev, w, h, ids)
         outs = [torch.empty_like(f) for f in frames]
+        last = {}
 
         def step():   # one batched call: every pass of a round covers all frames
             if nf == 1:
-                pkg.quant_device(frames[0], outs[0], k, max_iters=10, device=local, stream=stream)
+                ct, _ = pkg.quant_device(frames[0], outs[0], k, max_iters=10, device=local, stream=stream)
+                last["cts"] = [ct]
             else:
-                pkg.quant_batch_device(frames, outs, k, max_iters=10, device=local, stream=stream)
+                last["cts"], _ = pkg.quant_batch_device(frames, outs, k, max_iters=10, device=local,
+                                                        stream=stream)
         px_per_step = n * nf * world
         workload = ("C4 per-GPU share: %d x %dx%d frames per rank per step, K=%d, quant_recurse "
                     "max_iters=10 (cluster + dedup + map), one batched call" % (nf, w, h, k)
@@ -228,25 +323,16 @@ def main():
         if world > 1:
             pkg.comm_init_torch(device=local)
         r0, r1 = row_range(h, rank, world)
-        g = torch.Generator(device=dev)
-        g.manual_seed(frame_seed(0, 0))   # the same frame on every rank; each keeps its rows
-        mine = torch.empty(((r1 - r0) * w,), dtype=torch.int32, device=dev)
-        # generate the frame row-block by row-block (no full copy needed on any rank)
-        for rb in range(0, h, 1024):
-            blk = torch.randint(0, 1 << 24, (min(1024, h - rb) * w,), dtype=torch.int32, device=dev,
-                                generator=g)
-            lo, hi = max(rb, r0), min(rb + 1024, r1)
-            if lo < hi:
-                mine[(lo - r0) * w:(hi - r0) * w] = blk[(lo - rb) * w:(hi - rb) * w]
-        out = torch.empty_like(mine)
+        frames = upload_frames(torch, pkg, dev, w, h, range(nf), rows=(r0, r1))
+        outs = [torch.empty_like(f) for f in frames]
+        last = {}
 
         def step():
-            pkg.quant_rows_device([mine], [out], k, widths=[w], n_globals=[n], nshard=1,
-                                  max_iters=10, device=local, stream=stream)
-        nf = 1
-        px_per_step = n
-        workload = ("%s: one %dx%d frame, K=%d, row-tile sharded over %d rank(s), RCCL allreduce "
-                    "of the node totals per pass" % (a.config.upper(), w, h, k, world))
+            last["cts"], _ = pkg.quant_rows_device(frames, outs, k, widths=[w] * nf, n_globals=[n] * nf,
+                                                   nshard=1, max_iters=10, device=local, stream=stream)
+        px_per_step = n * nf
+        workload = ("%s: %d x %dx%d frame(s), K=%d, row-tile sharded over %d rank(s), one RCCL "
+                    "allreduce of all frames' node totals per pass" % (a.config.upper(), nf, w, h, k, world))
         parallelism = "row-tiles x%d" % world
         scaling = "strong"
 
@@ -256,7 +342,30 @@ def main():
         step()
     # --- timed region: no per-launch events (they would perturb the timing)
     pkg.set_timing(False, device=local)
-    dt = timed_region(step, a.steps, world, lambda: torch.cuda.synchronize(dev))
+    dt = timed_region(step, a.steps, world, sync)
+    # --- correctness of the timed work: the last step's outputs vs the reference
+    verified = None
+    if not a.no_verify:
+        sync()
+        res = []
+        for i in range(nf):
+            if a.mode == "frames":
+                fix = frame_fixture(w, h, k, ids[i])
+                res.append(check_frame(pkg, outs[i], last["cts"][i], fix))
+            else:
+                fix = frame_fixture(w, h, k, i)
+                res.append(check_frame(pkg, outs[i], last["cts"][i], fix, rows=(r0, r1), h=h,
+                                       world=world, rank=rank))
+        checked = [r for r in res if r is not None]
+        ok = all_ranks_ok(all(checked), world, dev)
+        verified = {"ok": ok, "frames_checked_rank0": len(checked), "frames_rank0": nf,
+                    "against": "reference build outputs (tests/golden/%s): colortable + out FNV-1a-64%s"
+                               % ("c4.json" if (w, h, k) == (3840, 2160, 256) else "big.json",
+                                  " of this rank's row bands" if a.mode == "rows" and world > 1 else "")}
+        if not ok:
+            print(json.dumps({"error": "bench outputs differ from the reference fixtures",
+                              "verified": verified, "per_frame_rank%d" % rank: res}), flush=True)
+            sys.exit(3)
     # --- roofline region: the same steps again with HIP events around every
     # launch (on the library's launch stream) for per-kernel durations
     stats = {}
@@ -269,7 +378,7 @@ def main():
         pkg.set_timing(True, device=local)
         for _ in range(a.steps):
             step()
-        torch.cuda.synchronize(dev)
+        sync()
         pkg.set_timing(False, device=local)
         stats = pkg.get_stats(device=local)
         pkg.set_lanes(a.lanes)
@@ -280,15 +389,64 @@ def main():
     # --- C3 single-frame latency (same frame shape, one frame per call)
     c3 = None
     if a.mode == "frames" and not a.no_c3 and nf > 1:
+        last3 = {}
+
         def one():
-            pkg.quant_device(frames[0], outs[0], k, max_iters=10, device=local, stream=stream)
+            last3["ct"], _ = pkg.quant_device(frames[0], outs[0], k, max_iters=10, device=local,
+                                              stream=stream)
         for _ in range(2):
             one()
-        dt1 = timed_region(one, a.steps, world, lambda: torch.cuda.synchronize(dev))
+        dt1 = timed_region(one, a.steps, world, sync)
         dt1 = max_over_ranks(dt1, world, dev)
+        ok1 = None
+        if not a.no_verify:
+            sync()
+            ok1 = all_ranks_ok(check_frame(pkg, outs[0], last3["ct"], frame_fixture(w, h, k, ids[0])) is not False,
+                               world, dev)
+            if not ok1:
+                print(json.dumps({"error": "C3 output differs from the reference fixture"}), flush=True)
+                sys.exit(3)
         c3 = {"ms_per_frame": round(dt1 * 1e3 / a.steps, 3),
               "Mpix_per_s": round(n * world * a.steps / dt1 / 1e6, 2),
-              "workload": "one %dx%d frame per call (C3), %d rank(s)" % (w, h, world)}
+              "workload": "one %dx%d frame per call (C3), %d rank(s)" % (w, h, world),
+              "verified": ok1}
+
+    # --- C4 row-tile variant: all 64 frames, each row-sharded over the ranks
+    rowtile = None
+    if a.mode == "frames" and not a.no_rowtile and (w, h, k) == (3840, 2160, 256):
+        del frames, outs
+        torch.cuda.empty_cache()
+        if world > 1:
+            pkg.comm_init_torch(device=local)
+        r0, r1 = row_range(h, rank, world)
+        nrt = 64
+        rf = upload_frames(torch, pkg, dev, w, h, range(nrt), rows=(r0, r1))
+        ro = [torch.empty_like(f) for f in rf]
+        lastr = {}
+
+        def rstep():
+            lastr["cts"], _ = pkg.quant_rows_device(rf, ro, k, widths=[w] * nrt, n_globals=[n] * nrt,
+                                                    nshard=1, max_iters=10, device=local, stream=stream)
+        rstep()
+        rsteps = max(1, min(3, a.steps))
+        dtr = max_over_ranks(timed_region(rstep, rsteps, world, sync), world, dev)
+        okr = None
+        if not a.no_verify:
+            sync()
+            rr = [check_frame(pkg, ro[i], lastr["cts"][i], frame_fixture(w, h, k, i), rows=(r0, r1), h=h,
+                              world=world, rank=rank) for i in range(nrt)]
+            okr = all_ranks_ok(all(r is not False for r in rr), world, dev)
+            if not okr:
+                print(json.dumps({"error": "C4 row-tile outputs differ from the reference fixtures"}), flush=True)
+                sys.exit(3)
+        rowtile = {"ms_per_step": round(dtr * 1e3 / rsteps, 3),
+                   "Mpix_per_s": round(n * nrt * rsteps / dtr / 1e6, 2), "steps": rsteps,
+                   "workload": "C4 row-tile variant: 64 x %dx%d frames, K=%d, each frame's rows split over "
+                               "%d rank(s), one RCCL allreduce of all frames' node totals per pass"
+                               % (w, h, k, world),
+                   "scaling": "strong", "verified": okr}
+        if world > 1:
+            pkg.comm_destroy(device=local)
 
     dt = max_over_ranks(dt, world, dev)
     value = px_per_step * a.steps / dt / 1e6
@@ -296,10 +454,9 @@ def main():
     if rank == 0:
         pmc_key = "%s_%s_f%d_n%d" % (a.mode, a.config, nf, world)
         roof = pick_roofline(stats, pmc_key) if stats else None
-        # whole-pipeline algorithmic bytes (B_alg = 4N + 44*sum|C_j| + 8N;
-        # sum|C_j| = log2(K) N for uniform inputs)
-        lk = int(round(np.log2(k)))
-        b_alg = (4 + 44 * lk + 8) * px_per_step * a.steps
+        # engine-model bytes of all kernels of the roofline region, per step,
+        # over the timed step's wall time (<= 1: they are bytes the kernels move)
+        eng_bytes = sum(v[2] for v in stats.values()) / max(1, a.steps)
         res = {
             "metric": "Mpixels/sec DivQuant K=%d on %dx%d RGB" % (k, w, h),
             "value": round(value, 2),
@@ -312,17 +469,21 @@ def main():
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8x3 pixels in u32, u32/u64 integer sums, f64 updates",
-            "data": "synthetic uniform-random 24-bit RGB frames (torch.randint on device)",
+            "data": "synthetic uniform-random 24-bit RGB frames (SURVEY 8c xorshift64, frame f = seed + f)",
             "config": {"workload": workload, "frames_per_rank_per_step": nf if a.mode == "frames" else None,
+                       "frames_per_step": nf if a.mode == "rows" else None,
                        "engine_lanes": lanes if a.mode == "frames" else 1,
                        "width": w, "height": h, "k": k, "max_iters": 10, "parallelism": parallelism},
+            "verified": verified,
             "roofline": roof,
-            "detail": {"ms_per_frame": round(dt * 1e3 / a.steps / (nf * world if a.mode == "frames" else 1), 3),
-                       "pipeline_alg_GBps": round(b_alg / dt / 1e9, 1),
-                       "pipeline_alg_frac_per_gpu": round(b_alg / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
+            "detail": {"ms_per_frame": round(dt * 1e3 / a.steps / (nf * world if a.mode == "frames" else nf), 3),
+                       "pipeline_engine_GBps_per_gpu": round(eng_bytes / (dt / a.steps) / 1e9, 1) if stats else None,
+                       "pipeline_engine_frac_per_gpu": round(eng_bytes / (dt / a.steps) / 1e9 / HBM_PEAK_GBS, 4)
+                       if stats else None,
                        "rounds_last_frame": rounds, "points_swept_last_call": swept,
                        "points_full_iterations_last_call": full,
                        "c3": c3,
+                       "c4_rowtile": rowtile,
                        "kernels": {kname: {"launches": v[0], "ms": round(v[1], 3),
                                            "GBps": round(v[2] / (v[1] / 1e3) / 1e9, 1) if v[1] > 0 and v[2] > 0 else None}
                                    for kname, v in stats.items() if v[0]}},

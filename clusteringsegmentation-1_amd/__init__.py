@@ -93,6 +93,8 @@ def lib():
         "dq_hip_block_hist_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, vp, c.c_int, c.c_uint32,
                                    c.c_uint32, c.c_uint32, vp, vp, vp, vp, vp, vp], c.c_int),
         "dq_subdivided_colors": ([vp], None),
+        "dq_synth_xorshift": ([vp, c.c_uint64, c.c_uint64], None),
+        "dq_fnv1a64": ([vp, c.c_uint64], c.c_uint64),
         "dq_hip_pack_bgr24_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp, vp], c.c_int),
         "dq_hip_unpack_bgr24_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp, vp],
                                     c.c_int),
@@ -311,6 +313,25 @@ def gather_bgr24_device(t_bgr, stride, t_coords, n, t_out, device=0, stream=None
     if lib().dq_hip_gather_bgr24_dev(device, _dptr(t_bgr), stride, _dptr(t_coords), n,
                                      _dptr(t_out), _stream_ptr(stream)) < 0:
         raise DivQuantError("dq_hip_gather_bgr24_dev: bad arguments")
+
+
+# ---------------------------------------------------------------------------
+# Synthetic benchmark frames and the fixtures' output checksum (host code).
+SYNTH_SEED = 0x9E3779B97F4A7C15
+
+
+def synth_frame(n, frame=0, seed=SYNTH_SEED):
+    """Frame `frame` of the benchmark batch: n xorshift64 draws
+    & 0xFFFFFF from seed + frame."""
+    out = np.empty(n, np.uint32)
+    lib().dq_synth_xorshift(_ptr(out), n, (seed + frame) & 0xFFFFFFFFFFFFFFFF)
+    return out
+
+
+def fnv1a64(a):
+    """Word-wise FNV-1a-64 of a uint32 array (the golden fixtures' out_fnv)."""
+    a = _u32(a).reshape(-1)
+    return int(lib().dq_fnv1a64(_ptr(a), a.size))
 
 
 # ---------------------------------------------------------------------------

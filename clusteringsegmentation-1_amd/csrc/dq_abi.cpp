@@ -121,11 +121,18 @@ int dq_hip_block_hist_dev(int device, const uint32_t* d_in, uint32_t width, uint
     return -1;
   Engine& e = engine_for(device);
   std::lock_guard<std::mutex> g(e.mutex());
-  e.map(d_in, width * height, d_quant, palette, npal, (hipStream_t)stream);
-  uint32_t* work = e.scratch_words(dq::block_hist_scratch_words(block_w, block_h));
+  hipStream_t st = stream ? (hipStream_t)stream : e.stream();
+  e.map(d_in, width * height, d_quant, palette, npal, st);
+  // the tie queues are private to this call (stream-ordered allocation): the
+  // kernels are still running when the call returns, and another call may
+  // run on another stream meanwhile
+  uint32_t* work = nullptr;
+  DQ_HIP(hipMallocAsync((void**)&work, dq::block_hist_scratch_words(block_w, block_h) * 4, st));
   dq::BlockHistArgs a{d_quant, width, height, block_w, block_h, d_mode, d_ndistinct, d_keys, d_counts,
                       work, nullptr, 0};
-  return dq::launch_block_hist(a, (int)dim, (hipStream_t)stream);
+  const int rc = dq::launch_block_hist(a, (int)dim, st);
+  DQ_HIP(hipFreeAsync(work, st));
+  return rc;
 }
 
 static bool bgr24_shape_ok(uint32_t width, uint32_t height, uint32_t stride) {
@@ -336,6 +343,27 @@ int dq_hip_map(const uint32_t* in, uint32_t n, uint32_t* out, const uint32_t* ct
   return 0;
 }
 
+// Synthetic frames of the benchmark configs (SURVEY 8c/8d generator) and the
+// output checksum the golden fixtures are keyed by.
+void dq_synth_xorshift(uint32_t* out, uint64_t n, uint64_t seed) {
+  uint64_t s = seed;
+  for (uint64_t i = 0; i < n; ++i) {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    out[i] = (uint32_t)(s & 0xFFFFFFu);
+  }
+}
+
+uint64_t dq_fnv1a64(const uint32_t* w, uint64_t n) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint64_t i = 0; i < n; ++i) {
+    h ^= w[i];
+    h *= 0x100000001b3ull;
+  }
+  return h;
+}
+
 void dq_subdivided_colors(uint32_t* out125) {
   static const uint32_t v[5] = {0, 63, 127, 191, 255};
   for (int i = 0; i < 125; ++i)   // R outermost, B innermost, alpha 0xFF (:874-888)
@@ -366,10 +394,12 @@ int dq_hip_block_hist(const uint32_t* in, uint32_t width, uint32_t height, const
     std::lock_guard<std::mutex> g(e.mutex());
     e.stage_in(in, (uint32_t)n, st);
     e.map(e.staged_in(), (uint32_t)n, e.staged_out(), palette, npal, st);
-    uint32_t* work = e.scratch_words(dq::block_hist_scratch_words(block_w, block_h));
+    uint32_t* work = nullptr;
+    DQ_HIP(hipMallocAsync((void**)&work, dq::block_hist_scratch_words(block_w, block_h) * 4, st));
     dq::BlockHistArgs a{e.staged_out(), width, height, block_w, block_h, d_mode, d_nd, d_keys, d_counts,
                         work, nullptr, 0};
     rc = dq::launch_block_hist(a, (int)dim, st);
+    DQ_HIP(hipFreeAsync(work, st));
     if (quant) DQ_HIP(hipMemcpyAsync(quant, e.staged_out(), n * 4, hipMemcpyDeviceToHost, st));
     DQ_HIP(hipMemcpyAsync(mode, d_mode, nb * 4, hipMemcpyDeviceToHost, st));
     if (ndistinct) DQ_HIP(hipMemcpyAsync(ndistinct, d_nd, nb * 4, hipMemcpyDeviceToHost, st));
@@ -380,7 +410,7 @@ int dq_hip_block_hist(const uint32_t* in, uint32_t width, uint32_t height, const
     DQ_HIP(hipStreamSynchronize(st));
   }
   for (uint32_t* p : {d_mode, d_nd, d_keys, d_counts})
-    if (p) DQ_HIP(hipFree(p));
+    if (p) DQ_HIP(hipFreeAsync(p, st));
   return rc;
 }
 

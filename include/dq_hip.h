@@ -56,6 +56,12 @@ int dq_hip_block_hist(const uint32_t *in, uint32_t width, uint32_t height,
                       uint32_t *counts);
 /* getSubdividedColors (superpixels/OpenCVUtil.cpp:853-897): 125 colours. */
 void dq_subdivided_colors(uint32_t *out125);
+/* Synthetic benchmark frames: xorshift64 s^=s<<13; s^=s>>7;
+ * s^=s<<17, one draw per pixel, pixel = draw & 0xFFFFFF; frame f of a batch
+ * uses seed 0x9E3779B97F4A7C15 + f.  Host memory, no GPU needed. */
+void dq_synth_xorshift(uint32_t *out, uint64_t n, uint64_t seed);
+/* Word-wise FNV-1a-64 of n uint32 words (the golden fixtures' output hash). */
+uint64_t dq_fnv1a64(const uint32_t *w, uint64_t n);
 
 /* ---- device-pointer entry points (inputs already resident in HBM) --------
  * d_in/d_out: device pointers on `device`; k/ct: host.  Synchronous with

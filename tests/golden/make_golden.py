@@ -132,6 +132,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true", help="also the 4K / 4096^2 configs (minutes)")
     ap.add_argument("--only", default="", help="comma list of sections")
+    ap.add_argument("--jobs", type=int, default=3, help="worker processes for the c4 section")
     a = ap.parse_args()
     only = set(a.only.split(",")) if a.only else None
     ref, instr = Ref(REF_SO), Ref(INSTR_SO)
@@ -236,6 +237,70 @@ def main():
     # ---- 8. host utilities of the ABI
     if want("utils"):
         utils_fixtures(ref)
+
+    # ---- 9. C4 at size: the 64 distinct 4K frames of the batch (frame f uses
+    #      seed SEED + f) -- hash, colortable, trace of every frame
+    if only is not None and "c4" in only:   # (explicit only: ~20 CPU-min)
+        c4_fixtures(a.jobs)
+
+    # ---- 10. C5 at size: 16384x16384 K=1024 (the LDS-spill map path);
+    #       ~13 CPU-min per reference run, ref and instr run in parallel
+    if only is not None and "c5" in only:   # (explicit only: ~13 CPU-min)
+        c5_fixture()
+
+
+def _c4_one(f):
+    ref, instr = Ref(REF_SO), Ref(INSTR_SO)
+    px = fx.xorshift(3840 * 2160, seed=fx.SEED + f)
+    out, ct, trace, means = full_run(ref, instr, px, 256)
+    r = rec(out, ct, trace)
+    # the 8 row bands of 270 rows rank r of N=8 owns (row-tile variant)
+    r["band_fnv"] = ["%016x" % fx.fnv(out[b * 270 * 3840:(b + 1) * 270 * 3840]) for b in range(8)]
+    return f, r, trace.astype(np.int32), means
+
+
+def c4_fixtures(jobs):
+    import multiprocessing as mp
+    res, arrs = {}, {}
+    with mp.get_context("fork").Pool(jobs) as pool:
+        for f, r, trace, means in pool.imap_unordered(_c4_one, range(64)):
+            res["f%02d" % f] = dict(w=3840, h=2160, k=256, seed="%x" % (fx.SEED + f), **r)
+            arrs["trace_f%02d" % f] = trace
+            arrs["means_f%02d" % f] = means
+            print("c4 frame", f, r["out_fnv"], flush=True)
+    fx.dump_json("c4.json", res)
+    np.savez_compressed(os.path.join(HERE, "c4.npz"), **arrs)
+
+
+def _c5_run(which):
+    r = Ref(REF_SO if which == "ref" else INSTR_SO)
+    px = fx.xorshift(16384 * 16384)
+    out, ct, err = r.quant(px, 1024, 1)
+    # row-band hashes: the 8 bands of 2048 rows rank r of N=8 owns (bench.py
+    # row_range); a rank of N<8 owns 8/N consecutive bands
+    bands = ["%016x" % fx.fnv(out[b * 2048 * 16384:(b + 1) * 2048 * 16384]) for b in range(8)]
+    return which, "%016x" % fx.fnv(out), ct, (err, bands)
+
+
+def c5_fixture():
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(2) as pool:
+        got = dict((w, (h, ct, err)) for w, h, ct, err in pool.map(_c5_run, ["ref", "instr"]))
+    h, ct, (_, bands) = got["ref"]
+    h2, ct2, (err, bands2) = got["instr"]
+    assert h == h2 and bands == bands2 and np.array_equal(ct, ct2), "instrumented build diverged"
+    trace, means = parse_instr(err, 1024)
+    key = "16384x16384_k1024"
+    path = os.path.join(HERE, "big.json")
+    big = json.load(open(path))
+    big[key] = dict(w=16384, h=16384, k=1024, out_fnv=h, ct=[int(v) for v in ct], k_out=int(len(ct)),
+                    band_fnv=bands, sum_split_sizes=int(trace[:, 2].sum()))
+    arrs = dict(np.load(os.path.join(HERE, "big.npz")))
+    arrs["trace_" + key] = trace.astype(np.int32)
+    arrs["means_" + key] = means
+    fx.dump_json("big.json", big)
+    np.savez_compressed(os.path.join(HERE, "big.npz"), **arrs)
+    print("c5", key, h, flush=True)
 
 
 def utils_fixtures(ref):

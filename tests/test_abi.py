@@ -130,3 +130,12 @@ def test_product_does_not_link_the_oracle(pkg):
     assert "dqoracle" not in deps and "dqref" not in deps
     syms = exported(pkg.LIB_PATH, demangle=False)
     assert "dqo_" not in syms
+
+
+def test_synth_frames_and_hash_match_the_fixture_spec(pkg):
+    """The bench's frame generator and checksum (product host code) equal the
+    oracle's (the spec every golden fixture was generated with)."""
+    for n, f in ((1, 0), (4099, 3), (100000, 63)):
+        a = pkg.synth_frame(n, f)
+        assert np.array_equal(a, fx.xorshift(n, seed=fx.SEED + f))
+        assert pkg.fnv1a64(a) == fx.fnv(a)

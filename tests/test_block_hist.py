@@ -169,3 +169,25 @@ def test_block_hist_device(gpu):
 def test_block_hist_bad_args(gpu):
     with pytest.raises(gpu.DivQuantError):
         gpu.gen_histograms_for_blocks(np.zeros((8, 8), np.uint32), superpixel_dim=5)
+
+
+@pytest.mark.gpu
+def test_block_hist_device_two_streams(gpu):
+    """Two asynchronous calls on two streams back to back: each call's tie
+    queues are its own, so both results are exact."""
+    import torch
+    h, w, dim = 1080, 1920, 4
+    frames = [_tie_frame(h, w, seed=11 + i, ncolors=4 + 4 * i) for i in range(2)]
+    bw, bh = gpu.block_grid(w, h, dim)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    ins = [torch.from_numpy(f.reshape(-1).view(np.int32)).to("cuda:0") for f in frames]
+    torch.cuda.synchronize()
+    qs = [torch.empty_like(t) for t in ins]
+    modes = [torch.empty(bw * bh, dtype=torch.int32, device="cuda:0") for _ in ins]
+    for _ in range(3):
+        for i in range(2):
+            gpu.block_hist_device(ins[i], w, h, qs[i], modes[i], superpixel_dim=dim, stream=streams[i])
+    torch.cuda.synchronize()
+    for i in range(2):
+        _, rmode, _, _, _ = _oracle_block_hist(frames[i], dim, fx.subdivided_colors())
+        assert np.array_equal(modes[i].cpu().numpy().view(np.uint32).reshape(bh, bw), rmode), i

@@ -20,8 +20,26 @@ WORKER = textwrap.dedent("""
     delay = 0.05 * (rank + 1)
     dt = bench.timed_region(lambda: time.sleep(delay), 3, world, lambda: None)
     dtmax = bench.max_over_ranks(dt, world)
-    seeds = [bench.frame_seed(rank, f) for f in range(4)]
-    print(json.dumps({"rank": rank, "dt": dt, "dtmax": dtmax, "seeds": seeds}), flush=True)
+    seeds = [bench.frame_id(rank, f, 4) for f in range(4)]
+    # the verification of a row-sharded output: each rank checks its own row
+    # bands against the fixture's 8 band hashes; a bad rank fails every rank
+    import numpy as np, torch
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    w, h = 64, 16
+    full = pkg.synth_frame(w * h, 5)
+    fix = {"ct": [1, 2], "out_fnv": "%%016x" %% pkg.fnv1a64(full),
+           "band_fnv": ["%%016x" %% pkg.fnv1a64(full[b * 2 * w:(b + 1) * 2 * w]) for b in range(8)]}
+    r0, r1 = bench.row_range(h, rank, world)
+    mine = torch.from_numpy(full[r0 * w:r1 * w].view(np.int32).copy())
+    good = bench.check_frame(pkg, mine, [1, 2], fix, rows=(r0, r1), h=h, world=world, rank=rank)
+    bad_ct = bench.check_frame(pkg, mine, [1, 3], fix, rows=(r0, r1), h=h, world=world, rank=rank)
+    if rank == 1:
+        mine[7] ^= 1
+    tampered = bench.check_frame(pkg, mine, [1, 2], fix, rows=(r0, r1), h=h, world=world, rank=rank)
+    agree = bench.all_ranks_ok(tampered, world, "cpu")
+    print(json.dumps({"rank": rank, "dt": dt, "dtmax": dtmax, "seeds": seeds, "good": good,
+                      "bad_ct": bad_ct, "tampered": tampered, "agree": agree}), flush=True)
     import torch.distributed as dist
     dist.destroy_process_group()
 """)
@@ -58,6 +76,10 @@ def test_two_rank_harness(tmp_path):
     assert outs[0]["dtmax"] >= max(o["dt"] for o in outs) - 1e-9
     # disjoint frames per rank
     assert not set(outs[0]["seeds"]) & set(outs[1]["seeds"])
+    # row-band verification: each rank's own bands; one bad rank fails both
+    assert all(o["good"] is True and o["bad_ct"] is False for o in outs)
+    assert outs[0]["tampered"] is True and outs[1]["tampered"] is False
+    assert outs[0]["agree"] is False and outs[1]["agree"] is False
 
 
 def test_row_ranges_partition_the_frame():

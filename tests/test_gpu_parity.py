@@ -295,3 +295,41 @@ def test_map_dense_palettes(gpu, kind):
     ref = np.zeros_like(px)
     fx.oracle().dqo_map(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(ref), fx.vp(pal), ctypes.c_int(k))
     assert np.array_equal(out, ref)
+
+
+def test_cpp_linkage_entry_points(gpu):
+    """The C++-linkage symbols the reference's callers link against
+    (DivQuantHeader.h:52-96): map_colors_mps (ClusteringSegmentation.cpp:408,
+    :2434) and quant_varpart_fast (quant_util.cpp:60) called by their mangled
+    names, against the reference's outputs."""
+    L = gpu.lib()
+    mcm = getattr(L, "_Z14map_colors_mpsPKjjPjS1_i")
+    mcm.restype = None
+    mcm.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    px = fx.xorshift(1 << 16, seed=fx.SEED + 7)
+    for c in fx.load_json("map.json"):
+        pal = fx.make_palette(c["spec"])
+        out = np.zeros_like(px)
+        mcm(fx.vp(px), len(px), fx.vp(out), fx.vp(pal), len(pal))
+        assert "%016x" % fx.fnv(out) == c["out_fnv"], c["spec"]
+    qvf = getattr(L, "_Z18quant_varpart_fastjPKjPjjjS1_S1_iiii")
+    qvf.restype = None
+    qvf.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    cases = fx.load_json("cases.json")
+    for i, c in enumerate(cases[:40]):
+        spec = c["spec"]
+        px = fx.make_case(spec)
+        tmp = np.zeros_like(px)
+        k = ctypes.c_uint32(spec["k"])
+        ct = np.zeros(spec["k"], np.uint32)
+        qvf(len(px), fx.vp(px), fx.vp(tmp), 1, len(px), ctypes.cast(ctypes.pointer(k), ctypes.c_void_p),
+            fx.vp(ct), 8, 1, 10, 1)
+        # quant_varpart_fast's table is cluster-index order before the dedup of
+        # quant_util.cpp:93-118: its first-occurrence dedup is the fixture's
+        seen, dd = set(), []
+        for v in ct[:k.value]:
+            if int(v) not in seen:
+                seen.add(int(v))
+                dd.append(int(v))
+        assert dd == c["ct"], (i, spec)
