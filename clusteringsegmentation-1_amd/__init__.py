@@ -32,7 +32,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DQ_HIP_LIB") or os.path.join(PKG_DIR, "libdivquant_hip.so")
 
 STAT_KINDS = ["pass_init", "pass_split", "pass_kmeans", "pass_klast",
-              "epilogue", "partition", "map_cells", "map"]
+              "epilogue", "partition", "map_cells", "map", "plan"]
 
 _lib = None
 
@@ -81,6 +81,8 @@ def lib():
         "dq_hip_last_points_swept": ([c.c_int], c.c_uint64),
         "dq_hip_last_points_full": ([c.c_int], c.c_uint64),
         "dq_hip_set_fixed_point": ([c.c_int, c.c_int], None),
+        "dq_hip_set_planned_rounds": ([c.c_int, c.c_int], None),
+        "dq_hip_last_planned_rounds": ([c.c_int], c.c_int),
         "dq_hip_set_timing": ([c.c_int, c.c_int], None),
         "dq_hip_reset_stats": ([c.c_int], None),
         "dq_hip_get_stat": ([c.c_int, c.c_int, c.POINTER(c.c_uint64), c.POINTER(c.c_double),
@@ -430,6 +432,15 @@ def last_points_full(device=0):
 def set_fixed_point(on, device=0):
     """Fixed-point finalisation of 2-means splits (identical outputs)."""
     lib().dq_hip_set_fixed_point(device, 1 if on else 0)
+
+
+def set_planned_rounds(on, device=0):
+    """Device-planned (speculative) rounds (identical outputs)."""
+    lib().dq_hip_set_planned_rounds(device, 1 if on else 0)
+
+
+def last_planned_rounds(device=0):
+    return lib().dq_hip_last_planned_rounds(device)
 
 
 def set_lanes(lanes):

@@ -204,6 +204,7 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
       Engine& e = engine_for(device, l);
       if (l > 0) {   // lanes inherit lane 0's switches
         e.set_fixed_point(e0.fixed_point());
+        e.set_plan(e0.plan());
         e.set_timing(e0.timing());
       }
       auto work = [&e, &jobs, f0, f1, max_iters, ready, device]() {
@@ -436,6 +437,10 @@ int dq_hip_last_rounds(int device) { return engine_for(device).last_rounds; }
 uint64_t dq_hip_last_points_swept(int device) { return engine_for(device).last_points_swept; }
 uint64_t dq_hip_last_points_full(int device) { return engine_for(device).last_points_full; }
 void dq_hip_set_fixed_point(int device, int on) { engine_for(device).set_fixed_point(on != 0); }
+void dq_hip_set_planned_rounds(int device, int on) {
+  for (int l = 0; l < dq::kMaxLanes; ++l) engine_for(device, l).set_plan(on != 0);
+}
+int dq_hip_last_planned_rounds(int device) { return engine_for(device).last_planned; }
 
 void dq_hip_set_timing(int device, int on) { engine_for(device).set_timing(on != 0); }
 
@@ -455,7 +460,7 @@ int dq_hip_get_stat(int device, int kind, uint64_t* launches, double* ms, double
 
 const char* dq_hip_stat_name(int kind) {
   static const char* names[] = {"pass_init", "pass_split", "pass_kmeans", "pass_klast",
-                                "epilogue", "partition", "map_cells", "map"};
+                                "epilogue", "partition", "map_cells", "map", "plan"};
   if (kind < 0 || kind >= dq::ST_COUNT) return "";
   return names[kind];
 }

@@ -12,6 +12,7 @@
 #include <map>
 #include <atomic>
 #include <chrono>
+#include <deque>
 #include <unordered_set>
 
 namespace dq {
@@ -57,8 +58,7 @@ Engine::Engine(int device) : device_(device) {
   if (const char* v = getenv("DQ_HIP_LDS_MAP")) use_lds_map_ = v[0] != '0';
   const char* la = getenv("DQ_HIP_LOOKAHEAD");
   if (la && la[0]) lookahead_ = std::max(0, std::min(8, atoi(la)));
-  const char* sp = std::getenv("DQ_HIP_SPEC_IT0");
-  if (sp && sp[0]) spec_it0_env_ = atoi(sp) != 0 ? 1 : 0;
+  if (const char* v = getenv("DQ_HIP_PLAN")) plan_ = v[0] != '0';
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
 }
@@ -198,33 +198,56 @@ static void grow_coherent(T** h, T** d, size_t* cap, size_t want) {
   *cap = c;
 }
 
-void Engine::ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t staging_bytes,
+// Capacities of one run, set at its start (nothing of this engine is in
+// flight then: the previous run ended with a stream synchronisation).
+// Per slot (round parity): rec_cap results, status words for max_iters
+// 2-means launches + the split epilogue, a plan list; tile partials for
+// tiles_cap tiles (every round's tiles and part tiles fit: a tile holds at
+// least kSweep points or is its record's last).
+void Engine::ensure_round(size_t rec_cap, size_t tiles_cap, size_t, size_t staging_bytes,
                           int max_iters, hipStream_t stream) {
-  // Lookahead launches of the previous round may still be queued (they may
-  // still read the part buffers and write a status word): drain the stream
-  // before any of these buffers moves.
-  const bool grow = staging_bytes > cap_stage_tab_ || nnodes > cap_res_ ||
-                    (size_t)max_iters > cap_stat_ || ntiles > cap_parts_ ||
-                    2 * nptiles > cap_sparts_ || !h_stage_ || !h_res_ || !h_stat_ || !d_parts_ ||
-                    !d_sparts_;
-  if (!grow) return;
   DQ_HIP(hipStreamSynchronize(stream));
   if (staging_bytes > cap_stage_tab_ || !h_stage_) {
     if (h_stage_) DQ_HIP(hipHostFree(h_stage_));
     const size_t c = std::max<size_t>(staging_bytes, (size_t)1 << 20);
-    DQ_HIP(hipHostMalloc((void**)&h_stage_, c, hipHostMallocDefault));
+    DQ_HIP(hipHostMalloc((void**)&h_stage_, c, hipHostMallocCoherent | hipHostMallocMapped));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_stage_view_, h_stage_, 0));
     cap_stage_tab_ = c;
   }
-  grow_coherent(&h_res_, &d_res_, &cap_res_, nnodes);
-  grow_coherent(&h_stat_, &d_stat_, &cap_stat_, (size_t)max_iters);
-  grow_device(&d_parts_, &cap_parts_, ntiles);
-  grow_device(&d_sparts_, &cap_sparts_, std::max<size_t>(2 * nptiles, 2));
+  if (!stage_ev_) DQ_HIP(hipEventCreateWithFlags(&stage_ev_, hipEventDisableTiming));
+  if (rec_cap > cap_res_ || !h_res_) {
+    if (h_res_) DQ_HIP(hipHostFree(h_res_));
+    if (d_dres_) DQ_HIP(hipFree(d_dres_));
+    if (h_plist_) DQ_HIP(hipHostFree(h_plist_));
+    const size_t c = std::max<size_t>(rec_cap, 256);
+    DQ_HIP(hipHostMalloc((void**)&h_res_, 2 * c * sizeof(NodeResult), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(h_res_, 0, 2 * c * sizeof(NodeResult));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_res_, h_res_, 0));
+    DQ_HIP(hipMalloc((void**)&d_dres_, 2 * c * sizeof(NodeResult)));
+    DQ_HIP(hipHostMalloc((void**)&h_plist_, 2 * c * sizeof(int32_t), hipHostMallocCoherent | hipHostMallocMapped));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_plist_, h_plist_, 0));
+    cap_res_ = c;
+    cap_plist_ = c;
+  }
+  if ((size_t)max_iters + 1 > cap_stat_ || !h_stat_) {
+    if (h_stat_) DQ_HIP(hipHostFree(h_stat_));
+    cap_stat_ = std::max<size_t>((size_t)max_iters + 1, 32);
+    DQ_HIP(hipHostMalloc((void**)&h_stat_, 2 * cap_stat_ * sizeof(uint64_t), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(h_stat_, 0, 2 * cap_stat_ * sizeof(uint64_t));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_stat_, h_stat_, 0));
+  }
+  if (!h_counts_) {
+    DQ_HIP(hipHostMalloc((void**)&h_counts_, 2 * 4 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(h_counts_, 0, 2 * 4 * sizeof(uint32_t));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_counts_h_, h_counts_, 0));
+  }
+  grow_device(&d_parts_, &cap_parts_, tiles_cap);
+  grow_device(&d_sparts_, &cap_sparts_, std::max<size_t>(2 * tiles_cap, 2));
 }
 
-// Wait for the status word of 2-means iteration `it` of round `seq`; returns
-// the number of nodes still active after it.  Bounded: once the stream has
-// drained the word must be there.
-uint32_t Engine::wait_status(int it, uint64_t seq, hipStream_t stream) {
+// Wait for a status word of round `seq`; returns the number of records still
+// active.  Bounded: once the stream has drained the word must be there.
+uint32_t Engine::wait_status(const uint64_t* slot, uint64_t seq, hipStream_t stream) {
   const double t0 = trace_ ? host_us() : 0.0;
   struct Acc {
     Engine* e; double t0;
@@ -232,7 +255,7 @@ uint32_t Engine::wait_status(int it, uint64_t seq, hipStream_t stream) {
   } acc{this, t0};
   const uint32_t want = (uint32_t)seq;
   auto ready = [&](uint32_t* act) {
-    const uint64_t v = __atomic_load_n(h_stat_ + it, __ATOMIC_ACQUIRE);
+    const uint64_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
     if (!(v & 1) || (uint32_t)(v >> 32) != want) return false;
     *act = (uint32_t)((v >> 1) & 0x7FFFFFFFu);
     return true;
@@ -245,7 +268,7 @@ uint32_t Engine::wait_status(int it, uint64_t seq, hipStream_t stream) {
       const hipError_t e = hipStreamQuery(stream);
       if (e == hipSuccess) {
         if (ready(&act)) return act;
-        die("status word", __FILE__, __LINE__, "stream drained without the 2-means status");
+        die("status word", __FILE__, __LINE__, "stream drained without the round's status");
       }
       if (e != hipErrorNotReady) die("hipStreamQuery", __FILE__, __LINE__, hipGetErrorString(e));
     }
@@ -257,8 +280,25 @@ const uint32_t* Engine::buf_ptr(int buf, const FrameState& f, int shard) const {
   return (buf == BUF_P0 ? d_p0_ : d_p1_) + f.base[shard];
 }
 
+// Tile length of a round of `total` points: whole 4096-point sweeps, about
+// tiles_target_ tiles, at most tile_max_ points.  A record gets at least
+// node_tiles_ tiles (a node still active late in a round is then swept by
+// several workgroups, not one).  plan_kernel restates both (plan_tile_len).
+uint64_t Engine::round_tile_len(uint64_t total) const {
+  uint64_t tl = (total + tiles_target_ - 1) / tiles_target_;
+  tl = ((tl + kSweep - 1) / kSweep) * kSweep;
+  return std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, tile_max_));
+}
+
+uint64_t Engine::tile_len_of(uint64_t len, uint64_t tl) const {
+  uint64_t t = (len + node_tiles_ - 1) / node_tiles_;
+  t = ((t + kSweep - 1) / kSweep) * kSweep;
+  return std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, t));
+}
+
 // ---------------------------------------------------------------------------
-// One round: split every node in `active` (one launch per pass for all).
+// Host-built round: split every node in `active` (one launch per pass for
+// all), launched up to its split epilogue; finish_round waits for it.
 //
 // Every logical node has one RECORD per shard (record r = node * S + shard):
 // the passes run over each record's own (local) points; the FP64 update
@@ -272,12 +312,17 @@ const uint32_t* Engine::buf_ptr(int buf, const FrameState& f, int shard) const {
 // nodes whose sibling already forced the partition) has its own split pass.
 // Partitions are lazy: a node is partitioned only when one of its children is
 // split, so the leaves of the last round never are.
-void Engine::run_round(const std::vector<int>& active_in, bool root_round, int max_iters,
-                       hipStream_t stream) {
+int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_round, int max_iters,
+                               hipStream_t stream) {
   const double tb0 = trace_ ? host_us() : 0.0;
   const int S = nshard_;
   const bool sharded = S > 1 || comm_ != nullptr;
-  std::vector<int> order, parents;
+  rounds_.emplace_back();
+  const int ri = (int)rounds_.size() - 1;
+  Round& R = rounds_[ri];
+  R.root = root_round;
+  std::vector<int>& order = R.order;
+  std::vector<int>& parents = R.parents;
   // node id -> logical slot in the round / position in `parents` (-1: none)
   slot_of_.assign(nodes_.size(), -1);
   parent_pos_.assign(nodes_.size(), -1);
@@ -295,6 +340,10 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   }
   const int nl = (int)order.size();   // logical nodes
   const int nr = nl * S;              // records
+  R.n_own = n_own;
+  R.nl = nl;
+  R.nr = nr;
+  DQ_CHECK((size_t)nr <= cap_res_, "round larger than the run's record capacity");
 
   uint64_t total = 0, own_total = 0, parent_total = 0;   // local points
   for (int a = 0; a < nl; ++a)
@@ -304,24 +353,12 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     }
   for (int p : parents)
     for (int sh = 0; sh < S; ++sh) parent_total += seg(p, sh).len;
-  // Tile length: whole 4096-point sweeps, about tiles_target_ tiles for big
-  // rounds, at most tile_max_ points (a node still active late in a round is
-  // swept by ceil(len / tl) workgroups only).
-  uint64_t tl = (total + tiles_target_ - 1) / tiles_target_;
-  tl = ((tl + kSweep - 1) / kSweep) * kSweep;
-  tl = std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, tile_max_));
-  // per record: at least node_tiles_ tiles (a node still active late in a
-  // round is then swept by several workgroups, not one)
-  auto tile_len = [&](uint64_t len) -> uint64_t {
-    uint64_t t = (len + node_tiles_ - 1) / node_tiles_;
-    t = ((t + kSweep - 1) / kSweep) * kSweep;
-    return std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, t));
-  };
+  const uint64_t tl = round_tile_len(total);
   size_t ntiles = 0, nt_own = 0;
   for (int a = 0; a < nl; ++a) {   // empty records get one empty tile (their epilogue still runs)
     for (int sh = 0; sh < S; ++sh) {
       const uint64_t len = seg(order[a], sh).len;
-      const uint64_t tln = tile_len(len);
+      const uint64_t tln = tile_len_of(len, tl);
       ntiles += std::max<size_t>(1, (len + tln - 1) / tln);
     }
     if (a == n_own - 1) nt_own = ntiles;
@@ -329,8 +366,16 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   size_t nptiles = 0;
   for (int p : parents)
     for (int sh = 0; sh < S; ++sh) nptiles += seg(p, sh).ntiles;
+  DQ_CHECK(ntiles <= cap_parts_ && 2 * nptiles <= cap_sparts_, "round larger than the run's tile capacity");
+  R.total = total;
+  R.own_total = own_total;
+  R.parent_total = parent_total;
+  R.tl = tl;
+  R.ntiles = R.tiles_cap = ntiles;
+  R.nptiles = R.ptiles_cap = nptiles;
+  R.nt_own = nt_own;
 
-  // the round's block: [DevNode nr | Tile ntiles | PartTile nptiles | LaunchCtr max_iters+1 | wparts]
+  // the round's block: [DevNode nr | Tile ntiles | PartTile nptiles | LaunchCtr max_iters+1 | wparts | rdone]
   auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
   const size_t o_tiles = al(nr * sizeof(DevNode));
   const size_t o_pt = o_tiles + al(ntiles * sizeof(Tile));
@@ -342,12 +387,24 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   // then the fused 2-means passes' arrival words, per (iteration, record)
   const size_t o_rd = o_wp + al(ntiles * kTileWaves * sizeof(uint32_t));
   const size_t bytes = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
-  ensure_round(nr, ntiles, nptiles, bytes, max_iters + 1, stream);
+  R.bytes = bytes;
   if (sharded && (size_t)nl * 8 > cap_tot_) {
     DQ_HIP(hipStreamSynchronize(stream));
     if (d_tot_) DQ_HIP(hipFree(d_tot_));
     cap_tot_ = std::max<size_t>((size_t)nl * 8, 4096);
     DQ_HIP(hipMalloc((void**)&d_tot_, cap_tot_ * sizeof(uint64_t)));
+  }
+  // the staging is rewritten: its previous upload must have run
+  if (stage_pending_) {
+    DQ_HIP(hipEventSynchronize(stage_ev_));
+    stage_pending_ = false;
+  }
+  if (bytes > cap_stage_tab_) {
+    DQ_HIP(hipHostFree(h_stage_));
+    const size_t c = std::max<size_t>(bytes, 2 * cap_stage_tab_);
+    DQ_HIP(hipHostMalloc((void**)&h_stage_, c, hipHostMallocCoherent | hipHostMallocMapped));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_stage_view_, h_stage_, 0));
+    cap_stage_tab_ = c;
   }
   char* dblk = arena_alloc(bytes);
   std::memset(h_stage_, 0, bytes);
@@ -356,6 +413,10 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   PartTile* hp = reinterpret_cast<PartTile*>(h_stage_ + o_pt);
   DevNode* dn = reinterpret_cast<DevNode*>(dblk);
   Tile* dt = reinterpret_cast<Tile*>(dblk + o_tiles);
+  R.dn = dn;
+  R.dt = dt;
+  R.tbeg.assign(nr, 0);
+  R.tend.assign(nr, 0);
 
   // first PartTile of each (parent, shard)
   std::vector<int> pt_first(parents.size() * S);
@@ -369,8 +430,10 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   }
   int t = 0;
   for (int a = 0; a < nl; ++a) {
-    const Node& n = nodes_[order[a]];
+    Node& n = nodes_[order[a]];
+    n.queued = true;
     slot_of_[order[a]] = a;
+    frames_[n.frame].splits_queued++;
     const FrameState& fs = frames_[n.frame];
     int32_t thr = 0, shift = 0;
     if (!root_round) {
@@ -383,8 +446,8 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       thr = split_threshold(cut);
       shift = 16 - 8 * axis;
     }
-    nodes_[order[a]].axis = (int16_t)((16 - shift) >> 3);
-    nodes_[order[a]].thr = (int16_t)thr;
+    n.axis = (int16_t)((16 - shift) >> 3);
+    n.thr = (int16_t)thr;
     for (int sh = 0; sh < S; ++sh) {
       DevNode& d = hn[a * S + sh];
       d.src = buf_ptr(n.buf, fs, sh);
@@ -407,7 +470,7 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
       d.prm.shift = shift;
       for (int c = 0; c < 3; ++c) { d.box_lo[c] = n.lo[c]; d.box_hi[c] = n.hi[c]; }
       d.tile_begin = t;
-      const uint64_t tln = tile_len(sg.len);
+      const uint64_t tln = tile_len_of(sg.len, tl);
       d.tile_len = (uint32_t)tln;
       for (uint64_t o = 0; o == 0 || o < sg.len; o += tln) {
         Tile& tt = ht[t++];
@@ -416,12 +479,15 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
         tt.end = sg.off + (uint32_t)std::min<uint64_t>(sg.len, o + tln);
       }
       d.tile_end = t;
+      R.tbeg[a * S + sh] = d.tile_begin;
+      R.tend[a * S + sh] = d.tile_end;
     }
   }
   {
     int q = 0;
     for (int p : parents) {
-      const Node& pn = nodes_[p];
+      Node& pn = nodes_[p];
+      pn.partitioned = true;
       int32_t thr[2], shift[2];
       const int ch[2] = {pn.child_old, pn.child_new};
       for (int c = 0; c < 2; ++c) {
@@ -448,23 +514,25 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     }
   }
   const double tb1 = trace_ ? host_us() : 0.0;
-  DQ_HIP(hipMemcpyAsync(dblk, h_stage_, bytes, hipMemcpyHostToDevice, stream));
-  const double tb2 = trace_ ? host_us() : 0.0;
-  if (trace_) tr_build_us_ += tb2 - tb0;
-  const double tw0 = tr_wait_us_;
+  // one upload kernel on the round's stream (no copy-engine hop)
+  launch_upload(dblk, d_stage_view_, bytes, stream);
+  DQ_HIP(hipEventRecord(stage_ev_, stream));
+  stage_pending_ = true;
+  if (trace_) tr_build_us_ += host_us() - tb0;
 
-  const uint64_t seq = ++seq_;
-  RoundArgs ra;
+  R.seq = ++seq_;
+  R.par = (int)(R.seq & 1);
+  RoundArgs& ra = R.ra;
   ra.tiles = dt;
   ra.nodes = dn;
   ra.parts = d_parts_;
   ra.wparts = reinterpret_cast<uint32_t*>(dblk + o_wp);
   ra.ptiles = reinterpret_cast<const PartTile*>(dblk + o_pt);
   ra.sparts = d_sparts_;
-  ra.hres = d_res_;
+  ra.hres = d_res_ + (size_t)R.par * cap_res_;
   ra.ctr = reinterpret_cast<LaunchCtr*>(dblk + o_ctr);
-  ra.hstat = d_stat_;
-  ra.seq = seq;
+  ra.hstat = d_stat_ + (size_t)R.par * cap_stat_;
+  ra.seq = R.seq;
   ra.fixed_point = fixed_point_ ? 1 : 0;
   ra.it = 0;
   ra.nn = nr;
@@ -472,18 +540,16 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
   ra.nshard = S;
   ra.pad = 0;
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
+  ra.dres = d_dres_ + (size_t)R.par * cap_res_;
+  ra.counts = nullptr;
   const double bytes_all = 4.0 * (double)total;
   const int nt = (int)ntiles;
-  // 2-means passes (iteration index) whose timing entry gets its swept bytes
-  // once the nodes' done_it are known
-  std::vector<std::pair<size_t, int>> km_events;
-  auto pass = [&](int kind, int st, int it, int tiles, double pbytes) {
-    ra.it = it < 0 ? 0 : it;
+  auto pass = [&](int kind, int st, int tiles, double pbytes) {
+    ra.it = 0;
     if (tiles > 0) {
       timed_begin(stream);
       launch_pass(kind, ra, tiles, stream);
       timed_end(st, pbytes, stream);
-      if (timing_ && it >= 0) km_events.push_back({pending_.size() - 1, it});
     }
   };
   auto epilogue = [&](int kind, int it) {
@@ -496,84 +562,300 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     launch_epilogue(kind, ra, nr, sharded, stream);
     timed_end(ST_EPILOGUE, 0.0, stream);
   };
-  // 2-means iteration `it`: pass + epilogue, one launch when unsharded
-  auto kmeans_iter = [&](int it) {
-    const bool last = it == max_iters - 1;
-    const int kind = last ? PASS_KLAST : PASS_KMEANS;
-    const int st = last ? ST_KLAST : ST_KMEANS;
-    if (sharded) {
-      pass(kind, st, it, nt, bytes_all);
-      epilogue(kind, it);
-      return;
-    }
-    ra.it = it;
-    timed_begin(stream);
-    launch_kpass(kind, ra, nt, stream);
-    timed_end(st, bytes_all, stream);
-    if (timing_) km_events.push_back({pending_.size() - 1, it});
-  };
   if (root_round) {
-    pass(PASS_INIT, ST_INIT, -1, nt, bytes_all);
+    pass(PASS_INIT, ST_INIT, nt, bytes_all);
     epilogue(PASS_INIT, -1);
   }
-  pass(PASS_SPLIT, ST_SPLIT, -1, (int)nt_own, 4.0 * (double)own_total);
+  pass(PASS_SPLIT, ST_SPLIT, (int)nt_own, 4.0 * (double)own_total);
   if (nptiles > 0) {
     timed_begin(stream);
     launch_partsplit(ra, (int)nptiles, stream);
     timed_end(ST_PARTITION, 8.0 * (double)parent_total, stream);
   }
   epilogue(PASS_SPLIT, max_iters);
-  // Splits the epilogue proved final (cut_is_fixed_point) need no 2-means
-  // pass: when that is all of them, the round ends here (latency mode: after
-  // the first iteration, queued meanwhile -- a no-op for proven nodes).
+  R.t_enq = tb1;
+  return ri;
+}
+
+// Which records of round ri the next round may split before ri's results
+// exist (speculation): every record of a frame whose splits queued so far
+// stay below k - 1 (the greedy replay may need more); whole unsharded
+// rounds only.  Returns false when nothing is planned.
+bool Engine::plan_list(int ri, std::vector<int32_t>* plist) {
+  const Round& R = rounds_[ri];
+  plist->clear();
+  if (!plan_ || !fixed_point_ || nshard_ != 1 || comm_ != nullptr) return false;
+  // frames of the round: speculate when the frame may need more splits
+  for (int a = 0; a < R.nl; ++a) {
+    const FrameState& f = frames_[nodes_[R.order[a]].frame];
+    if (f.splits_queued < f.job->k - 1) plist->push_back(a);
+  }
+  if (plist->empty() || 2 * plist->size() > cap_res_ || plist->size() > (size_t)kPlanMaxParents) {
+    plist->clear();
+    return false;
+  }
+  return true;
+}
+
+// Planned round: the children of `plist`'s records of round `prev`, tables
+// built on the device by plan_kernel, enqueued now -- before `prev`'s
+// results exist.  Grids are upper bounds (the kernels read the plan's
+// counts); if a listed record is not final after its split epilogue the plan
+// aborts the round (the host plans it again once `prev` has converged).
+int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, int max_iters,
+                                  hipStream_t stream) {
+  const double tb0 = trace_ ? host_us() : 0.0;
+  rounds_.emplace_back();
+  const int ri = (int)rounds_.size() - 1;
+  Round& R = rounds_[ri];
+  const Round& P = rounds_[prev];
+  R.planned = true;
+  R.prev = prev;
+  R.plist = plist;
+  const int np = (int)plist.size();
+  R.nl = R.nr = 2 * np;
+  R.n_own = 0;
+  uint64_t total = 0;
+  for (int32_t a : plist) {
+    const int id = P.order[a];
+    total += seg(id, 0).len;
+    Node& pn = nodes_[id];
+    pn.partitioned = true;
+    frames_[pn.frame].splits_queued += 2;
+  }
+  for (int32_t a : plist) R.parents.push_back(P.order[a]);
+  R.total = R.parent_total = total;
+  R.own_total = 0;
+  R.tl = round_tile_len(total);
+  R.tiles_cap = std::min<size_t>(total / kSweep + 2 * (size_t)np + 1,
+                                 total / R.tl + (size_t)2 * np * node_tiles_ + 1);
+  R.ptiles_cap = P.tiles_cap;
+  DQ_CHECK(R.tiles_cap <= cap_parts_ && 2 * R.ptiles_cap <= cap_sparts_, "planned round above the tile capacity");
+  auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
+  const size_t nr = (size_t)R.nr;
+  const size_t o_tiles = al(nr * sizeof(DevNode));
+  const size_t o_pt = o_tiles + al(R.tiles_cap * sizeof(Tile));
+  const size_t o_cnt = o_pt + al(R.ptiles_cap * sizeof(PartTile));
+  const size_t o_ctr = o_cnt + 64;
+  const size_t o_wp = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
+  const size_t o_rd = o_wp + al(R.tiles_cap * kTileWaves * sizeof(uint32_t));
+  const size_t bytes = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
+  R.bytes = bytes;
+  char* dblk = arena_alloc(bytes);
+  R.dn = reinterpret_cast<DevNode*>(dblk);
+  R.dt = reinterpret_cast<Tile*>(dblk + o_tiles);
+  R.dcounts = reinterpret_cast<uint32_t*>(dblk + o_cnt);
+  R.seq = ++seq_;
+  R.par = (int)(R.seq & 1);
+  // the plan list: identity unless some frames do not speculate
+  bool ident = true;
+  for (int i = 0; i < np; ++i) ident = ident && plist[i] == i && np == P.nl;
+  int32_t* hpl = h_plist_ + (size_t)R.par * cap_plist_;
+  if (!ident) std::memcpy(hpl, plist.data(), (size_t)np * sizeof(int32_t));
+
+  PlanArgs pa;
+  pa.pn = P.dn;
+  pa.pres = d_dres_ + (size_t)P.par * cap_res_;
+  pa.ptiles = P.dt;
+  pa.plist = ident ? nullptr : d_plist_ + (size_t)R.par * cap_plist_;
+  pa.np = np;
+  pa.node_tiles = node_tiles_;
+  pa.tl = (uint32_t)R.tl;
+  pa.tiles_cap = (uint32_t)R.tiles_cap;
+  pa.ptiles_cap = (uint32_t)R.ptiles_cap;
+  pa.cn = R.dn;
+  pa.ct = R.dt;
+  pa.cpt = reinterpret_cast<PartTile*>(dblk + o_pt);
+  pa.zero = reinterpret_cast<uint32_t*>(dblk + o_ctr);
+  pa.nzero = (uint32_t)((bytes - o_ctr) / 4);
+  pa.counts = R.dcounts;
+  pa.hcounts = d_counts_h_ + 4 * R.par;
+  pa.p0 = d_p0_;
+  pa.p1 = d_p1_;
+  pa.cap_px = cap_px_;
+  RoundArgs& ra = R.ra;
+  ra.tiles = R.dt;
+  ra.nodes = R.dn;
+  ra.parts = d_parts_;
+  ra.wparts = reinterpret_cast<uint32_t*>(dblk + o_wp);
+  ra.ptiles = pa.cpt;
+  ra.sparts = d_sparts_;
+  ra.hres = d_res_ + (size_t)R.par * cap_res_;
+  ra.ctr = reinterpret_cast<LaunchCtr*>(dblk + o_ctr);
+  ra.hstat = d_stat_ + (size_t)R.par * cap_stat_;
+  ra.seq = R.seq;
+  ra.fixed_point = fixed_point_ ? 1 : 0;
+  ra.it = max_iters;
+  ra.nn = R.nr;
+  ra.tot = d_tot_;
+  ra.nshard = 1;
+  ra.pad = 0;
+  ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
+  ra.dres = d_dres_ + (size_t)R.par * cap_res_;
+  ra.counts = R.dcounts;
+  timed_begin(stream);
+  launch_plan(pa, stream);
+  timed_end(ST_PLAN, 0.0, stream);
+  timed_begin(stream);
+  launch_partsplit(ra, (int)R.ptiles_cap, stream);
+  timed_end(ST_PARTITION, 8.0 * (double)total, stream);
+  timed_begin(stream);
+  launch_epilogue(PASS_SPLIT, ra, R.nr, false, stream);
+  timed_end(ST_EPILOGUE, 0.0, stream);
+  if (trace_) tr_build_us_ += host_us() - tb0;
+  R.t_enq = trace_ ? host_us() : 0.0;
+  return ri;
+}
+
+// Once the round a planned round is planned from is finished (its children
+// exist): the planned round's nodes, records and tiles on the host, as the
+// plan built them on the device (plan_kernel's layout rules).
+void Engine::assign_planned(int ri) {
+  Round& R = rounds_[ri];
+  const Round& P = rounds_[R.prev];
+  R.order.clear();
+  for (int32_t a : R.plist) {
+    const Node& pn = nodes_[P.order[a]];
+    R.order.push_back(pn.child_old);
+    R.order.push_back(pn.child_new);
+  }
+  R.tbeg.assign(R.nr, 0);
+  R.tend.assign(R.nr, 0);
+  int32_t t = 0;
+  size_t npt = 0;
+  for (int a = 0; a < R.nl; ++a) {
+    Node& n = nodes_[R.order[a]];
+    n.queued = true;
+    const uint64_t len = seg(R.order[a], 0).len;
+    const uint64_t tln = tile_len_of(len, R.tl);
+    R.tbeg[a] = t;
+    t += (int32_t)std::max<uint64_t>(1, (len + tln - 1) / tln);
+    R.tend[a] = t;
+    // the cut the plan chose (:388-403), for the children's boxes
+    double maxv = n.var[0], cut = n.mean[0];
+    int axis = 0;
+    if (maxv < n.var[1]) { maxv = n.var[1]; axis = 1; cut = n.mean[1]; }
+    if (maxv < n.var[2]) { axis = 2; cut = n.mean[2]; }
+    n.axis = (int16_t)axis;
+    n.thr = (int16_t)split_threshold(cut);
+  }
+  for (int p : R.parents) npt += seg(p, 0).ntiles;
+  R.ntiles = (size_t)t;
+  R.nptiles = npt;
+}
+
+// 2-means iteration `it` of a round: pass + epilogue, one launch when unsharded.
+void Engine::kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream) {
+  const bool sharded = nshard_ > 1 || comm_ != nullptr;
+  const bool last = it == max_iters - 1;
+  const int kind = last ? PASS_KLAST : PASS_KMEANS;
+  const int st = last ? ST_KLAST : ST_KMEANS;
+  RoundArgs& ra = R.ra;
+  ra.it = it;
+  const double bytes_all = 4.0 * (double)R.total;
+  if (sharded) {
+    timed_begin(stream);
+    launch_pass(kind, ra, (int)R.ntiles, stream);
+    timed_end(st, bytes_all, stream);
+    if (timing_) R.km_events.push_back({pending_.size() - 1, it});
+    timed_begin(stream);
+    launch_nodesum(kind, ra, R.nl, stream);
+    if (comm_) allreduce_totals(R.nl, stream);
+    launch_epilogue(kind, ra, R.nr, true, stream);
+    timed_end(ST_EPILOGUE, 0.0, stream);
+    return;
+  }
+  timed_begin(stream);
+  launch_kpass(kind, ra, (int)R.ntiles, stream);
+  timed_end(st, bytes_all, stream);
+  if (timing_) R.km_events.push_back({pending_.size() - 1, it});
+}
+
+// Wait for a round's split epilogue, run its 2-means iterations if any record
+// is still active (host-polled, `lookahead_` launched past the one awaited),
+// then take its results: children nodes, segments, the parents' tiles.
+void Engine::finish_round(int ri, int max_iters, hipStream_t stream) {
+  Round& R = rounds_[ri];
+  const int S = nshard_;
+  const double tw0 = tr_wait_us_;
+  const double tf0 = trace_ ? host_us() : 0.0;
+  const uint64_t* stat = h_stat_ + (size_t)R.par * cap_stat_;
+  const NodeResult* res = h_res_ + (size_t)R.par * cap_res_;
   int launched = 0, known = 0;
   bool all_proven = false;
-  if (fixed_point_) {
-    if (spec_it0_) {
-      kmeans_iter(0);
-      launched = 1;
-    }
-    all_proven = wait_status(max_iters, seq, stream) == 0;
+  if (fixed_point_) all_proven = wait_status(stat + max_iters, R.seq, stream) == 0;
+  if (R.planned) {   // the plan's counts equal the host's mirror of its layout
+    const uint32_t* hc = h_counts_ + 4 * R.par;
+    const uint32_t ab = __atomic_load_n(hc + 2, __ATOMIC_ACQUIRE);
+    DQ_CHECK(ab == 0, "a finished planned round was aborted or overflowed");
+    DQ_CHECK(__atomic_load_n(hc + 0, __ATOMIC_ACQUIRE) == (uint32_t)R.ntiles &&
+                 __atomic_load_n(hc + 1, __ATOMIC_ACQUIRE) == (uint32_t)R.nptiles,
+             "plan_kernel's tile counts differ from the host's mirror");
   }
-  // 2-means iterations, `lookahead_` launched past the one whose status the
-  // host waits for; stop as soon as every node is final.
+  R.kmeans = !all_proven;
   while (!all_proven) {
     while (launched < max_iters && launched <= known + lookahead_) {
-      kmeans_iter(launched);
+      kmeans_iter(R, launched, max_iters, stream);
       ++launched;
     }
-    const uint32_t act = wait_status(known, seq, stream);
+    const uint32_t act = wait_status(stat + known, R.seq, stream);
     ++known;
     if (act == 0) break;
     DQ_CHECK(known < max_iters, "nodes still active after the last 2-means iteration");
   }
-
   const double tp0 = trace_ ? host_us() : 0.0;
+  const int nl = R.nl;
+  // Every record's result carries the round's tag, stored after its other
+  // words: read a record only once its tag is there (bounded by the stream
+  // draining).  Then check the device's view of the round against the
+  // host's: the record's points (the layout mirror) and, below the root, the
+  // node's own mean / variance the round ran with.
+  for (int r = 0; r < R.nr; ++r) {
+    const uint32_t* tag = &res[r].tag;
+    for (uint64_t spin = 0; __atomic_load_n(tag, __ATOMIC_ACQUIRE) != (uint32_t)R.seq; ++spin) {
+      __builtin_ia32_pause();
+      if ((spin & 0xFFFF) == 0xFFFF && hipStreamQuery(stream) == hipSuccess &&
+          __atomic_load_n(tag, __ATOMIC_ACQUIRE) != (uint32_t)R.seq)
+        die("node result", __FILE__, __LINE__, "a record's result never arrived");
+    }
+    const int a = r / S;
+    const Node& nd = nodes_[R.order[a]];
+    bool ok = res[r].len_local == seg(R.order[a], r % S).len;
+    if (!R.root)
+      for (int c = 0; c < 3; ++c)
+        ok = ok && std::memcmp(&res[r].tm[c], &nd.mean[c], 8) == 0 && std::memcmp(&res[r].tv[c], &nd.var[c], 8) == 0;
+    if (!ok) {
+      char msg[200];
+      std::snprintf(msg, sizeof msg, "round seq %llu (%s) record %d: device and host views differ (len %u vs %u)",
+                    (unsigned long long)R.seq, R.planned ? "planned" : "host", r, res[r].len_local,
+                    seg(R.order[a], r % S).len);
+      die("round check", __FILE__, __LINE__, msg);
+    }
+  }
   // points actually swept: iteration `it` reads a node iff it is not final
   // before it (done_it <= 0: final at the last iteration, or it < done_it)
   auto swept_in = [&](int it) {
     uint64_t px = 0;
     for (int a = 0; a < nl; ++a) {
-      const int di = h_res_[a * S].done_it;
-      if (!h_res_[a * S].proven && (di <= 0 || it < di))
-        for (int sh = 0; sh < S; ++sh) px += seg(order[a], sh).len;
+      const int di = res[a * S].done_it;
+      if (!res[a * S].proven && (di <= 0 || it < di))
+        for (int sh = 0; sh < S; ++sh) px += seg(R.order[a], sh).len;
     }
     return px;
   };
-  last_points_full += total * (uint64_t)((root_round ? 2 : 1) + max_iters);
-  last_points_swept += total * (uint64_t)(root_round ? 2 : 1);
+  last_points_full += R.total * (uint64_t)((R.root ? 2 : 1) + max_iters);
+  last_points_swept += R.total * (uint64_t)(R.root ? 2 : 1);
   for (int it = 0; it < max_iters; ++it) last_points_swept += swept_in(it);
   if (timing_) {
     DQ_HIP(hipStreamSynchronize(stream));
-    for (auto& e : km_events) pending_[e.first].bytes = 4.0 * (double)swept_in(e.second);
+    for (auto& e : R.km_events) pending_[e.first].bytes = 4.0 * (double)swept_in(e.second);
     collect_timing();
   }
 
-  for (int p : parents) nodes_[p].partitioned = true;
   for (int a = 0; a < nl; ++a) {
-    const int id = order[a];
-    const NodeResult& r = h_res_[a * S];   // global results: every record agrees
-    if (root_round) {
+    const int id = R.order[a];
+    const NodeResult& r = res[a * S];   // global results: every record agrees
+    if (R.root) {
       for (int c = 0; c < 3; ++c) { nodes_[id].mean[c] = r.tm[c]; nodes_[id].var[c] = r.tv[c]; }
       // the cut the INIT epilogue chose on the device, same comparisons
       double maxv = r.tv[0], cut = r.tm[0];
@@ -615,12 +897,11 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     nodes_.push_back(cn);
     segs_.resize((size_t)(io + 2) * S);
     for (int sh = 0; sh < S; ++sh) {
-      const DevNode& d = hn[a * S + sh];
       Seg& ps = seg(id, sh);
-      ps.dnode = dn + a * S + sh;
-      ps.dtiles = dt + d.tile_begin;
-      ps.ntiles = d.tile_end - d.tile_begin;
-      const uint32_t n_new = h_res_[a * S + sh].n_new_local;
+      ps.dnode = R.dn + a * S + sh;
+      ps.dtiles = R.dt + R.tbeg[a * S + sh];
+      ps.ntiles = R.tend[a * S + sh] - R.tbeg[a * S + sh];
+      const uint32_t n_new = res[a * S + sh].n_new_local;
       const uint32_t n_old = ps.len - n_new;
       Seg& so = seg(io, sh);
       Seg& sn = seg(io + 1, sh);
@@ -633,14 +914,15 @@ void Engine::run_round(const std::vector<int>& active_in, bool root_round, int m
     pp.child_old = io;
     pp.child_new = io + 1;
     pp.expanded = true;
+    pp.queued = false;
   }
   if (trace_rounds_) {
     const double tp1 = host_us();
     std::fprintf(stderr,
-                 "divquant-hip round: nodes=%d records=%d tiles=%zu parttiles=%zu upload=%zuB "
-                 "fill=%.1fus memcpy=%.1fus launch+wait=%.1fus (wait %.1f) post=%.1fus\n",
-                 nl, nr, ntiles, nptiles, bytes, tb1 - tb0, tb2 - tb1, tp0 - tb2,
-                 tr_wait_us_ - tw0, tp1 - tp0);
+                 "divquant-hip round %s: nodes=%d records=%d tiles=%zu parttiles=%zu bytes=%zu "
+                 "enq->finish %.1fus (wait %.1f, 2-means its %d) post=%.1fus%s\n",
+                 R.planned ? "planned" : "host", nl, R.nr, R.ntiles, R.nptiles, R.bytes,
+                 tf0 - R.t_enq, tr_wait_us_ - tw0, launched, tp1 - tp0, R.kmeans ? " kmeans" : "");
   }
 }
 
@@ -683,10 +965,11 @@ void Engine::replay(FrameState& f) {
 // Next round's nodes of a frame: the node the replay waits for plus every
 // unexpanded leaf among the top r = (splits left) of the greedy order -- a
 // leaf outside the current top r can never be picked in the remaining splits.
+// Nodes already queued in an enqueued round are left out.
 void Engine::next_active(FrameState& f, std::vector<int>* active) {
   if (f.need < 0) return;
   const size_t r = (size_t)(f.job->k - f.new_index);
-  active->push_back(f.need);
+  if (!nodes_[f.need].queued) active->push_back(f.need);
   // the valid leaves of the greedy order, then its top r (keys are unique)
   top_.clear();
   for (const auto& e : f.heap)
@@ -697,7 +980,8 @@ void Engine::next_active(FrameState& f, std::vector<int>* active) {
     top_.resize(r);
   }
   for (const auto& e : top_)
-    if (!nodes_[e.second].expanded && e.second != f.need) active->push_back(e.second);
+    if (!nodes_[e.second].expanded && !nodes_[e.second].queued && e.second != f.need)
+      active->push_back(e.second);
 }
 
 // Final centres (:1029-1094): round, pack, drop empty clusters.
@@ -752,7 +1036,6 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   last_points_full = 0;
   nshard_ = jobs[0].nshard;
   DQ_CHECK(nshard_ >= 1 && nshard_ <= kMaxShard, "shards per frame must be in [1, 8]");
-  spec_it0_ = spec_it0_env_ >= 0 ? spec_it0_env_ == 1 : nframes == 1;
   const int S = nshard_;
   size_t total = 0, align_need = 0;
   for (int i = 0; i < nframes; ++i) {
@@ -830,11 +1113,49 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
 
   const double t_run0 = trace_ ? host_us() : 0.0;
   tr_wait_us_ = tr_build_us_ = tr_replay_us_ = 0.0;
-  bool root_round = true;
-  while (!active.empty()) {
-    run_round(active, root_round, max_iters, stream);
-    root_round = false;
+  last_planned = last_aborted = 0;
+  {   // this run's capacities (nothing in flight now)
+    size_t rec_cap = 64, px = 0;
+    for (int i = 0; i < nframes; ++i) {
+      rec_cap += 2 * (size_t)jobs[i].k * S;
+      px += jobs[i].n;
+    }
+    const size_t tiles_cap = px / kSweep + rec_cap * (size_t)node_tiles_ + 64;
+    ensure_round(rec_cap, tiles_cap, 0, 0, max_iters, stream);
+  }
+  rounds_.clear();
+  // Rounds in flight, oldest first.  While the oldest is the only one, the
+  // next is planned on the device before its results exist; the host then
+  // finishes the oldest (waits, 2-means iterations if needed, results),
+  // replays the greedy order, and enqueues a host-built round for whatever
+  // the replay needs that no enqueued round covers.
+  std::deque<int> q;
+  if (!active.empty()) q.push_back(enqueue_host_round(active, true, max_iters, stream));
+  std::vector<int32_t> plist;
+  while (!q.empty()) {
+    const int ri = q.front();
+    if (q.size() == 1 && plan_list(ri, &plist)) q.push_back(enqueue_planned_round(ri, plist, max_iters, stream));
+    finish_round(ri, max_iters, stream);
+    q.pop_front();
     last_rounds++;
+    if (rounds_[ri].planned) last_planned++;
+    if (!q.empty() && rounds_[q.front()].planned && rounds_[q.front()].prev == ri && rounds_[ri].kmeans) {
+      // The plan ran after ri's split epilogue: if a listed record was still
+      // active then, it aborted its round.  (ri's 2-means launches came
+      // after the plan in stream order, so its counts are visible now.)
+      const int pi = q.front();
+      const uint32_t ab = __atomic_load_n(h_counts_ + 4 * rounds_[pi].par + 2, __ATOMIC_ACQUIRE);
+      DQ_CHECK(ab != 2, "plan_kernel: tables above the round's capacity");
+      if (ab == 1) {
+        q.pop_front();
+        last_aborted++;
+        const std::vector<int32_t> pl = rounds_[pi].plist;
+        for (int32_t a : pl) frames_[nodes_[rounds_[ri].order[a]].frame].splits_queued -= 2;
+        q.push_front(enqueue_planned_round(ri, pl, max_iters, stream));
+      }
+    }
+    for (int p : q)
+      if (rounds_[p].planned && rounds_[p].prev == ri) assign_planned(p);
     active.clear();
     const double tr0 = trace_ ? host_us() : 0.0;
     for (auto& f : frames_) {
@@ -843,6 +1164,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
       next_active(f, &active);
     }
     if (trace_) tr_replay_us_ += host_us() - tr0;
+    if (!active.empty()) q.push_back(enqueue_host_round(active, false, max_iters, stream));
   }
   const double t_clu = trace_ ? host_us() : 0.0;
 

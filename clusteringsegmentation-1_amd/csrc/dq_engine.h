@@ -48,6 +48,7 @@ struct Node {
   int parent = -1;
   int32_t buf = 0;                   // 0: caller's input, 1: P0, 2: P1
   bool expanded = false;
+  bool queued = false;               // in a round enqueued but not yet finished
   bool partitioned = false;          // children's points written to child_buf(buf)
   double w = 0.0;                    // weight[]   (:290, :862-863)
   double mean[3] = {0, 0, 0};        // mean[]     (:309)
@@ -94,7 +95,7 @@ struct KernelStat {
   double bytes = 0.0;   // algorithmic bytes (4 B per point read, +4 B written)
 };
 enum StatKind { ST_INIT = 0, ST_SPLIT, ST_KMEANS, ST_KLAST, ST_EPILOGUE, ST_PARTITION,
-                ST_CELLS, ST_MAP, ST_COUNT };
+                ST_CELLS, ST_MAP, ST_PLAN, ST_COUNT };
 
 class Engine {
  public:
@@ -145,6 +146,8 @@ class Engine {
   std::vector<int64_t> last_sizes;    // K sizes
   std::vector<int64_t> last_trace;    // (K-1)*4: new_index old_index |C| |new|
   int last_rounds = 0;
+  int last_planned = 0;               // rounds planned on the device (of last_rounds)
+  int last_aborted = 0;               // planned rounds whose plan found a parent unfinished
   uint64_t last_points_swept = 0;     // sum over passes of points read (all frames)
   uint64_t last_points_full = 0;      // the same without fixed-point finalisation
 
@@ -162,6 +165,9 @@ class Engine {
   // Finalise a split when its 2-means reaches an exact fixed point (default
   // on; results are identical either way -- dq_kernels.hip, node_update).
   void set_fixed_point(bool on) { fixed_point_ = on; }
+  // Device-planned rounds (default on; DQ_HIP_PLAN=0 turns the default off).
+  void set_plan(bool on) { plan_ = on; }
+  bool plan() const { return plan_; }
   bool fixed_point() const { return fixed_point_; }
   void reset_stats();
   KernelStat stats[ST_COUNT];
@@ -182,16 +188,54 @@ class Engine {
     std::vector<HeapEnt> heap;        // max-heap of ((tse, -idx), node) (std::push_heap)
     int new_index = 1, old_index = 0;
     int need = -1;                    // node the replay waits for (-1: done)
+    int splits_queued = 0;            // nodes expanded or queued for expansion
     std::vector<int64_t> trace;
   };
+
+  // One enqueued split round.  Host-built rounds get their
+  // tables from the host (staging + upload kernel); planned rounds from
+  // plan_kernel, enqueued before the results of the round they are planned
+  // from exist (their records: the children of `plist`'s records of `prev`).
+  struct Round {
+    uint64_t seq = 0;
+    int par = 0;                      // status / result slot parity
+    bool root = false, planned = false;
+    int prev = -1;                    // planned: the round it is planned from
+    std::vector<int32_t> plist;       // planned: records of `prev` split in it
+    std::vector<int> order;           // node id per logical slot (planned: once prev is done)
+    std::vector<int> parents;         // nodes the round's partsplit partitions
+    int n_own = 0, nl = 0, nr = 0;
+    size_t ntiles = 0, nptiles = 0, nt_own = 0;
+    size_t tiles_cap = 0, ptiles_cap = 0;
+    uint64_t tl = 0;
+    uint64_t total = 0, own_total = 0, parent_total = 0;
+    std::vector<int32_t> tbeg, tend;  // per record: its tiles
+    size_t bytes = 0;
+    DevNode* dn = nullptr;
+    Tile* dt = nullptr;
+    uint32_t* dcounts = nullptr;      // planned: plan_kernel's counts (device)
+    RoundArgs ra{};
+    bool kmeans = false;              // its split epilogue left records active
+    std::vector<std::pair<size_t, int>> km_events;
+    double t_enq = 0;
+  };
+  std::vector<Round> rounds_;
 
   void ensure_pixels(size_t total);
   void ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t staging_bytes,
                     int max_iters, hipStream_t stream);
   char* arena_alloc(size_t bytes);
-  uint32_t wait_status(int it, uint64_t seq, hipStream_t stream);
-  void run_round(const std::vector<int>& active, bool root_round, int max_iters,
-                 hipStream_t stream);
+  uint32_t wait_status(const uint64_t* slot, uint64_t seq, hipStream_t stream);
+  int enqueue_host_round(const std::vector<int>& active, bool root_round, int max_iters,
+                         hipStream_t stream);
+  bool plan_list(int ri, std::vector<int32_t>* plist);
+  int enqueue_planned_round(int prev, const std::vector<int32_t>& plist, int max_iters,
+                            hipStream_t stream);
+  void assign_planned(int ri);
+  void finish_round(int ri, int max_iters, hipStream_t stream);
+  void kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream);
+  uint64_t tile_len_of(uint64_t len, uint64_t tl) const;
+  uint64_t round_tile_len(uint64_t total) const;
   void replay(FrameState& f);
   void next_active(FrameState& f, std::vector<int>* active);
   void finish_frame(FrameState& f, bool last);
@@ -231,21 +275,27 @@ class Engine {
   TilePartial* d_parts_ = nullptr;    // per tile of the round
   TilePartial* d_sparts_ = nullptr;   // per PartTile of the round
   size_t cap_parts_ = 0, cap_sparts_ = 0;
-  // host-coherent pinned memory the epilogues write (results, status words)
+  // host-coherent pinned memory the epilogues write (results, status words),
+  // two slots (round parity: a planned round runs while the host finishes
+  // the previous one); the results' device copy the plans read
   NodeResult* h_res_ = nullptr;
   NodeResult* d_res_ = nullptr;       // device view of h_res_
-  size_t cap_res_ = 0;
+  NodeResult* d_dres_ = nullptr;      // device memory
+  size_t cap_res_ = 0;                // records per slot
   uint64_t* h_stat_ = nullptr;
   uint64_t* d_stat_ = nullptr;
-  size_t cap_stat_ = 0;
+  size_t cap_stat_ = 0;               // words per slot
+  int32_t* h_plist_ = nullptr;        // per slot: a planned round's parent records
+  int32_t* d_plist_ = nullptr;
+  size_t cap_plist_ = 0;
+  uint32_t* h_counts_ = nullptr;      // per slot: plan_kernel's counts (host mirror)
+  uint32_t* d_counts_h_ = nullptr;
+  char* d_stage_view_ = nullptr;      // device view of h_stage_ (host-coherent)
+  hipEvent_t stage_ev_ = nullptr;     // the last upload of h_stage_
+  bool stage_pending_ = false;
+  bool plan_ = true;                  // device-planned rounds (DQ_HIP_PLAN=0: host only)
   uint64_t seq_ = 0;                  // round sequence number
   int lookahead_ = 1;                 // 2-means iterations queued past the one awaited
-  // Latency mode (one frame per call, nothing else to overlap the host's
-  // waits): queue the first 2-means iteration before knowing whether the
-  // split epilogue proved every node final (then it is a no-op) instead of
-  // waiting for that status.  DQ_HIP_SPEC_IT0=0/1 forces it off/on.
-  int spec_it0_env_ = -1;
-  bool spec_it0_ = false;
   int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TILES)
   int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_NODE_TILES)
   uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TILE_MAX)
@@ -274,7 +324,7 @@ class Engine {
   size_t cap_tot_ = 0;
   void* comm_ = nullptr;              // ncclComm_t across processes (row-tile sharding)
   int comm_ranks_ = 1, comm_rank_ = 0;
-  std::vector<int> slot_of_, parent_pos_;   // run_round scratch, indexed by node id
+  std::vector<int> slot_of_, parent_pos_;   // enqueue_host_round scratch, indexed by node id
   std::vector<FrameState> frames_;
   struct PendingEvent { hipEvent_t a, b; int kind; double bytes; };
   std::vector<PendingEvent> pending_;

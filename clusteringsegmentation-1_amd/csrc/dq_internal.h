@@ -98,6 +98,9 @@ struct alignas(16) NodeResult {
   int32_t done_it;          // see DevNode
   int32_t proven;           // 1: final at the split epilogue -- the halves are the cut's
   int32_t pad;
+  uint32_t len_local;       // the record's points (the host checks its mirror of the layout)
+  uint32_t tag;             // round sequence number, stored LAST (after the other words
+                            //   completed): the host reads a record only once it matches
 };
 
 // One workgroup's share of a pass.  Inside a tile, wave w of the workgroup

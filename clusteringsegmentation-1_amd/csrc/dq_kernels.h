@@ -46,7 +46,43 @@ struct RoundArgs {
   int32_t nshard;           // records per logical node (record r = node * nshard + shard)
   int32_t pad;
   uint32_t* rdone;          // per (2-means iteration, record): kpass workgroups finished
+  NodeResult* dres;         // device copy of the final results (read by the next round's plan)
+  const uint32_t* counts;   // planned rounds: [tiles, part tiles, aborted] written by
+                            //   plan_kernel (grids are upper bounds); nullptr: host-built
 };
+
+// A round planned on the device (plan_kernel): the children of every listed
+// record of the previous round are this round's nodes, record 2i = the old
+// half of parent plist[i], 2i+1 = its new half ("device-planned
+// rounds").  The host enqueues the round before the previous round's results
+// exist; the plan aborts the round (counts[2] = 1, every kernel of it exits)
+// when a listed parent is not final after its split epilogue.
+struct PlanArgs {
+  const DevNode* pn;        // previous round: records
+  const NodeResult* pres;   //                 results (device copy)
+  const Tile* ptiles;       //                 tiles (the part tiles point into them)
+  const int32_t* plist;     // parent records to split (host-coherent pinned memory)
+  int32_t np;
+  int32_t node_tiles;       // tiles per record at least (Engine::tile_len)
+  uint32_t tl;              // tile length of the round (Engine::tile_len)
+  uint32_t tiles_cap, ptiles_cap;
+  DevNode* cn;              // this round: 2 np records
+  Tile* ct;
+  PartTile* cpt;
+  uint32_t* zero;           // [LaunchCtr | wparts | rdone] words to clear
+  uint32_t nzero;
+  uint32_t* counts;         // device: tiles, part tiles, aborted (2: overflow)
+  uint32_t* hcounts;        // host-coherent mirror of counts
+  const uint32_t* p0;       // the two working buffers (a child's dst is the
+  const uint32_t* p1;       //   other one of its src)
+  uint64_t cap_px;          // words per working buffer
+};
+constexpr int kPlanMaxParents = 6144;   // parents per planned round (LDS scans)
+void launch_plan(const PlanArgs& a, hipStream_t stream);
+// Host-built round tables: copy `bytes` from host-coherent pinned staging
+// (device view) into the round's device block on the round's stream (no
+// copy-engine hop between the host and the round's first kernel).
+void launch_upload(void* dst, const void* src_dev_view, size_t bytes, hipStream_t stream);
 
 // One statistics pass over tiles [0, ntiles) of the round (one workgroup per tile).
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);

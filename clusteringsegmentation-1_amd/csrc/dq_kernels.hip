@@ -555,15 +555,33 @@ __device__ __forceinline__ void record_cursors(Tile* tiles, const uint32_t* wp, 
 }
 
 // Final results go straight to host-coherent memory: relaxed system-scope
-// 8-B stores, one per lane (no L2 write-back); the caller drains them
-// (s_waitcnt vmcnt(0)) before arriving.
-__device__ __forceinline__ void store_result(NodeResult* dst, const NodeResult& r, uint32_t lane) {
+// 8-B stores, one per lane (no L2 write-back); the device copy (ddst, may be
+// null) is what the next round's plan reads.  The last word (len_local,
+// tag = round seq) is stored only after the others completed (vmcnt(0)), so
+// a host that sees the tag sees the record; the caller drains the tag store
+// before arriving.
+__device__ __forceinline__ void store_result(NodeResult* dst, NodeResult* ddst, NodeResult& r,
+                                             uint32_t lane, uint32_t len_local, uint64_t seq) {
   constexpr int kWords = (int)(sizeof(NodeResult) / 8);
   static_assert(kWords <= 64, "one wave stores the result");
-  if (lane < (uint32_t)kWords) {
-    const uint64_t v = reinterpret_cast<const uint64_t*>(&r)[lane];
+  if (lane == 0) {
+    r.len_local = len_local;
+    r.tag = (uint32_t)seq;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint64_t v = lane < (uint32_t)kWords ? reinterpret_cast<const uint64_t*>(&r)[lane] : 0ull;
+  if (lane < (uint32_t)kWords - 1) {
     __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + lane, v, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+    if (ddst) reinterpret_cast<uint64_t*>(ddst)[lane] = v;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == (uint32_t)kWords - 1) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + lane, v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    if (ddst) reinterpret_cast<uint64_t*>(ddst)[lane] = v;
   }
 }
 
@@ -592,36 +610,51 @@ __device__ __forceinline__ void arrive(LaunchCtr* c, uint32_t rec, uint32_t nn, 
 }
 
 // ---------------------------------------------------------------------------
-// Epilogue: ONE WAVE per node record of the round (no workgroup barrier).
+// Epilogue: ONE WORKGROUP per node record of the round.
 //   * the node's sums: its own partials (FROM_TOT: the logical node's global
 //     totals from nodesum + allreduce; its own partials then only give the
-//     record's local new-half size);
-//   * lane 0 runs the FP64 update (node_update) -- every record of a
+//     record's local new-half size), summed by all kEpiBlock lanes (a record
+//     of an early round has ~1000 tile partials), then reduced in LDS;
+//   * wave 0, lane 0 runs the FP64 update (node_update) -- every record of a
 //     logical node runs it on the same totals, so all agree bit for bit;
 //   * a record whose split became final: the partition's per-(tile, wave)
 //     write cursors (a shuffle scan over the lanes' tile chunks), and the
-//     results written straight to host memory (NodeResult);
+//     results written straight to host memory (NodeResult) and to the
+//     device copy the next round's plan reads;
 //   * 2-means and split launches: every record arrives on the launch's
 //     (sharded) counter; the last to arrive publishes (round seq, records
 //     still active) to the host, which stops launching iterations once no
 //     node is active (after the split: nodes proven final by
 //     cut_is_fixed_point need no 2-means pass at all).
-constexpr int kEpiBlock = 64;
+constexpr int kEpiBlock = 256;
 template <int KIND, bool FROM_TOT>
 __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
   constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
+  if (a.counts && a.counts[2] != 0) return;   // planned round aborted by its plan
   DevNode* w = a.nodes + blockIdx.x;
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = lane_id();
   const bool skip = kMeans && w->done_it != 0;   // final in an earlier launch
   __shared__ NodeResult sres;
+  __shared__ uint64_t red[kEpiBlock / 64][8];
+  uint64_t tot[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (!skip) {
+    uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    sum_record<KIND, kEpiBlock>(a, w, acc, (int)threadIdx.x);
+#pragma unroll
+    for (int k = 0; k < F_NUM; ++k) acc[k] = wave_sum_u64(acc[k]);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < F_NUM; ++k) red[wave_id()][k] = acc[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < F_NUM; ++k)
+      for (int v = 0; v < kEpiBlock / 64; ++v) tot[k] += red[v][k];   // (every lane)
+  }
+  if (wave_id() != 0) return;   // the rest is one wave's
   bool final_results = false;
   if (!skip) {
     const int tb = w->tile_begin, te = w->tile_end;
-    uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    sum_record<KIND, kEpiBlock>(a, w, acc, (int)lane);
-    uint64_t tot[7];
-#pragma unroll
-    for (int k = 0; k < F_NUM; ++k) tot[k] = wave_sum_u64(acc[k]);   // in every lane
     int fin = 0;
     if (lane == 0) {
       const uint32_t local_new = (uint32_t)tot[F_CNT];
@@ -644,7 +677,8 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (final_results) store_result(a.hres + blockIdx.x, sres, lane);
+    if (final_results)
+      store_result(a.hres + blockIdx.x, a.dres ? a.dres + blockIdx.x : nullptr, sres, lane, w->len, a.seq);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
       arrive(a.ctr + a.it, blockIdx.x, (uint32_t)a.nn, !skip && !final_results, a.hstat + a.it, a.seq);
@@ -688,7 +722,7 @@ __device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int rec
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (final_results) store_result(a.hres + rec, *sres, lane);
+  if (final_results) store_result(a.hres + rec, a.dres ? a.dres + rec : nullptr, *sres, lane, w->len, a.seq);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0)
     arrive(a.ctr + a.it, (uint32_t)rec, (uint32_t)a.nn, !final_results, a.hstat + a.it, a.seq);
@@ -997,6 +1031,7 @@ __device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32
 }
 
 __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArgs a) {
+  if (a.counts && blockIdx.x >= a.counts[1]) return;   // planned round: grid is an upper bound
   const PartTile pt = a.ptiles[blockIdx.x];
   const Tile* tp = pt.tile;
   const DevNode& nd = *pt.parent;
@@ -1133,6 +1168,216 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
     for (int ww = 0; ww < kTileWaves; ++ww) x += red[ww][threadIdx.x];
     as_gw(a.sparts[2 * blockIdx.x].f)[threadIdx.x] = x;   // (2 TilePartials: 16 words)
   }
+}
+
+// ---------------------------------------------------------------------------
+// Device-planned rounds (PlanArgs, dq_kernels.h).  The tables a host-built
+// round gets from Engine::run_round -- records, tiles, part tiles, cleared
+// counters -- built on the device from the previous round's records and
+// results, so the round can be enqueued before those results exist.  The
+// layout rules are Engine::tile_len and the record fill of run_round,
+// restated; the host mirrors them (Engine::mirror_planned) and checks the
+// counts.
+__device__ __forceinline__ uint32_t plan_tile_len(uint32_t len, uint32_t tl, int32_t nt) {
+  uint64_t t = ((uint64_t)len + (uint32_t)nt - 1) / (uint32_t)nt;
+  t = ((t + kSweep - 1) / kSweep) * kSweep;
+  return (uint32_t)max((uint64_t)kSweep, min((uint64_t)tl, t));
+}
+
+__device__ __forceinline__ uint32_t plan_ntiles(uint32_t len, uint32_t tl, int32_t nt) {
+  if (len == 0) return 1;   // an empty record still gets one (empty) tile
+  const uint32_t t = plan_tile_len(len, tl, nt);
+  return (len + t - 1) / t;
+}
+
+// The split threshold / shift of a child (the cut of :388-403 from its mean
+// and variance), as plan_child and Engine::run_round.
+__device__ __forceinline__ void plan_cut(const NodeResult& r, int side, int32_t* thr, int32_t* shift) {
+  const double* mean = side ? r.nm : r.om;
+  const double* var = side ? r.nv : r.ov;
+  double maxv = var[0], cut = mean[0];
+  int axis = 0;
+  if (maxv < var[1]) { maxv = var[1]; axis = 1; cut = mean[1]; }
+  if (maxv < var[2]) { axis = 2; cut = mean[2]; }
+  *thr = split_threshold(cut);
+  *shift = 16 - 8 * axis;
+}
+
+// One child record: the parent's old (side 0) or new (side 1) half
+// (run_round's fill for a node fused into its parent's partition).
+__device__ void plan_child(const PlanArgs& a, const DevNode& P, const NodeResult& r, int side,
+                           int32_t rec, uint32_t off, uint32_t len, int32_t tb, int32_t pb, int32_t pe) {
+  DevNode d;
+  d.src = P.dst;
+  const uint32_t* pd = P.dst;
+  const bool in_p0 = pd >= a.p0 && pd < a.p0 + a.cap_px;
+  d.dst = const_cast<uint32_t*>(in_p0 ? a.p1 + (pd - a.p0) : a.p0 + (pd - a.p1));
+  d.off = off;
+  d.len = len;
+  d.tile_begin = tb;
+  const uint32_t tln = plan_tile_len(len, a.tl, a.node_tiles);
+  d.tile_end = tb + (int32_t)plan_ntiles(len, a.tl, a.node_tiles);
+  d.split_pb = pb;
+  d.split_pe = pe;
+  d.split_side = side;
+  d.pad0 = 0;
+  d.s = P.s;
+  d.tw = side ? r.nw : r.ow;
+  for (int c = 0; c < 3; ++c) {
+    d.tm[c] = side ? r.nm[c] : r.om[c];
+    d.tv[c] = side ? r.nv[c] : r.ov[c];
+  }
+  int32_t thr, shift;
+  plan_cut(r, side, &thr, &shift);   // the cut of :388-403
+  Params q;
+  q.lhs = q.rr = q.rg = q.rb = 0.0;
+  q.lhsf = q.rrf = q.rgf = q.rbf = q.eps = 0.0f;
+  q.thr = thr;
+  q.shift = shift;
+  q.pad = 0;
+  d.prm = q;
+  for (int c = 0; c < 4; ++c) d.prev[c] = 0;
+  d.n_new_local = 0;
+  d.iter = 0;
+  d.done_it = 0;
+  d.tile_len = tln;
+  d.proven = 0;
+  d.pad2[0] = d.pad2[1] = d.pad2[2] = 0;
+  // the box: the parent's, clipped at the parent's cut when its halves are the cut's
+  const int pax = (16 - P.prm.shift) >> 3;
+  for (int c = 0; c < 3; ++c) { d.box_lo[c] = P.box_lo[c]; d.box_hi[c] = P.box_hi[c]; }
+  if (r.proven) {
+    if (side) d.box_lo[pax] = max(P.box_lo[pax], P.prm.thr);
+    else d.box_hi[pax] = min(P.box_hi[pax], P.prm.thr - 1);
+  }
+  a.cn[rec] = d;
+}
+
+// grid: nb_rec + nb_tile workgroups.  Every workgroup checks that all listed
+// parents are final (else the round aborts) and scans all parents' tile
+// counts into LDS (children's tiles, part tiles: exclusive bases).  Then
+// workgroup b < nb_rec writes the two child records of parents
+// [b * kPlanBlock, ...) (one lane each); the others write one child tile and
+// one part tile per lane (output slot -> parent by binary search), so a
+// parent with ~1000 tiles is spread over the grid.
+constexpr int kPlanBlock = 256;
+__global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t nb_rec) {
+  __shared__ uint32_t s_cb[kPlanMaxParents + 1];   // children's tiles before parent i
+  __shared__ uint32_t s_pb[kPlanMaxParents + 1];   // part tiles before parent i
+  __shared__ uint32_t s_abort;
+  __shared__ uint32_t s_w[kPlanBlock / 64][2];
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int32_t np = a.np;
+  auto parent = [&](int32_t i) -> int32_t { return a.plist ? a.plist[i] : i; };
+  if (tid == 0) s_abort = 0;
+  // clear [LaunchCtr | wparts | rdone] (grid-stride)
+  for (uint32_t i = blockIdx.x * kPlanBlock + tid; i < a.nzero; i += gridDim.x * kPlanBlock) a.zero[i] = 0u;
+  __syncthreads();
+  // (1) every parent final? exclusive scans of the tile counts, chunk by chunk
+  uint32_t run_t = 0, run_p = 0;
+  bool bad = false;
+  for (int32_t c0 = 0; c0 < np; c0 += kPlanBlock) {
+    const int32_t i = c0 + (int32_t)tid;
+    uint32_t t = 0, q = 0;
+    if (i < np) {
+      const DevNode& P = a.pn[parent(i)];
+      bad |= P.done_it == 0;
+      const uint32_t nn = P.n_new_local;
+      t = plan_ntiles(P.len - nn, a.tl, a.node_tiles) + plan_ntiles(nn, a.tl, a.node_tiles);
+      q = (uint32_t)(P.tile_end - P.tile_begin);
+    }
+    uint32_t it = t, ip = q;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(it, o, 64), v = __shfl_up(ip, o, 64);
+      if (lane >= (uint32_t)o) { it += u; ip += v; }
+    }
+    if (lane == 63) { s_w[wv][0] = it; s_w[wv][1] = ip; }
+    __syncthreads();
+    uint32_t bt = run_t, bp = run_p;
+    for (uint32_t w = 0; w < wv; ++w) { bt += s_w[w][0]; bp += s_w[w][1]; }
+    if (i < np) {
+      s_cb[i] = bt + it - t;
+      s_pb[i] = bp + ip - q;
+    }
+    for (int w = 0; w < kPlanBlock / 64; ++w) { run_t += s_w[w][0]; run_p += s_w[w][1]; }
+    __syncthreads();   // (s_w reuse)
+  }
+  if (__any(bad) && lane == 0) s_abort = 1;
+  if (tid == 0) { s_cb[np] = run_t; s_pb[np] = run_p; }
+  __syncthreads();
+  const bool overflow = run_t > a.tiles_cap || run_p > a.ptiles_cap;
+  if (blockIdx.x == 0 && tid == 0) {
+    const uint32_t ab = s_abort ? 1u : (overflow ? 2u : 0u);
+    const uint32_t c[3] = {ab ? 0u : run_t, ab ? 0u : run_p, ab};
+    for (int k = 0; k < 3; ++k) {
+      a.counts[k] = c[k];
+      __hip_atomic_store(a.hcounts + k, c[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (s_abort || overflow) return;
+  if (blockIdx.x < nb_rec) {
+    // (2a) records: parent i -> children 2i (old half), 2i+1 (new half)
+    const int32_t i = (int32_t)(blockIdx.x * kPlanBlock + tid);
+    if (i >= np) return;
+    const int32_t ai = parent(i);
+    const DevNode& P = a.pn[ai];
+    const NodeResult& r = a.pres[ai];
+    const uint32_t nn = P.n_new_local, lo = P.len - nn;
+    const uint32_t t0 = plan_ntiles(lo, a.tl, a.node_tiles);
+    const int32_t pb = (int32_t)s_pb[i], pe = (int32_t)s_pb[i + 1];
+    plan_child(a, P, r, 0, 2 * i, P.off, lo, (int32_t)s_cb[i], pb, pe);
+    plan_child(a, P, r, 1, 2 * i + 1, P.off + lo, nn, (int32_t)(s_cb[i] + t0), pb, pe);
+    return;
+  }
+  // (2b) one child tile and one part tile per lane
+  const uint32_t j = (blockIdx.x - nb_rec) * kPlanBlock + tid;
+  auto find = [&](const uint32_t* base, uint32_t x) -> int32_t {   // last i with base[i] <= x
+    int32_t lo = 0, hi = np - 1;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi + 1) >> 1;
+      if (base[mid] <= x) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  if (j < run_t) {
+    const int32_t i = find(s_cb, j);
+    const DevNode& P = a.pn[parent(i)];
+    const uint32_t nn = P.n_new_local, lo = P.len - nn;
+    const uint32_t t0 = plan_ntiles(lo, a.tl, a.node_tiles);
+    uint32_t k = j - s_cb[i];
+    const int side = k >= t0 ? 1 : 0;
+    if (side) k -= t0;
+    const uint32_t off = side ? P.off + lo : P.off, len = side ? nn : lo;
+    const uint32_t tln = plan_tile_len(len, a.tl, a.node_tiles);
+    Tile tt;
+    tt.node = 2 * i + side;
+    tt.start = off + k * tln;
+    tt.end = off + min(len, (k + 1) * tln);
+    tt.pad = 0;
+    for (int w = 0; w < kTileWaves; ++w) { tt.old_base[w] = 0; tt.new_base[w] = 0; }
+    a.ct[j] = tt;
+  }
+  if (j < run_p) {
+    const int32_t i = find(s_pb, j);
+    const int32_t ai = parent(i);
+    const DevNode& P = a.pn[ai];
+    const NodeResult& r = a.pres[ai];
+    PartTile pt;
+    pt.tile = a.ptiles + P.tile_begin + (j - s_pb[i]);
+    pt.parent = a.pn + ai;
+    plan_cut(r, 0, &pt.thr[0], &pt.shift[0]);
+    plan_cut(r, 1, &pt.thr[1], &pt.shift[1]);
+    pt.child[0] = 2 * i;
+    pt.child[1] = 2 * i + 1;
+    a.cpt[j] = pt;
+  }
+}
+
+// Host-built round tables: host-coherent staging -> the round's device block.
+__global__ __launch_bounds__(256) void upload_kernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
+                                                     uint32_t n16) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n16; i += gridDim.x * 256u) dst[i] = src[i];
 }
 
 // Map, step 1: per colour cell (8x8x8 values), the palette entries that can
@@ -1672,6 +1917,19 @@ void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stre
 void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream) {
   if (nptiles <= 0) return;
   partsplit_kernel<<<dim3(nptiles), dim3(kBlock), 0, stream>>>(a);
+}
+
+void launch_plan(const PlanArgs& a, hipStream_t stream) {
+  const uint32_t nb_rec = (uint32_t)max(1, (a.np + kPlanBlock - 1) / kPlanBlock);
+  const uint32_t nb_tile = (max(a.tiles_cap, a.ptiles_cap) + kPlanBlock - 1) / kPlanBlock;
+  plan_kernel<<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
+}
+
+void launch_upload(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  const uint32_t n16 = (uint32_t)((bytes + 15) / 16);
+  if (n16 == 0) return;
+  const uint32_t nb = min(256u, (n16 + 255u) / 256u);
+  upload_kernel<<<dim3(nb), dim3(256), 0, stream>>>((u32x4*)dst, (const u32x4*)src, n16);
 }
 
 void launch_build_cells(const MapTask* tasks, int ntasks, int kmax, hipStream_t stream) {

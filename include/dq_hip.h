@@ -154,6 +154,14 @@ uint64_t dq_hip_last_points_full(int device);
  * (DivQuantCluster.cpp:613) would recompute the same means and decision.
  * Outputs are identical either way; only the swept points differ. */
 void dq_hip_set_fixed_point(int device, int on);
+/* Device-planned rounds (default on; DQ_HIP_PLAN=0 turns the default off):
+ * while a frame may still need splits, the next round's tables are built on
+ * the GPU from the current round's results and the round is enqueued before
+ * the host has seen them.  Outputs are identical either way;
+ * speculation may expand nodes the greedy replay never uses.
+ * dq_hip_last_planned_rounds: how many rounds of the last run were planned. */
+void dq_hip_set_planned_rounds(int device, int on);
+int dq_hip_last_planned_rounds(int device);
 
 /* Engine lanes a batch of frames is split over (each: own stream, own host
  * thread; DQ_HIP_LANES, default 2).  lanes = 0 restores the default. */

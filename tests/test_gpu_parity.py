@@ -237,16 +237,20 @@ def test_fixed_point_finalisation_is_exact(gpu):
                 full_swept, full = gpu.last_points_swept(), gpu.last_points_full()
                 assert full_swept == full
                 gpu.set_fixed_point(True)
-                b_out, b_ct = _quant_dev(gpu, px, k)
-                assert np.array_equal(a_out, b_out) and np.array_equal(a_ct, b_ct)
-                assert np.array_equal(gpu.last_trace(k), a_trace)
-                b_means, _ = gpu.last_centroids(k)
-                assert np.array_equal(np.nan_to_num(a_means).view(np.uint64),
-                                      np.nan_to_num(b_means).view(np.uint64))
-                assert gpu.last_points_full() == full
-                assert gpu.last_points_swept() < full
+                for plan in (False, True):   # host-planned rounds only: the same nodes
+                    gpu.set_planned_rounds(plan)
+                    b_out, b_ct = _quant_dev(gpu, px, k)
+                    assert np.array_equal(a_out, b_out) and np.array_equal(a_ct, b_ct)
+                    assert np.array_equal(gpu.last_trace(k), a_trace)
+                    b_means, _ = gpu.last_centroids(k)
+                    assert np.array_equal(np.nan_to_num(a_means).view(np.uint64),
+                                          np.nan_to_num(b_means).view(np.uint64))
+                    if not plan:
+                        assert gpu.last_points_full() == full
+                        assert gpu.last_points_swept() < full
     finally:
         gpu.set_fixed_point(True)
+        gpu.set_planned_rounds(True)
 
 
 def test_batch_over_lanes(gpu):
@@ -333,3 +337,42 @@ def test_cpp_linkage_entry_points(gpu):
                 seen.add(int(v))
                 dd.append(int(v))
         assert dd == c["ct"], (i, spec)
+
+
+def test_planned_rounds_equal_host_rounds(gpu):
+    """Device-planned (speculative) rounds against host-planned rounds only:
+    identical colortables, label maps, traces and centroid doubles, on
+    uniform, clustered, coarse and image inputs, single frames and a batch."""
+    import torch
+    cases = [(fx.xorshift(1 << 20, seed=31), 256), (fx.xorshift(500000, seed=32) & 0xF0E0F0, 64),
+             (fx.make_case({"n": 70001, "k": 32, "kind": "clustered", "seed": 5}), 32),
+             (fx.load_png_u32(fx.os.path.join(fx.GOLDEN, "png", "cookie.png"))[0], 125),
+             (fx.xorshift(3000, seed=33), 1024)]
+    try:
+        for px, k in cases:
+            res = []
+            for plan in (False, True):
+                gpu.set_planned_rounds(plan)
+                out, ct = _quant_dev(gpu, px, k)
+                m, _ = gpu.last_centroids(k)
+                res.append((out, ct, gpu.last_trace(k), np.nan_to_num(m).view(np.uint64)))
+            if len(px) == 1 << 20:
+                assert gpu.last_planned_rounds() > 0
+            for x, y in zip(res[0], res[1]):
+                assert np.array_equal(x, y), (len(px), k)
+        frames = [fx.xorshift(300000, seed=40 + i) for i in range(4)]
+        frames[1] &= 0xF8F8F8
+        t_in = [torch.from_numpy(p.view(np.int32)).to("cuda:0") for p in frames]
+        outs = []
+        for plan in (False, True):
+            gpu.set_planned_rounds(plan)
+            t_out = [torch.empty_like(t) for t in t_in]
+            cts, _ = gpu.quant_batch_device(t_in, t_out, 128)
+            torch.cuda.synchronize()
+            outs.append(([t.cpu().numpy() for t in t_out], cts))
+        for a, b in zip(outs[0][0], outs[1][0]):
+            assert np.array_equal(a, b)
+        for a, b in zip(outs[0][1], outs[1][1]):
+            assert np.array_equal(a, b)
+    finally:
+        gpu.set_planned_rounds(True)
