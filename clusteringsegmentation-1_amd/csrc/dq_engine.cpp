@@ -206,6 +206,10 @@ static void grow_coherent(T** h, T** d, size_t* cap, size_t want) {
 // least kSweep points or is its record's last).
 void Engine::ensure_round(size_t rec_cap, size_t tiles_cap, size_t, size_t staging_bytes,
                           int max_iters, hipStream_t stream) {
+  const bool grow = staging_bytes > cap_stage_tab_ || !h_stage_ || !stage_ev_ || rec_cap > cap_res_ ||
+                    !h_res_ || (size_t)max_iters + 1 > cap_stat_ || !h_stat_ || !h_counts_ ||
+                    tiles_cap > cap_parts_ || !d_parts_ || 2 * tiles_cap > cap_sparts_ || !d_sparts_;
+  if (!grow) return;
   DQ_HIP(hipStreamSynchronize(stream));
   if (staging_bytes > cap_stage_tab_ || !h_stage_) {
     if (h_stage_) DQ_HIP(hipHostFree(h_stage_));
@@ -1294,11 +1298,17 @@ constexpr int kMapChunk = 16;   // tasks per batched launch (cell tables: 2.5 MB
 
 void Engine::ensure_map_stage(size_t nmaps) {
   if (nmaps <= cap_mapstage_ && h_mapstage_) return;
+  if (map_pending_) {
+    DQ_HIP(hipEventSynchronize(map_ev_));
+    map_pending_ = false;
+  }
   if (h_mapstage_) DQ_HIP(hipHostFree(h_mapstage_));
   if (d_mapstage_) DQ_HIP(hipFree(d_mapstage_));
   const size_t words = nmaps * (kMapBlockWords + sizeof(MapTask) / 4);
-  DQ_HIP(hipHostMalloc((void**)&h_mapstage_, words * 4, hipHostMallocDefault));
+  DQ_HIP(hipHostMalloc((void**)&h_mapstage_, words * 4, hipHostMallocCoherent | hipHostMallocMapped));
+  DQ_HIP(hipHostGetDevicePointer((void**)&d_mapstage_view_, h_mapstage_, 0));
   DQ_HIP(hipMalloc((void**)&d_mapstage_, words * 4));
+  if (!map_ev_) DQ_HIP(hipEventCreateWithFlags(&map_ev_, hipEventDisableTiming));
   cap_mapstage_ = nmaps;
 }
 
@@ -1313,9 +1323,12 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     DQ_CHECK(jobs[i].k > 0, "colormapSize must be > 0 (DivQuantMapColors.cpp:264)");
     DQ_CHECK(jobs[i].k <= (int)kMapPal, "colormapSize > 16384 is not supported by the LDS palette");
   }
-  // the staging is reused: the previous map's upload must have been consumed
+  // the staging is reused: the previous map's upload must have run
   const double tm0 = trace_ ? host_us() : 0.0;
-  DQ_HIP(hipStreamSynchronize(stream));
+  if (map_pending_) {
+    DQ_HIP(hipEventSynchronize(map_ev_));
+    map_pending_ = false;
+  }
   const double tm1 = trace_ ? host_us() : 0.0;
   const int chunk = std::min(njobs, kMapChunk);
   ensure_map_stage(chunk);
@@ -1334,7 +1347,10 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
   }
   for (int c0 = 0; c0 < njobs; c0 += chunk) {
     const int nt = std::min(chunk, njobs - c0);
-    if (c0 > 0) DQ_HIP(hipStreamSynchronize(stream));   // staging reuse
+    if (c0 > 0 && map_pending_) {   // staging reuse
+      DQ_HIP(hipEventSynchronize(map_ev_));
+      map_pending_ = false;
+    }
     MapTask* ht = reinterpret_cast<MapTask*>(h_mapstage_);
     uint32_t* hblk0 = h_mapstage_ + (size_t)chunk * sizeof(MapTask) / 4;
     uint32_t* dblk0 = d_mapstage_ + (size_t)chunk * sizeof(MapTask) / 4;
@@ -1392,7 +1408,9 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     const size_t bytes = (size_t)chunk * sizeof(MapTask) + woff * 4;
     if (trace_) tr_mapprep_us_ = host_us() - tm1;
     if (staged.empty()) {
-      DQ_HIP(hipMemcpyAsync(d_mapstage_, h_mapstage_, bytes, hipMemcpyHostToDevice, stream));
+      launch_upload(d_mapstage_, d_mapstage_view_, bytes, stream);
+      DQ_HIP(hipEventRecord(map_ev_, stream));
+      map_pending_ = true;
       const MapTask* dt = reinterpret_cast<const MapTask*>(d_mapstage_);
       timed_begin(stream);
       launch_build_cells(dt, nt, kmax, stream);
@@ -1421,13 +1439,13 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
         one.cell_idx = d_cell_idx_;
         one.cell_c32 = d_cell_c32_;
         DQ_HIP(hipStreamSynchronize(stream));   // staging slot 0 reuse
+        map_pending_ = false;
         ht[0] = one;
         if (t != 0) std::memmove(hblk0, hblk0 + blk_off[t], blk_words[t] * 4);
         ht[0].pal = dblk0 + 768 / 2;
         ht[0].lut = reinterpret_cast<const uint16_t*>(dblk0);
-        DQ_HIP(hipMemcpyAsync(d_mapstage_, h_mapstage_,
-                              (size_t)chunk * sizeof(MapTask) + blk_words[t] * 4,
-                              hipMemcpyHostToDevice, stream));
+        launch_upload(d_mapstage_, d_mapstage_view_, (size_t)chunk * sizeof(MapTask) + blk_words[t] * 4,
+                      stream);
         const MapTask* dt = reinterpret_cast<const MapTask*>(d_mapstage_);
         const uint32_t nb = std::max<uint32_t>(1, (j.n / 8 + one.grp_per_block - 1) / one.grp_per_block);
         timed_begin(stream);

@@ -313,6 +313,9 @@ class Engine {
   uint16_t* d_cell_idx_ = nullptr;
   uint32_t* h_mapstage_ = nullptr;   // pinned: per map [sorted palette | start LUT]
   uint32_t* d_mapstage_ = nullptr;
+  uint32_t* d_mapstage_view_ = nullptr;   // device view of h_mapstage_ (host-coherent)
+  hipEvent_t map_ev_ = nullptr;           // the last upload of h_mapstage_
+  bool map_pending_ = false;
   size_t cap_mapstage_ = 0;
   void ensure_map_stage(size_t nmaps);
 

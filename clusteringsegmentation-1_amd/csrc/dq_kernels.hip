@@ -554,6 +554,50 @@ __device__ __forceinline__ void record_cursors(Tile* tiles, const uint32_t* wp, 
     }
 }
 
+// record_cursors over a whole workgroup of W lanes (the split / sharded
+// epilogue: a record of an early round has ~1000 tiles).  Every lane of the
+// workgroup must call it; s_tot: W / 64 words of LDS.
+template <int W>
+__device__ __forceinline__ void block_cursors(Tile* tiles, const uint32_t* wp, int tb, int te,
+                                              uint64_t* s_tot) {
+  const int T = te - tb;
+  const int chunk = (T + W - 1) / W;
+  const int c0 = tb + (int)threadIdx.x * chunk;
+  const int c1 = min(te, c0 + chunk);
+  const uint32_t lane = lane_id(), wv = wave_id();
+  uint64_t local = 0;   // old | new << 32
+  for (int i = c0; i < c1; ++i) {
+    const u32x4 x = *(const u32x4*)(wp + (size_t)i * kTileWaves);
+#pragma unroll
+    for (int ww = 0; ww < kTileWaves; ++ww) local += (uint64_t)(x[ww] & 0xFFFFu) | ((uint64_t)(x[ww] >> 16) << 32);
+  }
+  uint64_t inc = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t u = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += u;
+  }
+  if (lane == 63) s_tot[wv] = inc;
+  __syncthreads();
+  uint64_t base = 0;
+  for (uint32_t w = 0; w < wv; ++w) base += s_tot[w];
+  const uint64_t run0 = base + inc - local;
+  uint32_t ro = (uint32_t)run0, rn = (uint32_t)(run0 >> 32);
+  for (int i = c0; i < c1; ++i) {
+    const u32x4 x = *(const u32x4*)(wp + (size_t)i * kTileWaves);
+    u32x4 ob, nb;
+#pragma unroll
+    for (int ww = 0; ww < kTileWaves; ++ww) {
+      ob[ww] = ro;
+      nb[ww] = rn;
+      ro += x[ww] & 0xFFFFu;
+      rn += x[ww] >> 16;
+    }
+    *(u32x4*)tiles[i].old_base = ob;
+    *(u32x4*)tiles[i].new_base = nb;
+  }
+}
+
 // Final results go straight to host-coherent memory: relaxed system-scope
 // 8-B stores, one per lane (no L2 write-back); the device copy (ddst, may be
 // null) is what the next round's plan reads.  The last word (len_local,
@@ -651,12 +695,13 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
     for (int k = 0; k < F_NUM; ++k)
       for (int v = 0; v < kEpiBlock / 64; ++v) tot[k] += red[v][k];   // (every lane)
   }
-  if (wave_id() != 0) return;   // the rest is one wave's
-  bool final_results = false;
-  if (!skip) {
-    const int tb = w->tile_begin, te = w->tile_end;
+  // lane 0 of wave 0: the FP64 update; the workgroup: the partition cursors
+  // of a record whose split became final; wave 0: results + arrival
+  __shared__ int s_fin;
+  __shared__ uint64_t s_tot[kEpiBlock / 64];
+  if (threadIdx.x == 0) {
     int fin = 0;
-    if (lane == 0) {
+    if (!skip) {
       const uint32_t local_new = (uint32_t)tot[F_CNT];
       if (FROM_TOT) {
         const uint64_t* g = a.tot + (size_t)(blockIdx.x / a.nshard) * 8;
@@ -670,9 +715,13 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
         sres.done_it = w->done_it;
       }
     }
-    final_results = __shfl(fin, 0, 64) != 0;
-    if ((kMeans || KIND == PASS_SPLIT) && final_results) record_cursors(a.tiles, a.wparts, tb, te, lane);
+    s_fin = fin;
   }
+  __syncthreads();
+  const bool final_results = s_fin != 0;
+  if ((kMeans || KIND == PASS_SPLIT) && final_results)
+    block_cursors<kEpiBlock>(a.tiles, a.wparts, w->tile_begin, w->tile_end, s_tot);
+  if (wave_id() != 0) return;
   if (kMeans || KIND == PASS_SPLIT) {   // (split: proven fixed points, status slot max_iters)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1788,13 +1837,23 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   const uint32_t lb = blockIdx.x - tk.block_begin;
   const uint32_t g0 = lb * tk.grp_per_block;
   const uint32_t g1 = min(ngrp, g0 + tk.grp_per_block);
+  // the next iteration's pixels are loaded before this one's are mapped
+  u32x4 na = (u32x4){0u, 0u, 0u, 0u}, nb = na;
+  if (g0 + threadIdx.x < g1) {
+    na = in4[2 * (g0 + threadIdx.x)];
+    nb = in4[2 * (g0 + threadIdx.x) + 1];
+  }
   for (uint32_t gb = g0; gb < g1; gb += kMapLdsBlock) {
     const uint32_t g = gb + threadIdx.x;
     const bool have = g < g1;
     uint32_t px[kMapPx];
     {
-      const u32x4 a = have ? in4[2 * g] : (u32x4){0u, 0u, 0u, 0u};
-      const u32x4 b = have ? in4[2 * g + 1] : (u32x4){0u, 0u, 0u, 0u};
+      const u32x4 a = na, b = nb;
+      const uint32_t gn = g + kMapLdsBlock;
+      if (gn < g1) {
+        na = in4[2 * gn];
+        nb = in4[2 * gn + 1];
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) { px[e] = a[e] & 0xFFFFFFu; px[4 + e] = b[e] & 0xFFFFFFu; }
     }
