@@ -340,6 +340,198 @@ int dqo_quant_recurse(uint32_t n, const uint32_t* in, uint32_t* out,
   return empty;
 }
 
+// ---------------------------------------------------------------------------
+// Weighted path (allPixelsUnique=0): quant_varpart_fast's calc_color_table
+// dedup + DivQuantCluster<false,MT,true> (DivQuantCluster.cpp:1133-1138,
+// :1163-1166).  Every weighted statistic is a sequential FP64 fold over the
+// cluster's points in point order, so the restatement keeps each cluster's
+// (colour, weight) points in order (the reference gathers them by ascending
+// point index, :894-1026) and folds exactly as the reference does.
+
+// calc_color_table restated (DivQuantMapColors.cpp:82-203): unique colours of
+// in[0..n) with weights norm*count, ordered by hash bucket ((R*33023 +
+// G*30013 + B*27011) & 0x7fffffff) % 20023 ascending and, inside a bucket,
+// by first occurrence DESCENDING (chains are prepended, :154-158).  Returns the
+// number of colours.  (numRows = 1, dec_factor = 1: the quant_recurse call.)
+int dqo_color_table(uint32_t n, const uint32_t* in, uint32_t* colours, double* weights) {
+  struct E { uint32_t c, first, count, hash; };
+  std::unordered_map<uint32_t, uint32_t> at;
+  std::vector<E> es;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t c = in[i] & 0xFFFFFF;
+    auto it = at.find(c);
+    if (it != at.end()) { es[it->second].count++; continue; }
+    const long R = (c >> 16) & 0xFF, G = (c >> 8) & 0xFF, B = c & 0xFF;
+    at.emplace(c, (uint32_t)es.size());
+    es.push_back({c, i, 1u, (uint32_t)(((R * 33023 + G * 30013 + B * 27011) & 0x7fffffff) % 20023)});
+  }
+  std::vector<uint32_t> ord(es.size());
+  for (size_t i = 0; i < ord.size(); ++i) ord[i] = (uint32_t)i;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+    return es[a].hash != es[b].hash ? es[a].hash < es[b].hash : es[a].first > es[b].first;
+  });
+  const double norm = 1.0 / (std::ceil(1 / 1.0) * std::ceil(n / 1.0));   // :184
+  for (size_t i = 0; i < ord.size(); ++i) {
+    colours[i] = es[ord[i]].c;
+    weights[i] = norm * es[ord[i]].count;                                  // :195
+  }
+  return (int)es.size();
+}
+
+// DivQuantCluster<false,*,true> restated over (colour, weight) points.
+// Outputs as dqo_cluster; sizes and the trace count points (unique colours).
+int dqo_cluster_weighted(uint32_t num_points, const uint32_t* data, const double* wts,
+                         uint32_t* k_inout, uint32_t* ct, int max_iters, double* means_out,
+                         int64_t* sizes_out, int64_t* trace_out) {
+  if (num_points == 0 || *k_inout == 0 || max_iters < 1) return -1;
+  const int K = (int)*k_inout;
+  struct P { uint32_t c; double w; };
+  struct WC {
+    std::vector<P> px;
+    double weight = 0.0, mean[3] = {0, 0, 0}, var[3] = {0, 0, 0}, tse = 0.0;
+    int64_t size = 0;
+  };
+  std::vector<WC> cl(K);
+  cl[0].px.resize(num_points);
+  for (uint32_t i = 0; i < num_points; ++i) cl[0].px[i] = {data[i] & 0xFFFFFF, wts[i]};
+  cl[0].weight = 1.0;                                   // :329
+  cl[0].size = num_points;
+  int old_index = 0;
+  for (int new_index = 1; new_index < K; ++new_index) {
+    WC& C = cl[old_index];
+    const double tw = C.weight;
+    double tm[3], tv[3];
+    if (new_index == 1) {                               // InitMeanAndVar, weighted (:73-85, :99-101)
+      double m[3] = {0, 0, 0}, v[3] = {0, 0, 0};
+      for (const P& p : C.px) {
+        uint32_t c[3];
+        unpack(p.c, c);
+        for (int a = 0; a < 3; ++a) {
+          m[a] += p.w * c[a];
+          v[a] += p.w * (c[a] * c[a]);
+        }
+      }
+      for (int a = 0; a < 3; ++a) {
+        v[a] -= m[a] * m[a];
+        tm[a] = m[a];
+        tv[a] = v[a];
+      }
+    } else {
+      for (int a = 0; a < 3; ++a) { tm[a] = C.mean[a]; tv[a] = C.var[a]; }
+    }
+    int axis = 0;                                       // :388-403
+    double maxv = tv[0], cut = tm[0];
+    if (maxv < tv[1]) { maxv = tv[1]; axis = 1; cut = tm[1]; }
+    if (maxv < tv[2]) { axis = 2; cut = tm[2]; }
+    // split pass (:438-559), weighted folds in point order
+    double nm[3] = {0, 0, 0}, nw = 0.0, om[3], ow;
+    for (const P& p : C.px) {
+      uint32_t c[3];
+      unpack(p.c, c);
+      if (cut < (double)c[axis]) {
+        for (int a = 0; a < 3; ++a) nm[a] += p.w * c[a];
+        nw += p.w;
+      }
+    }
+    ow = tw - nw;                                       // :576
+    for (int a = 0; a < 3; ++a) nm[a] /= nw;            // :579-581
+    for (int a = 0; a < 3; ++a) om[a] = (tw * tm[a] - nw * nm[a]) / ow;   // :596-598
+    std::vector<P> keep, moved;
+    double nvq[3] = {0, 0, 0};
+    int64_t new_size = 0;
+    for (int it = 0; it < max_iters; ++it) {            // :613-811
+      const bool last = it == max_iters - 1;
+      const double lhs = 0.5 * (om[0] * om[0] - nm[0] * nm[0] + om[1] * om[1] - nm[1] * nm[1] +
+                                om[2] * om[2] - nm[2] * nm[2]);
+      const double rr = om[0] - nm[0], rg = om[1] - nm[1], rb = om[2] - nm[2];
+      double sm[3] = {0, 0, 0}, sq[3] = {0, 0, 0};
+      nw = 0.0;
+      new_size = 0;
+      if (last) { keep.clear(); moved.clear(); }
+      for (const P& p : C.px) {
+        uint32_t c[3];
+        unpack(p.c, c);
+        const double red = c[0], green = c[1], blue = c[2];
+        if (lhs < ((rr * red) + (rg * green) + (rb * blue))) {
+          if (last) keep.push_back(p);
+        } else {
+          sm[0] += p.w * red;
+          sm[1] += p.w * green;
+          sm[2] += p.w * blue;
+          if (last) {
+            for (int a = 0; a < 3; ++a) sq[a] += p.w * (c[a] * c[a]);
+            moved.push_back(p);
+          }
+          nw += p.w;
+          new_size++;
+        }
+      }
+      for (int a = 0; a < 3; ++a) nm[a] = sm[a] / nw;   // :800-802
+      ow = tw - nw;                                     // :805
+      for (int a = 0; a < 3; ++a) om[a] = (tw * tm[a] - nw * nm[a]) / ow;
+      for (int a = 0; a < 3; ++a) nvq[a] = sq[a];
+    }
+    WC& D = cl[new_index];
+    const int64_t parent_size = C.size;
+    if (trace_out) {
+      int64_t* t = trace_out + 4 * (new_index - 1);
+      t[0] = new_index; t[1] = old_index; t[2] = parent_size; t[3] = new_size;
+    }
+    C.size = parent_size - new_size;
+    D.size = new_size;
+    for (int a = 0; a < 3; ++a) { C.mean[a] = om[a]; D.mean[a] = nm[a]; }
+    C.px.swap(keep);
+    D.px.swap(moved);
+    if (new_index == K - 1) break;
+    double nv[3], ov[3];
+    for (int a = 0; a < 3; ++a) nv[a] = nvq[a] / nw - nm[a] * nm[a];   // :836-838
+    for (int a = 0; a < 3; ++a) {
+      const double dn = nm[a] - tm[a], dox = om[a] - tm[a];
+      ov[a] = ((tw * tv[a] - nw * (nv[a] + dn * dn)) / ow) - dox * dox;
+    }
+    for (int a = 0; a < 3; ++a) { C.var[a] = ov[a]; D.var[a] = nv[a]; }
+    C.weight = ow;
+    D.weight = nw;
+    C.tse = ow * (ov[0] + ov[1] + ov[2]);
+    D.tse = nw * (nv[0] + nv[1] + nv[2]);
+    double best = DBL_MIN;
+    for (int ic = 0; ic <= new_index; ++ic)
+      if (best < cl[ic].tse) { best = cl[ic].tse; old_index = ic; }
+  }
+  int out = 0;
+  for (int ic = 0; ic < K; ++ic) {
+    if (means_out)
+      for (int a = 0; a < 3; ++a) means_out[3 * ic + a] = cl[ic].mean[a];
+    if (sizes_out) sizes_out[ic] = cl[ic].size;
+    if (cl[ic].size > 0) {
+      const uint32_t R = (uint8_t)(cl[ic].mean[0] + 0.5);
+      const uint32_t G = (uint8_t)(cl[ic].mean[1] + 0.5);
+      const uint32_t B = (uint8_t)(cl[ic].mean[2] + 0.5);
+      ct[out++] = (R << 16) | (G << 8) | B;
+    }
+  }
+  *k_inout = (uint32_t)out;
+  return K - out;
+}
+
+// quant_recurse(..., allPixelsUnique = 0): table, weighted clustering, dedup, map.
+int dqo_quant_recurse_weighted(uint32_t n, const uint32_t* in, uint32_t* out, uint32_t* k_inout,
+                               uint32_t* ct) {
+  std::vector<uint32_t> colours(n);
+  std::vector<double> w(n);
+  const int u = dqo_color_table(n, in, colours.data(), w.data());
+  int empty = dqo_cluster_weighted((uint32_t)u, colours.data(), w.data(), k_inout, ct, 10, nullptr,
+                                   nullptr, nullptr);
+  if (empty < 0) return empty;
+  std::unordered_set<uint32_t> seen;
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < *k_inout; ++i)
+    if (seen.insert(ct[i]).second) ct[m++] = ct[i];
+  *k_inout = m;
+  dqo_map(in, n, out, ct, (int)m);
+  return empty;
+}
+
 // getSubdividedColors restated (superpixels/OpenCVUtil.cpp:853-897): the 5^3
 // cube {0,63,127,191,255}, R outermost, B innermost, alpha 0xFF.
 void dqo_subdivided_colors(uint32_t* out125) {

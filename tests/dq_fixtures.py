@@ -196,3 +196,47 @@ def load_png_u32(path):
     a = np.asarray(im, dtype=np.uint32)
     px = (a[:, :, 0] << 16) | (a[:, :, 1] << 8) | a[:, :, 2]
     return np.ascontiguousarray(px.reshape(-1), np.uint32), im.width, im.height
+
+
+# --------------------------------------------------------------------------
+# Weighted-path (allPixelsUnique=0) cases: duplicate-heavy inputs where the
+# reference's weighted FP64 folds and the uniform-weight integer sums often
+# decide differently (near-tie TSEs, cuts, 2-means planes), and image regions
+# like the app's per-region calls (ClusteringSegmentation.cpp:1779-1803, K=4).
+def weighted_case_specs():
+    specs = []
+    kinds = ["fewcolours", "greyramp", "tight", "coarse"]
+    ks = [1, 2, 3, 4, 5, 8, 16, 64]
+    for i in range(320):
+        n = 1 + (int(xorshift(1, seed=0xA5A5 + i)[0]) % 3000)
+        specs.append({"n": n, "k": ks[i % len(ks)], "kind": kinds[i % 4], "seed": 5000 + i})
+    for i, (name, k) in enumerate([(nm, k) for nm in ("batman", "cookie") for k in (2, 4, 8, 16)]):
+        for j in range(4):
+            specs.append({"n": 0, "k": k, "kind": "crop_" + name, "seed": 7000 + 10 * i + j})
+    return specs
+
+
+def make_weighted_case(spec):
+    n, kind, seed = spec["n"], spec["kind"], spec["seed"]
+    if kind.startswith("crop_"):   # a rectangle of a sample image, 1K..40K pixels
+        px, w, h = load_png_u32(os.path.join(GOLDEN, "png", kind[5:] + ".png"))
+        r = xorshift(4, seed=seed)
+        cw, ch = 16 + int(r[0]) % 200, 16 + int(r[1]) % 200
+        x0, y0 = int(r[2]) % (w - cw), int(r[3]) % (h - ch)
+        return np.ascontiguousarray(px.reshape(h, w)[y0:y0 + ch, x0:x0 + cw].reshape(-1))
+    r = xorshift(4 * n + 64, seed=seed)
+    if kind == "fewcolours":   # a small palette, skewed counts (geometric-like)
+        ncol = 2 + int(r[0]) % 38
+        pal = r[1:1 + ncol]
+        sel = np.minimum(np.log2(1 + (r[64:64 + n] & 0xFFFF)).astype(np.int64), ncol - 1)
+        return pal[sel].astype(np.uint32)
+    if kind == "greyramp":
+        return (((r[64:64 + n] % 32) * 8) * 0x010101).astype(np.uint32)
+    if kind == "tight":        # one cluster, +-3 per channel
+        base = np.array([60 + int(r[0]) % 140, 60 + int(r[1]) % 140, 60 + int(r[2]) % 140], np.int64)
+        d = np.stack([r[64:64 + n] % 7, (r[64:64 + n] >> 8) % 7, (r[64:64 + n] >> 16) % 7], 1).astype(np.int64) - 3
+        c = np.clip(base + d, 0, 255).astype(np.uint32)
+        return (c[:, 0] << 16) | (c[:, 1] << 8) | c[:, 2]
+    if kind == "coarse":
+        return (r[64:64 + n] & 0xC0C0C0).astype(np.uint32)
+    raise ValueError(kind)

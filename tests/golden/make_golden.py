@@ -238,6 +238,23 @@ def main():
     if want("utils"):
         utils_fixtures(ref)
 
+    # ---- 8b. weighted path on duplicate-heavy inputs and image regions:
+    #        out hash, colortable, trace, centroids, and whether UW differs
+    if want("weighted2"):
+        res, arrs = [], {}
+        for i, spec in enumerate(fx.weighted_case_specs()):
+            px = fx.make_weighted_case(spec)
+            out, ct, trace, means = full_run(ref, instr, px, spec["k"], 0)
+            o1, c1, _ = ref.quant(px, spec["k"], 1)
+            r = dict(spec=spec, n_px=int(len(px)), **rec(out, ct, trace))
+            r["uw_differs"] = bool(not (np.array_equal(o1, out) and np.array_equal(c1, ct)))
+            res.append(r)
+            arrs["trace_%d" % i] = trace.astype(np.int32)
+            arrs["means_%d" % i] = means
+        fx.dump_json("weighted2.json", res)
+        np.savez_compressed(os.path.join(HERE, "weighted2.npz"), **arrs)
+        print("weighted2: %d cases, %d where UW differs" % (len(res), sum(r["uw_differs"] for r in res)))
+
     # ---- 9. C4 at size: the 64 distinct 4K frames of the batch (frame f uses
     #      seed SEED + f) -- hash, colortable, trace of every frame
     if only is not None and "c4" in only:   # (explicit only: ~20 CPU-min)

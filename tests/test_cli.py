@@ -1,0 +1,134 @@
+"""The ClusteringSegmentation command line (clusteringsegmentation-1_amd/cli/):
+the reference's argv contract (ClusteringSegmentationMain.cpp:48-120), its
+PNG codec (imread(IMREAD_COLOR) semantics), and -- on the GPU -- the images
+it writes against the reference's own outputs / the oracle.
+
+CPU: the codec against PIL on the sample images and on every colour type;
+the usage / unreadable-file / no-GPU exits.
+GPU: the CLI on the reference's batman.png: block_quant_full_output.png (the
+125-colour map), block_quant_output.png (4x4 block modes) against the
+oracle, and the tags image against the reference build's quant_recurse
+output (tests/golden/png.json, allPixelsUnique = 0, K = 256).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import dq_fixtures as fx
+
+PKG = os.path.join(fx.ROOT, "clusteringsegmentation-1_amd")
+CLI = os.path.join(PKG, "ClusteringSegmentation")
+NATIVE = os.path.join(fx.TESTS, "native")
+
+
+@pytest.fixture(scope="module")
+def png_check(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("png") / "png_check")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(NATIVE, "png_check.cpp"),
+                           os.path.join(PKG, "cli", "png_io.cpp"), "-lz"])
+    return exe
+
+
+def _decode(png_check, path, tmp_path):
+    raw = str(tmp_path / "out.raw")
+    subprocess.check_call([png_check, "decode", str(path), raw])
+    b = open(raw, "rb").read()
+    w, h = np.frombuffer(b[:8], np.uint32)
+    return np.frombuffer(b[8:], np.uint8).reshape(h, w, 3)
+
+
+def _pil_bgr(path):
+    from PIL import Image
+    a = np.asarray(Image.open(path).convert("RGB"), np.uint8)
+    return a[:, :, ::-1]
+
+
+@pytest.mark.parametrize("name", ["batman", "cookie"])
+def test_decode_sample_images(png_check, tmp_path, name):
+    p = os.path.join(fx.GOLDEN, "png", name + ".png")
+    assert np.array_equal(_decode(png_check, p, tmp_path), _pil_bgr(p))
+
+
+@pytest.mark.parametrize("mode", ["RGB", "RGBA", "L", "LA", "P", "1", "I;16"])
+def test_decode_colour_types(png_check, tmp_path, mode):
+    from PIL import Image
+    rng = np.random.default_rng(7)
+    rgb = rng.integers(0, 256, (37, 53, 3), dtype=np.uint8)
+    if mode == "I;16":
+        g16 = rng.integers(0, 65536, (37, 53), dtype=np.uint16)
+        im = Image.fromarray(g16)
+        expect = np.repeat((g16 >> 8).astype(np.uint8)[:, :, None], 3, axis=2)
+    else:
+        im = Image.fromarray(rgb, "RGB").convert(mode)
+        expect = np.asarray(im.convert("RGB"), np.uint8)[:, :, ::-1]
+    p = tmp_path / ("img_%s.png" % mode.replace(";", ""))
+    im.save(p)
+    assert np.array_equal(_decode(png_check, p, tmp_path), expect)
+
+
+def test_encode_round_trip(png_check, tmp_path):
+    from PIL import Image
+    rng = np.random.default_rng(8)
+    bgr = rng.integers(0, 256, (61, 29, 3), dtype=np.uint8)
+    raw = tmp_path / "in.raw"
+    raw.write_bytes(np.array([29, 61], np.uint32).tobytes() + bgr.tobytes())
+    out = tmp_path / "o.png"
+    subprocess.check_call([png_check, "encode", str(raw), str(out)])
+    assert np.array_equal(np.asarray(Image.open(out).convert("RGB"))[:, :, ::-1], bgr)
+
+
+def test_cli_argv_contract(tmp_path):
+    if not os.path.exists(CLI):
+        pytest.skip("CLI not built")
+    r = subprocess.run([CLI], capture_output=True, text=True)
+    assert r.returncode == 1 and "usage : " in r.stderr and "IMAGE ?TAGS_IMAGE?" in r.stderr
+    r = subprocess.run([CLI, "a", "b", "c"], capture_output=True, text=True)
+    assert r.returncode == 1 and "usage : " in r.stderr
+    r = subprocess.run([CLI, str(tmp_path / "missing.png"), str(tmp_path / "t.png")], capture_output=True,
+                       text=True, cwd=tmp_path)
+    assert r.returncode == 1 and 'read "' in r.stdout and "could not read" in r.stderr
+    # one argument with a directory: cd there, default output outtags.png
+    (tmp_path / "notpng.png").write_bytes(b"nope")
+    r = subprocess.run([CLI, str(tmp_path / "notpng.png")], capture_output=True, text=True)
+    assert r.returncode == 1 and ('cd "%s"' % tmp_path) in r.stdout and 'read "notpng.png"' in r.stdout
+
+
+@pytest.mark.gpu
+def test_cli_on_batman(gpu, tmp_path):
+    """The CLI on the reference's sample image, every output image checked."""
+    src = os.path.join(fx.GOLDEN, "png", "batman.png")
+    r = subprocess.run([CLI, src, str(tmp_path / "tags.png")], capture_output=True, text=True, cwd=tmp_path,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    for line in ['read "', "wrote block_quant_full_output.png", "wrote block_quant_output.png",
+                 "quant_varpart_fast() elapsed:", "map_colors_mps() elapsed:", "quant_recurse K=256",
+                 "wrote %s" % (tmp_path / "tags.png")]:
+        assert line in r.stdout, (line, r.stdout)
+    from PIL import Image
+    px, w, h = fx.load_png_u32(src)
+    # the 125-colour map and the block modes against the oracle
+    pal = fx.subdivided_colors()
+    quant = np.zeros_like(px)
+    fx.oracle().dqo_map(fx.vp(px), ctypes.c_uint32(px.size), fx.vp(quant), fx.vp(pal), ctypes.c_int(125))
+    q_img = np.asarray(Image.open(tmp_path / "block_quant_full_output.png").convert("RGB"), np.uint32)
+    q_u32 = (q_img[:, :, 0] << 16) | (q_img[:, :, 1] << 8) | q_img[:, :, 2]
+    assert np.array_equal(q_u32.reshape(-1), quant & 0xFFFFFF)
+    bw, bh = -(-w // 4), -(-h // 4)
+    mode = np.zeros(bw * bh, np.uint32)
+    z = np.zeros(bw * bh * 16, np.uint32)
+    fx.oracle().dqo_block_hist(fx.vp(quant), ctypes.c_uint32(w), ctypes.c_uint32(h), ctypes.c_uint32(bw),
+                               ctypes.c_uint32(bh), ctypes.c_uint32(4), fx.vp(mode), fx.vp(np.zeros_like(mode)),
+                               fx.vp(z), fx.vp(np.zeros_like(z)))
+    b_img = np.asarray(Image.open(tmp_path / "block_quant_output.png").convert("RGB"), np.uint32)
+    b_u32 = (b_img[:, :, 0] << 16) | (b_img[:, :, 1] << 8) | b_img[:, :, 2]
+    assert np.array_equal(b_u32.reshape(-1), mode & 0xFFFFFF)
+    # the tags against the reference build's quant_recurse(batman, K=256, allPixelsUnique=0)
+    fix = fx.load_json("png.json")["batman"]["k256_weighted"]
+    t_img = np.asarray(Image.open(tmp_path / "tags.png").convert("RGB"), np.uint32)
+    tags = ((t_img[:, :, 0] << 16) | (t_img[:, :, 1] << 8) | t_img[:, :, 2]).reshape(-1)
+    ct = np.array(fix["ct"], np.uint32)
+    assert tags.max() < len(ct)
+    assert "%016x" % fx.fnv(ct[tags]) == fix["out_fnv"]

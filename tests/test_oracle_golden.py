@@ -162,16 +162,79 @@ def test_map_equals_argmin_distance_rank():
         assert np.array_equal(got, want), trial
 
 
-def test_weighted_fixtures_equal_uniform_path():
-    """allPixelsUnique=0 outputs of the reference equal the uniform-weight
-    algorithm on every committed fixture (the GPU serves both with it)."""
+def oracle_quant_weighted(px, k):
+    orc = fx.oracle()
+    px = np.ascontiguousarray(px, np.uint32)
+    out = np.zeros(len(px), np.uint32)
+    ct = np.zeros(k, np.uint32)
+    kk = ctypes.c_uint32(k)
+    orc.dqo_quant_recurse_weighted(ctypes.c_uint32(len(px)), fx.vp(px), fx.vp(out), ctypes.byref(kk),
+                                   fx.vp(ct))
+    return out, ct[:kk.value]
+
+
+def oracle_cluster_weighted(px, k, max_iters=10):
+    orc = fx.oracle()
+    px = np.ascontiguousarray(px, np.uint32)
+    col = np.zeros(len(px), np.uint32)
+    w = np.zeros(len(px), np.float64)
+    u = orc.dqo_color_table(ctypes.c_uint32(len(px)), fx.vp(px), fx.vp(col), fx.vp(w))
+    ct = np.zeros(k, np.uint32)
+    kk = ctypes.c_uint32(k)
+    means = np.zeros((k, 3), np.float64)
+    sizes = np.zeros(k, np.int64)
+    trace = np.zeros((max(k - 1, 1), 4), np.int64)
+    orc.dqo_cluster_weighted(ctypes.c_uint32(u), fx.vp(col), fx.vp(w), ctypes.byref(kk), fx.vp(ct),
+                             ctypes.c_int(max_iters), fx.vp(means), fx.vp(sizes), fx.vp(trace))
+    return ct[:kk.value], means, sizes, trace[:k - 1]
+
+
+def test_weighted_fixtures():
+    """allPixelsUnique=0 (every live app call site): the oracle's weighted
+    restatement (calc_color_table order + ordered FP64 folds) against the
+    reference's outputs -- the synthetic fixtures, the sample images, and the
+    duplicate-heavy / image-region cases of weighted2.json."""
     for c in fx.load_json("weighted.json"):
         s = c["spec"]
         px = fx.xorshift(s["w"] * s["h"]) if s.get("kind") == "xorshift" else fx.make_case(s)
-        out, ct = oracle_quant(px, s["k"])
+        out, ct = oracle_quant_weighted(px, s["k"])
         assert [int(v) for v in ct] == c["ct"], s
         assert "%016x" % fx.fnv(out) == c["out_fnv"], s
     for name, fix in fx.load_json("png.json").items():
-        for k in (4, 16, 125, 256):
-            a, b = fix["k%d" % k], fix["k%d_weighted" % k]
-            assert (a["ct"], a["out_fnv"]) == (b["ct"], b["out_fnv"]), (name, k)
+        px = fx.load_png_u32(fx.os.path.join(fx.GOLDEN, "png", name + ".png"))[0]
+        for k in (4, 16):
+            out, ct = oracle_quant_weighted(px, k)
+            assert [int(v) for v in ct] == fix["k%d_weighted" % k]["ct"], (name, k)
+            assert "%016x" % fx.fnv(out) == fix["k%d_weighted" % k]["out_fnv"], (name, k)
+
+
+def test_weighted2_fixtures():
+    cases = fx.load_json("weighted2.json")
+    arrs = fx.load_npz("weighted2.npz")
+    assert sum(c["uw_differs"] for c in cases) >= 20   # the fixture set exercises the difference
+    for i, c in enumerate(cases):
+        s = c["spec"]
+        px = fx.make_weighted_case(s)
+        assert len(px) == c["n_px"]
+        out, ct = oracle_quant_weighted(px, s["k"])
+        assert [int(v) for v in ct] == c["ct"], (i, s)
+        assert "%016x" % fx.fnv(out) == c["out_fnv"], (i, s)
+        if s["k"] > 1 and i % 4 == 0:
+            _, means, sizes, trace = oracle_cluster_weighted(px, s["k"])
+            assert np.array_equal(trace, arrs["trace_%d" % i]), (i, s)
+            ref = arrs["means_%d" % i]
+            filled = ~np.isnan(ref[:, 0])
+            assert np.array_equal(filled, sizes > 0)
+            assert np.array_equal(means[filled].view(np.uint64), ref[filled].view(np.uint64)), (i, s)
+
+
+def test_color_table_matches_reference():
+    """dqo_color_table against the reference's calc_color_table outputs."""
+    for c in fx.load_json("utils.json")["calc_color_table"]:
+        px = fx.make_case(c["spec"])
+        col = np.zeros(len(px), np.uint32)
+        w = np.zeros(len(px), np.float64)
+        u = fx.oracle().dqo_color_table(ctypes.c_uint32(len(px)), fx.vp(px), fx.vp(col), fx.vp(w))
+        assert u == c["num_colors"]
+        assert [int(v) for v in col[:u]] == c["colors"]
+        assert [float(x).hex() for x in w[:u]] == c["weights"]
