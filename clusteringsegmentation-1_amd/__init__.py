@@ -75,6 +75,7 @@ def lib():
         "dq_hip_comm_destroy": ([c.c_int], c.c_int),
         "dq_hip_cluster_dev": ([c.c_int, vp, c.c_uint32, u32p, vp, c.c_int, vp], c.c_int),
         "dq_hip_map_dev": ([c.c_int, vp, c.c_uint32, vp, vp, c.c_int, vp], c.c_int),
+        "dq_hip_quant_weighted_dev": ([c.c_int, vp, c.c_uint32, vp, u32p, vp, c.c_int, vp], c.c_int),
         "dq_hip_last_centroids": ([c.c_int, vp, vp, c.c_int], c.c_int),
         "dq_hip_last_trace": ([c.c_int, vp, c.c_int], c.c_int),
         "dq_hip_last_rounds": ([c.c_int], c.c_int),
@@ -152,14 +153,22 @@ def map_colors_mps(pixels, colortable):
     return out
 
 
-def quant_varpart_fast(pixels, num_clusters, max_iters=10, device=0):
-    """quant_varpart_fast (DivQuantCluster.cpp:1099-1179), uniform-weight path:
-    the non-empty cluster colours in cluster-index order (not deduplicated)."""
+def quant_varpart_fast(pixels, num_clusters, max_iters=10, device=0, all_pixels_unique=1):
+    """quant_varpart_fast (DivQuantCluster.cpp:1099-1179): the non-empty
+    cluster colours in cluster-index order (not deduplicated); uniform-weight
+    path, or the weighted one for all_pixels_unique=0."""
     import torch
     _require_gpu()
     px = torch.from_numpy(_u32(pixels).reshape(-1).view(np.int32)).to(f"cuda:{device}")
-    ct, _ = cluster_device(px, num_clusters, max_iters=max_iters, device=device)
-    return ct
+    if all_pixels_unique:
+        ct, _ = cluster_device(px, num_clusters, max_iters=max_iters, device=device)
+        return ct
+    ct = np.zeros(num_clusters, np.uint32)
+    k = ctypes.c_uint32(num_clusters)
+    if lib().dq_hip_quant_weighted_dev(device, _dptr(px), px.numel(), None, ctypes.byref(k), _ptr(ct),
+                                       max_iters, None) < 0:
+        raise DivQuantError("dq_hip_quant_weighted_dev: bad arguments")
+    return ct[:k.value].copy()
 
 
 # ---------------------------------------------------------------------------
@@ -181,13 +190,15 @@ def _stream_ptr(stream):
     return ctypes.c_void_p(stream.cuda_stream)
 
 
-def quant_device(t_in, t_out, num_clusters, max_iters=10, device=0, n=None, stream=None):
-    """Cluster + dedup + map of device-resident pixels; returns (colortable, empty)."""
+def quant_device(t_in, t_out, num_clusters, max_iters=10, device=0, n=None, stream=None,
+                 all_pixels_unique=1):
+    """Cluster + dedup + map of device-resident pixels; returns (colortable, empty).
+    all_pixels_unique=0: the weighted path (calc_color_table + ordered folds)."""
     n = _nelem(t_in, n)
     ct = np.zeros(num_clusters, np.uint32)
     k = ctypes.c_uint32(num_clusters)
-    r = lib().dq_hip_quant_dev(device, _dptr(t_in), n, _dptr(t_out), ctypes.byref(k), _ptr(ct),
-                               max_iters, _stream_ptr(stream))
+    fn = lib().dq_hip_quant_dev if all_pixels_unique else lib().dq_hip_quant_weighted_dev
+    r = fn(device, _dptr(t_in), n, _dptr(t_out), ctypes.byref(k), _ptr(ct), max_iters, _stream_ptr(stream))
     if r < 0:
         raise DivQuantError("dq_hip_quant_dev: bad arguments")
     return ct[:k.value].copy(), r

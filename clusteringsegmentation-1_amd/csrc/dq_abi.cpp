@@ -94,6 +94,22 @@ int dq_hip_cluster_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* k
   return j.num_empty;
 }
 
+int dq_hip_quant_weighted_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out,
+                              uint32_t* k, uint32_t* ct, int max_iters, void* stream) {
+  if (!d_in || !k || !ct || n == 0 || *k == 0 || max_iters < 1) return -1;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  dq::FrameJob j;
+  j.d_in = d_in;
+  j.n = n;
+  j.d_out = d_out;
+  j.k = (int)*k;
+  j.ct = ct;
+  e.run_weighted(j, max_iters, d_out != nullptr, (hipStream_t)stream);
+  *k = (uint32_t)j.k_out;
+  return j.num_empty;
+}
+
 int dq_hip_map_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out,
                    const uint32_t* ct, int k, void* stream) {
   if (!d_in || !d_out || !ct || k <= 0) return -1;
@@ -311,7 +327,6 @@ int dq_hip_quant_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_o
 
 int dq_hip_quant(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* k,
                  uint32_t* ct, int uniq, int ngpus) {
-  (void)uniq;
   (void)ngpus;
   if (!in || !out || !k || !ct || n == 0 || *k == 0) return -1;
   Engine& e = engine_for(current_device());
@@ -324,7 +339,8 @@ int dq_hip_quant(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* k,
   j.d_out = e.staged_out();
   j.k = (int)*k;
   j.ct = ct;
-  e.run(&j, 1, 10, true, st);
+  if (uniq) e.run(&j, 1, 10, true, st);
+  else e.run_weighted(j, 10, true, st);
   DQ_HIP(hipMemcpyAsync(out, e.staged_out(), (size_t)n * 4, hipMemcpyDeviceToHost, st));
   DQ_HIP(hipStreamSynchronize(st));
   *k = (uint32_t)j.k_out;
@@ -472,7 +488,6 @@ const char* dq_hip_stat_name(int kind) {
 // quant_util.cpp:20-158.
 void quant_recurse(uint32_t numPixels, const uint32_t* inPixelsPtr, uint32_t* outPixelsPtr,
                    uint32_t* numClustersPtr, uint32_t* outColortablePtr, int allPixelsUnique) {
-  (void)allPixelsUnique;   // both paths run the uniform-weight kernels
   if (numPixels == 0 || *numClustersPtr == 0)
     dq::die("quant_recurse", __FILE__, __LINE__, "numPixels and *numClustersPtr must be > 0");
   Engine& e = engine_for(current_device());
@@ -485,7 +500,8 @@ void quant_recurse(uint32_t numPixels, const uint32_t* inPixelsPtr, uint32_t* ou
   j.n = numPixels;
   j.k = (int)*numClustersPtr;
   j.ct = outColortablePtr;
-  e.run(&j, 1, 10, false, st);
+  if (allPixelsUnique) e.run(&j, 1, 10, false, st);   // uniform weights (:1130-1132)
+  else e.run_weighted(j, 10, false, st);               // calc_color_table + weighted (:1133-1138)
   report_empty(j.num_empty);
   uint32_t k = (uint32_t)j.k_out;
   *numClustersPtr = k;
@@ -524,7 +540,6 @@ void quant_varpart_fast(const uint32_t numPixels, const uint32_t* inPixels, uint
   (void)tmpPixels;
   (void)numRows;
   (void)numCols;
-  (void)allPixelsUnique;
   if (!validate_num_bits((uchar)num_bits))
     dq::die("quant_varpart_fast", __FILE__, __LINE__, "invalid num_bits");
   if (num_bits != 8 || dec_factor != 1)
@@ -542,7 +557,8 @@ void quant_varpart_fast(const uint32_t numPixels, const uint32_t* inPixels, uint
   j.n = numPixels;
   j.k = (int)*numClustersPtr;
   j.ct = colortablePtr;
-  e.run(&j, 1, max_iters, false, st);
+  if (allPixelsUnique) e.run(&j, 1, max_iters, false, st);
+  else e.run_weighted(j, max_iters, false, st);
   report_empty(j.num_empty);
   const int k = j.k_out;
   *numClustersPtr = (uint32_t)k;

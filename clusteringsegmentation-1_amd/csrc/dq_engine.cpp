@@ -1,5 +1,6 @@
 // dq_engine.cpp -- host side of the DivQuant hot path (see dq_engine.h).
 #include "dq_engine.h"
+#include "dq_weighted.h"
 
 #include <rccl/rccl.h>
 
@@ -1215,6 +1216,180 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
                  nframes, S, last_rounds, t_clu - t_run0, tr_build_us_, tr_wait_us_,
                  tr_replay_us_, t_end - t_clu, t_end - t_run0);
   }
+}
+
+// ---------------------------------------------------------------------------
+// The weighted path: quant_varpart_fast's calc_color_table dedup and
+// DivQuantCluster<false,*,true> (DivQuantCluster.cpp:1133-1138, :1163-1166).
+// Rounds as run(): a round splits every node the greedy replay needs, each in
+// one workgroup of wsplit_kernel (its folds are sequential in point order);
+// the host replays the reference's greedy order over the results.
+void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream) {
+  DQ_CHECK(job.n > 0, "num_points must be > 0 (DivQuantCluster.cpp:211)");
+  DQ_CHECK(job.k > 0, "num_colors must be > 0 (DivQuantCluster.cpp:229)");
+  DQ_CHECK(job.d_in && job.ct, "null buffer");
+  DQ_CHECK(max_iters >= 1, "max_iters < 1 is not supported (the reference never writes member[] then)");
+  DQ_CHECK(job.nshard == 1 && (job.n_global == 0 || job.n_global == job.n),
+           "the weighted path takes whole frames in one process");
+  DQ_HIP(hipSetDevice(device_));
+  if (!stream) stream = stream_;
+  const uint32_t n = job.n;
+  ensure_round(2 * (size_t)job.k + 64, 1024, 0, 0, max_iters, stream);   // staging, results
+  // scratch: colour table, unique colours + weights, two id buffers (P0/P1)
+  const size_t need_scratch = color_table_scratch_bytes(n);
+  if (need_scratch > cap_wscratch_) {
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (d_wscratch_) DQ_HIP(hipFree(d_wscratch_));
+    DQ_HIP(hipMalloc(&d_wscratch_, need_scratch));
+    cap_wscratch_ = need_scratch;
+  }
+  if (n > cap_w_) {
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (d_wcol_) DQ_HIP(hipFree(d_wcol_));
+    if (d_ww_) DQ_HIP(hipFree(d_ww_));
+    DQ_HIP(hipMalloc((void**)&d_wcol_, (size_t)n * 4));
+    DQ_HIP(hipMalloc((void**)&d_ww_, (size_t)n * 8));
+    cap_w_ = n;
+  }
+  ensure_pixels((size_t)n + 4);
+  // norm_factor = 1 / (ceil(numRows / dec) * ceil(numCols / dec)), numRows = 1 (:184)
+  const double norm = 1.0 / (std::ceil(1 / 1.0) * std::ceil((double)n / 1.0));
+  uint32_t nu = 0;
+  const int rc = launch_color_table(job.d_in, n, norm, d_wscratch_, cap_wscratch_, d_wcol_, d_ww_, &nu, stream);
+  DQ_CHECK(rc == 0, "colour table failed");
+  launch_iota(d_p0_, nu, stream);
+
+  frames_.assign(1, FrameState());
+  nodes_.clear();
+  segs_.clear();
+  nshard_ = 1;
+  last_rounds = last_planned = last_aborted = 0;
+  last_points_swept = last_points_full = 0;
+  FrameState& f = frames_[0];
+  f.job = &job;
+  f.s = 0.0;
+  Node root;
+  root.w = 1.0;        // :329
+  root.glen = nu;
+  root.buf = BUF_P0;
+  f.leaf.assign(job.k, -1);
+  f.leaf[0] = 0;
+  nodes_.push_back(root);
+  Seg rs;
+  rs.off = 0;
+  rs.len = nu;
+  segs_.push_back(rs);
+  std::vector<int> active;
+  if (job.k > 1) active.push_back(0);
+  std::vector<NodeResult> res;
+  while (!active.empty()) {
+    const int nn = (int)active.size();
+    const size_t rec_bytes = ((size_t)nn * sizeof(WNode) + 255) & ~(size_t)255;
+    const size_t bytes = rec_bytes + (size_t)nn * sizeof(NodeResult);
+    if (bytes > cap_wnodes_) {
+      DQ_HIP(hipStreamSynchronize(stream));
+      if (d_wnodes_) DQ_HIP(hipFree(d_wnodes_));
+      cap_wnodes_ = std::max<size_t>(bytes, 1 << 16);
+      DQ_HIP(hipMalloc(&d_wnodes_, cap_wnodes_));
+    }
+    if (stage_pending_) {
+      DQ_HIP(hipEventSynchronize(stage_ev_));
+      stage_pending_ = false;
+    }
+    DQ_CHECK(rec_bytes <= cap_stage_tab_, "staging too small for the weighted round");
+    WNode* hw = reinterpret_cast<WNode*>(h_stage_);
+    for (int a = 0; a < nn; ++a) {
+      const Node& nd = nodes_[active[a]];
+      const Seg& sg = seg(active[a], 0);
+      WNode& w = hw[a];
+      std::memset(&w, 0, sizeof w);
+      w.src = nd.buf == BUF_P0 ? d_p0_ : d_p1_;
+      w.dst = nd.buf == BUF_P0 ? d_p1_ : d_p0_;
+      w.off = sg.off;
+      w.len = sg.len;
+      w.tw = nd.w;
+      for (int c = 0; c < 3; ++c) { w.tm[c] = nd.mean[c]; w.tv[c] = nd.var[c]; }
+      w.root = active[a] == 0 ? 1 : 0;
+    }
+    launch_upload(d_wnodes_, d_stage_view_, rec_bytes, stream);
+    DQ_HIP(hipEventRecord(stage_ev_, stream));
+    stage_pending_ = true;
+    WArgs wa;
+    wa.nodes = reinterpret_cast<const WNode*>(d_wnodes_);
+    wa.ucol = d_wcol_;
+    wa.uw = d_ww_;
+    wa.res = reinterpret_cast<NodeResult*>(static_cast<char*>(d_wnodes_) + rec_bytes);
+    wa.max_iters = max_iters;
+    wa.fixed_point = fixed_point_ ? 1 : 0;
+    launch_wsplit(wa, nn, stream);
+    res.resize(nn);
+    DQ_HIP(hipMemcpyAsync(res.data(), wa.res, (size_t)nn * sizeof(NodeResult), hipMemcpyDeviceToHost, stream));
+    DQ_HIP(hipStreamSynchronize(stream));
+    last_rounds++;
+    for (int a = 0; a < nn; ++a) {
+      const int id = active[a];
+      const NodeResult& r = res[a];
+      last_points_swept += seg(id, 0).len;
+      if (id == 0)
+        for (int c = 0; c < 3; ++c) { nodes_[0].mean[c] = r.tm[c]; nodes_[0].var[c] = r.tv[c]; }
+      Node co, cn;
+      const int io = (int)nodes_.size();
+      const Node& p = nodes_[id];
+      co.frame = cn.frame = 0;
+      co.parent = cn.parent = id;
+      co.w = r.ow;
+      cn.w = r.nw;
+      for (int c = 0; c < 3; ++c) {
+        co.mean[c] = r.om[c];
+        cn.mean[c] = r.nm[c];
+        co.var[c] = r.ov[c];
+        cn.var[c] = r.nv[c];
+      }
+      co.tse = r.tse_old;
+      cn.tse = r.tse_new;
+      cn.glen = r.n_new;
+      co.glen = p.glen - r.n_new;
+      co.buf = cn.buf = child_buf(p.buf);
+      nodes_.push_back(co);
+      nodes_.push_back(cn);
+      segs_.resize((size_t)(io + 2));
+      Seg& ps = seg(id, 0);
+      Seg& so = seg(io, 0);
+      Seg& sn = seg(io + 1, 0);
+      so.off = ps.off;
+      so.len = ps.len - (uint32_t)r.n_new;
+      sn.off = ps.off + so.len;
+      sn.len = (uint32_t)r.n_new;
+      Node& pp = nodes_[id];
+      pp.child_old = io;
+      pp.child_new = io + 1;
+      pp.expanded = true;
+    }
+    active.clear();
+    if (!(f.need < 0 && f.new_index >= job.k)) {
+      replay(f);
+      next_active(f, &active);
+    }
+  }
+  finish_frame(f, true);
+  if (dedup_map) {
+    size_t cap = 16;
+    while (cap < 2 * (size_t)job.k_out) cap <<= 1;
+    std::vector<uint32_t> table(cap, 0u);
+    int m = 0;
+    for (int i = 0; i < job.k_out; ++i) {   // first-occurrence dedup (quant_util.cpp:93-118)
+      const uint32_t c = job.ct[i];
+      size_t h = (size_t)((c * 2654435761u) >> 7) & (cap - 1);
+      while (table[h] != 0 && table[h] != c + 1) h = (h + 1) & (cap - 1);
+      if (table[h] == 0) {
+        table[h] = c + 1;
+        job.ct[m++] = c;
+      }
+    }
+    job.k_out = m;
+    if (job.d_out) map(job.d_in, job.n, job.d_out, job.ct, m, stream);
+  }
+  DQ_HIP(hipStreamSynchronize(stream));
 }
 
 // ---------------------------------------------------------------------------

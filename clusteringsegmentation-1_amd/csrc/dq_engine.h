@@ -108,6 +108,11 @@ class Engine {
   // with dedup_map, also the colortable dedup (quant_util.cpp:93-118) and
   // map_colors_mps into each frame's d_out.  All frames use max_iters.
   void run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map, hipStream_t stream);
+  // The weighted path (allPixelsUnique = 0): calc_color_table on the device,
+  // then DivQuantCluster<false,*,true> with the reference's ordered FP64 folds
+  // (dq_weighted.hip); dedup + map as run().  last_sizes / last_trace count
+  // points = unique colours, as the reference's size[].
+  void run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream);
 
   // map_colors_mps (DivQuantMapColors.cpp:243-539) on device buffers.
   void map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
@@ -318,6 +323,14 @@ class Engine {
   bool map_pending_ = false;
   size_t cap_mapstage_ = 0;
   void ensure_map_stage(size_t nmaps);
+  // weighted path buffers
+  uint32_t* d_wcol_ = nullptr;        // unique colours
+  double* d_ww_ = nullptr;            // their weights
+  size_t cap_w_ = 0;
+  void* d_wscratch_ = nullptr;        // colour-table scratch (sorts)
+  size_t cap_wscratch_ = 0;
+  void* d_wnodes_ = nullptr;          // a round's WNode records + results
+  size_t cap_wnodes_ = 0;
 
   std::vector<Node> nodes_;
   std::vector<Seg> segs_;             // node * nshard_ + shard

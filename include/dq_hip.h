@@ -28,8 +28,9 @@ int dq_hip_device_count(void);
 
 /* ---- host-pointer entry points (SURVEY 8b build-side shim) ---------------
  * dq_hip_quant: quant_recurse semantics (quant_util.cpp:20-158) without the
- * stdout timer lines.  uniq: allPixelsUnique (both values run the
- * uniform-weight kernels).  ngpus <= 1: current device.
+ * stdout timer lines.  uniq: allPixelsUnique (1: uniform weights; 0: the
+ * weighted path -- calc_color_table dedup + ordered FP64 folds, exactly the
+ * reference's).  ngpus <= 1: current device.
  * Returns the number of empty clusters (>= 0) or < 0 on bad arguments. */
 int dq_hip_quant(const uint32_t *in, uint32_t n, uint32_t *out, uint32_t *k,
                  uint32_t *ct, int uniq, int ngpus);
@@ -133,6 +134,14 @@ int dq_hip_comm_destroy(int device);
  * writes the non-empty cluster colours (cluster-index order, NOT deduped). */
 int dq_hip_cluster_dev(int device, const uint32_t *d_in, uint32_t n,
                        uint32_t *k, uint32_t *ct, int max_iters, void *stream);
+/* The weighted path (allPixelsUnique = 0) on device pixels: calc_color_table
+ * on the GPU (DivQuantMapColors.cpp:82-203), DivQuantCluster<false,*,true>
+ * with the reference's ordered FP64 folds, then (d_out != NULL) the colortable
+ * dedup and map_colors_mps into d_out; d_out NULL: quant_varpart_fast's table
+ * (cluster-index order, not deduped).  Synchronous on return. */
+int dq_hip_quant_weighted_dev(int device, const uint32_t *d_in, uint32_t n,
+                              uint32_t *d_out, uint32_t *k, uint32_t *ct,
+                              int max_iters, void *stream);
 int dq_hip_map_dev(int device, const uint32_t *d_in, uint32_t n,
                    uint32_t *d_out, const uint32_t *ct, int k, void *stream);
 

@@ -164,7 +164,8 @@ def test_png_bgr_end_to_end(gpu, name):
     torch.cuda.synchronize()
     px = _orc_pack(bgr.reshape(-1), w, h, 3 * w)
     mapped = np.zeros(n, np.uint32)
-    fx.oracle().dqo_map(fx.vp(px), ctypes.c_uint32(n), fx.vp(mapped), fx.vp(np.asarray(ct, np.uint32)),
+    ct_u32 = np.asarray(ct, np.uint32)   # (alive across the call)
+    fx.oracle().dqo_map(fx.vp(px), ctypes.c_uint32(n), fx.vp(mapped), fx.vp(ct_u32),
                         ctypes.c_int(len(ct)))
     assert "%016x" % fx.fnv(mapped) == fix["k16"]["out_fnv"]
     assert np.array_equal(d_out.cpu().numpy(), _orc_unpack(mapped, w, h, 3 * w))

@@ -118,10 +118,12 @@ def test_cli_on_batman(gpu, tmp_path):
     assert np.array_equal(q_u32.reshape(-1), quant & 0xFFFFFF)
     bw, bh = -(-w // 4), -(-h // 4)
     mode = np.zeros(bw * bh, np.uint32)
-    z = np.zeros(bw * bh * 16, np.uint32)
+    nd = np.zeros_like(mode)
+    keys = np.zeros(bw * bh * 16, np.uint32)
+    counts = np.zeros_like(keys)   # (all kept alive across the call)
     fx.oracle().dqo_block_hist(fx.vp(quant), ctypes.c_uint32(w), ctypes.c_uint32(h), ctypes.c_uint32(bw),
-                               ctypes.c_uint32(bh), ctypes.c_uint32(4), fx.vp(mode), fx.vp(np.zeros_like(mode)),
-                               fx.vp(z), fx.vp(np.zeros_like(z)))
+                               ctypes.c_uint32(bh), ctypes.c_uint32(4), fx.vp(mode), fx.vp(nd),
+                               fx.vp(keys), fx.vp(counts))
     b_img = np.asarray(Image.open(tmp_path / "block_quant_output.png").convert("RGB"), np.uint32)
     b_u32 = (b_img[:, :, 0] << 16) | (b_img[:, :, 1] << 8) | b_img[:, :, 2]
     assert np.array_equal(b_u32.reshape(-1), mode & 0xFFFFFF)

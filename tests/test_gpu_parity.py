@@ -150,7 +150,11 @@ def test_map_colors_mps(gpu):
 
 
 def test_weighted_path(gpu):
-    """allPixelsUnique=0 (the live app call site, ClusteringSegmentation.cpp:1803)."""
+    """allPixelsUnique=0 (every live app call site, ClusteringSegmentation.cpp:1803):
+    the reference's weighted outputs -- calc_color_table order + ordered FP64
+    folds -- on the synthetic fixtures and on the 352 duplicate-heavy /
+    image-region cases of weighted2.json (55 of which the uniform-weight
+    algorithm gets wrong)."""
     bad = []
     for c in fx.load_json("weighted.json"):
         s = c["spec"]
@@ -158,7 +162,67 @@ def test_weighted_path(gpu):
         out, ct = gpu.quant_recurse(px, s["k"], 0)
         if [int(v) for v in ct] != c["ct"] or "%016x" % fx.fnv(out) != c["out_fnv"]:
             bad.append(s)
+    cases = fx.load_json("weighted2.json")
+    for i, c in enumerate(cases):
+        s = c["spec"]
+        px = fx.make_weighted_case(s)
+        out, ct = gpu.quant_recurse(px, s["k"], 0)
+        if [int(v) for v in ct] != c["ct"] or "%016x" % fx.fnv(out) != c["out_fnv"]:
+            bad.append((i, s, c["uw_differs"]))
     assert not bad, bad
+
+
+def test_weighted_trace_and_centroids(gpu):
+    """The weighted path's split trace (sizes in unique colours) and centroid
+    doubles against the reference's (instrumented build, weighted2.npz)."""
+    import torch
+    cases = fx.load_json("weighted2.json")
+    arrs = fx.load_npz("weighted2.npz")
+    for i, c in enumerate(cases):
+        s = c["spec"]
+        if s["k"] == 1 or i % 3:
+            continue
+        px = fx.make_weighted_case(s)
+        t = torch.from_numpy(px.view(np.int32)).to("cuda:0")
+        o = torch.empty_like(t)
+        ct, _ = gpu.quant_device(t, o, s["k"], all_pixels_unique=0)
+        torch.cuda.synchronize()
+        assert [int(v) for v in ct] == c["ct"], (i, s)
+        assert "%016x" % fx.fnv(o.cpu().numpy().view(np.uint32)) == c["out_fnv"], (i, s)
+        assert np.array_equal(gpu.last_trace(s["k"]), arrs["trace_%d" % i]), (i, s)
+        _check_centroids(gpu, s["k"], arrs["means_%d" % i])
+
+
+def test_weighted_vs_oracle_sweep(gpu):
+    """Fresh seeded duplicate-heavy inputs against the oracle's weighted restatement."""
+    rng = np.random.default_rng(777)
+    for trial in range(40):
+        n = int(rng.integers(1, 60000))
+        k = int(rng.choice([1, 2, 3, 4, 7, 16, 64, 256]))
+        ncol = int(rng.integers(1, 3000))
+        pal = rng.integers(0, 1 << 24, ncol, dtype=np.uint32)
+        px = pal[rng.integers(0, ncol, n)]
+        if trial % 3 == 0:
+            px &= 0xE0E0E0
+        out, ct = gpu.quant_recurse(px, k, 0)
+        ref_out = np.zeros(n, np.uint32)
+        ref_ct = np.zeros(k, np.uint32)
+        kk = ctypes.c_uint32(k)
+        fx.oracle().dqo_quant_recurse_weighted(ctypes.c_uint32(n), fx.vp(px), fx.vp(ref_out), ctypes.byref(kk),
+                                               fx.vp(ref_ct))
+        assert np.array_equal(ct, ref_ct[:kk.value]), (trial, n, k)
+        assert np.array_equal(out, ref_out), (trial, n, k)
+    # quant_varpart_fast(allPixelsUnique=0): the table before the dedup
+    px = fx.make_weighted_case(fx.weighted_case_specs()[5])
+    ct = gpu.quant_varpart_fast(px, 8, all_pixels_unique=0)
+    col = np.zeros(len(px), np.uint32)
+    w = np.zeros(len(px), np.float64)
+    u = fx.oracle().dqo_color_table(ctypes.c_uint32(len(px)), fx.vp(px), fx.vp(col), fx.vp(w))
+    rct = np.zeros(8, np.uint32)
+    kk = ctypes.c_uint32(8)
+    fx.oracle().dqo_cluster_weighted(ctypes.c_uint32(u), fx.vp(col), fx.vp(w), ctypes.byref(kk), fx.vp(rct),
+                                     ctypes.c_int(10), None, None, None)
+    assert np.array_equal(ct, rct[:kk.value])
 
 
 def test_oracle_random_sweep(gpu):
