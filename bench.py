@@ -44,11 +44,6 @@ import time
 
 import numpy as np
 
-# The engine overlaps frames on two lanes (HIP streams); with HIP's default
-# of 4 hardware queues per process the lanes' streams and torch's sometimes
-# share a queue and serialise (measured: ~1 run in 5 at the one-lane speed).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")

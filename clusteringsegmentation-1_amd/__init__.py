@@ -140,6 +140,20 @@ def quant_recurse(pixels, num_clusters, all_pixels_unique=1):
     return out, ct[:k.value].copy()
 
 
+def quant_host(pixels, num_clusters, all_pixels_unique=1, ngpus=1):
+    """dq_hip_quant (quant_recurse without the timer lines) on host pixels;
+    ngpus > 1 shards the frame over this process's devices (RCCL in-process)."""
+    _require_gpu()
+    px = _u32(pixels).reshape(-1)
+    out = np.zeros(px.size, np.uint32)
+    ct = np.zeros(num_clusters, np.uint32)
+    k = ctypes.c_uint32(num_clusters)
+    if lib().dq_hip_quant(_ptr(px), px.size, _ptr(out), ctypes.byref(k), _ptr(ct), int(all_pixels_unique),
+                          int(ngpus)) < 0:
+        raise DivQuantError("dq_hip_quant: bad arguments")
+    return out, ct[:k.value].copy()
+
+
 def map_colors_mps(pixels, colortable):
     """map_colors_mps (DivQuant/DivQuantMapColors.cpp:243-539)."""
     _require_gpu()

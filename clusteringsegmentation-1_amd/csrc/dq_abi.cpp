@@ -25,6 +25,9 @@
 #include "../../include/quant_util.h"
 #include "dq_engine.h"
 
+#include <rccl/rccl.h>
+#include <map>
+
 using dq::Engine;
 using dq::engine_for;
 
@@ -325,10 +328,80 @@ int dq_hip_quant_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_o
   return r;
 }
 
+// dq_hip_quant over ngpus devices of this process: the frame's pixels split
+// into ngpus row ranges (4-point multiples), one per device, every pass's node
+// totals allreduced over an in-process RCCL communicator set
+// (ncclCommInitAll, created once per device count); each device maps its own
+// range.  Uniform-weight path only (the weighted path's folds are sequential).
+static int quant_multi_gpu(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* k, uint32_t* ct,
+                           int G) {
+  static std::mutex mu;
+  static std::map<int, std::vector<ncclComm_t>> sets;
+  std::vector<ncclComm_t>* comms;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = sets.find(G);
+    if (it == sets.end()) {
+      std::vector<ncclComm_t> c(G);
+      std::vector<int> devs(G);
+      for (int d = 0; d < G; ++d) devs[d] = d;
+      const ncclResult_t r = ncclCommInitAll(c.data(), G, devs.data());
+      if (r != ncclSuccess) dq::die("ncclCommInitAll", __FILE__, __LINE__, ncclGetErrorString(r));
+      it = sets.emplace(G, std::move(c)).first;
+    }
+    comms = &it->second;
+  }
+  std::vector<uint32_t> first(G + 1);
+  for (int g = 0; g <= G; ++g) first[g] = g == G ? n : (uint32_t)(((uint64_t)n * g / G) & ~(uint64_t)3);
+  std::vector<std::vector<uint32_t>> cts(G, std::vector<uint32_t>(*k));
+  std::vector<int> kout(G, 0), empty(G, 0);
+  auto work = [&](int g) {
+    Engine& e = engine_for(g);
+    std::lock_guard<std::mutex> lk(e.mutex());
+    DQ_HIP(hipSetDevice(g));
+    hipStream_t st = e.stream();
+    const uint32_t len = first[g + 1] - first[g];
+    const Engine::CommState prev = e.swap_comm({(*comms)[g], G, g});
+    dq::FrameJob j;
+    if (len > 0) {
+      e.stage_in(in + first[g], len, st);
+      j.d_in = e.staged_in();
+      j.d_out = e.staged_out();
+    } else {   // (n < 4 G: an empty range still takes part in every allreduce)
+      e.stage_in(in, 1, st);
+      j.d_in = e.staged_in();
+    }
+    j.n = len > 0 ? len : 1;
+    j.n_global = n;
+    j.k = (int)*k;
+    j.ct = cts[g].data();
+    e.run(&j, 1, 10, true, st);
+    if (len > 0)
+      DQ_HIP(hipMemcpyAsync(out + first[g], e.staged_out(), (size_t)len * 4, hipMemcpyDeviceToHost, st));
+    DQ_HIP(hipStreamSynchronize(st));
+    e.swap_comm(prev);
+    kout[g] = j.k_out;
+    empty[g] = j.num_empty;
+  };
+  std::vector<std::thread> th;
+  for (int g = 1; g < G; ++g) th.emplace_back(work, g);
+  work(0);
+  for (auto& t : th) t.join();
+  for (int g = 1; g < G; ++g)   // every device ran the identical FP64 updates on identical totals
+    if (kout[g] != kout[0] || cts[g] != cts[0]) dq::die("dq_hip_quant", __FILE__, __LINE__, "devices disagree");
+  std::memcpy(ct, cts[0].data(), (size_t)kout[0] * 4);
+  *k = (uint32_t)kout[0];
+  return empty[0];
+}
+
 int dq_hip_quant(const uint32_t* in, uint32_t n, uint32_t* out, uint32_t* k,
                  uint32_t* ct, int uniq, int ngpus) {
-  (void)ngpus;
   if (!in || !out || !k || !ct || n == 0 || *k == 0) return -1;
+  const int G = std::min(std::max(ngpus, 1), dq_hip_device_count());
+  // (DQ_HIP_MULTI_1=1: the in-process communicator path even on one device -- tests)
+  const char* m1 = std::getenv("DQ_HIP_MULTI_1");
+  const bool force = m1 && m1[0] == '1' && ngpus >= 1;
+  if ((G > 1 || force) && uniq && n >= 4u * (uint32_t)G) return quant_multi_gpu(in, n, out, k, ct, G);
   Engine& e = engine_for(current_device());
   std::lock_guard<std::mutex> g(e.mutex());
   hipStream_t st = e.stream();

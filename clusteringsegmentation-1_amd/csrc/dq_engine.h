@@ -141,6 +141,17 @@ class Engine {
   static void comm_unique_id(char id[128]);
   void comm_init(int nranks, int rank, const char id[128]);
   void comm_destroy();
+  // In-process multi-GPU (dq_hip_quant's ngpus): borrow a communicator of a
+  // set created by ncclCommInitAll for the duration of one run; returns the
+  // engine's previous one (restore with the same call).
+  struct CommState { void* comm; int ranks, rank; };
+  CommState swap_comm(CommState c) {
+    CommState old{comm_, comm_ranks_, comm_rank_};
+    comm_ = c.comm;
+    comm_ranks_ = c.ranks;
+    comm_rank_ = c.rank;
+    return old;
+  }
   int comm_ranks() const { return comm_ranks_; }
   void allreduce_totals(int nlogical, hipStream_t stream);
   int device() const { return device_; }

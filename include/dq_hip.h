@@ -30,7 +30,11 @@ int dq_hip_device_count(void);
  * dq_hip_quant: quant_recurse semantics (quant_util.cpp:20-158) without the
  * stdout timer lines.  uniq: allPixelsUnique (1: uniform weights; 0: the
  * weighted path -- calc_color_table dedup + ordered FP64 folds, exactly the
- * reference's).  ngpus <= 1: current device.
+ * reference's).  ngpus <= 1: current device; ngpus > 1 (uniform
+ * weights): the pixels split into ngpus ranges over devices 0..ngpus-1 of
+ * this process (clamped to the visible devices), every pass's node totals
+ * allreduced over an in-process RCCL communicator set (ncclCommInitAll,
+ * xGMI), each device mapping its own range.
  * Returns the number of empty clusters (>= 0) or < 0 on bad arguments. */
 int dq_hip_quant(const uint32_t *in, uint32_t n, uint32_t *out, uint32_t *k,
                  uint32_t *ct, int uniq, int ngpus);

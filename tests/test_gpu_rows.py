@@ -119,3 +119,27 @@ def test_rows_n_global_needs_comm(gpu):
     t = torch.zeros(4096, dtype=torch.int32, device="cuda:0")
     with pytest.raises(gpu.DivQuantError):
         gpu.quant_rows_device([t], [torch.empty_like(t)], 16, n_globals=[8192])
+
+
+def test_dq_hip_quant_ngpus(gpu):
+    """dq_hip_quant's ngpus (in-process multi-GPU over ncclCommInitAll): the
+    result equals the oracle's for every ngpus (clamped to the devices here);
+    DQ_HIP_MULTI_1=1 drives the in-process communicator path on one device."""
+    import os
+    import subprocess
+    import sys
+    px = fx.xorshift(300001, seed=4321)
+    r_out, r_ct = _oracle(px, 128)[:2]
+    for ng in (1, 2, 8):
+        out, ct = gpu.quant_host(px, 128, 1, ng)
+        assert np.array_equal(ct, r_ct) and np.array_equal(out, r_out), ng
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "import dq_fixtures as fx\nfrom __graft_entry__ import load_package\n"
+            "p = load_package(); px = fx.xorshift(300001, seed=4321)\n"
+            "out, ct = p.quant_host(px, 128, 1, 1)\n"
+            "print(fx.fnv(out), ' '.join(str(int(c)) for c in ct))\n") % (fx.TESTS, fx.ROOT)
+    env = dict(os.environ, DQ_HIP_MULTI_1="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=200)
+    assert r.returncode == 0, r.stderr[-2000:]
+    h, cts = r.stdout.strip().splitlines()[-1].split(" ", 1)
+    assert int(h) == fx.fnv(r_out) and [int(c) for c in cts.split()] == [int(c) for c in r_ct]
