@@ -56,15 +56,19 @@ CONFIGS = {   # BASELINE.json configs (C4 = 64 x c3 frames; C5 = c5 row-sharded)
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # kernel kinds the roofline may name -> (kernel symbol, engine-model bytes per
-# point, SURVEY 8(d)-model bytes per point).  Engine model:
-# every statistics pass reads 4 B per swept point, the fused partition +
-# split pass reads 4 B and writes 4 B per parent point, the map reads 4 B and
-# writes 4 B per pixel.  SURVEY 8(d) counts the partition's write as overhead.
-ROOF_KERNELS = {"pass_kmeans": ("kpass_kernel<PASS_KMEANS>", 4, 4),
-                "partition": ("partsplit_kernel", 8, 4),
-                "pass_split": ("pass_kernel<PASS_SPLIT>", 4, 4),
-                "pass_init": ("pass_kernel<PASS_INIT>", 4, 4),
-                "map": ("map_lds_kernel", 8, 8)}
+# point as stated in DESIGN.md 5, SURVEY 8(d)-model bytes per point).  Engine
+# model: a pass reads 4 B per point of the caller's packed frame (the roots)
+# and 3 B per point of the planar working buffers; the fused partition +
+# split pass reads 4 or 3 B and writes 3 B per parent point; the map reads
+# 4 B and writes 4 B per pixel.  The engine counts these bytes per launch
+# (dq_hip_get_stat); SURVEY 8(d) counts 4 B per point read and classes the
+# partition's write as overhead.
+ROOF_KERNELS = {"pass_kmeans": ("kpass_kernel<PASS_KMEANS>", "3 B read per swept point", 4),
+                "partition": ("partsplit_kernel", "3 B read (4 B from a root's packed frame) + 3 B written "
+                              "per parent point", 4),
+                "pass_split": ("pass_kernel<PASS_SPLIT>", "4 B read per root point, 3 B per other point", 4),
+                "pass_init": ("pass_kernel<PASS_INIT>", "4 B read per point (packed frames)", 4),
+                "map": ("map_lds_kernel", "4 B read + 4 B written per pixel", 8)}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -243,16 +247,18 @@ def pick_roofline(stats, pmc_key):
     if not cand:
         return None
     kind = max(cand, key=lambda k: cand[k][1])
-    launches, ms, alg = cand[kind]
+    launches, ms, alg, units = cand[kind]
     sym, b_eng, b_survey = ROOF_KERNELS[kind]
     gbs = alg / (ms / 1e3) / 1e9
+    gbs_survey = b_survey * units / (ms / 1e3) / 1e9
     roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": sym, "launches": launches,
             "avg_launch_us": round(ms * 1e3 / launches, 2),
             "alg_bytes_per_launch": round(alg / launches),
-            "alg_model": "engine work model (DESIGN.md 5): %d B per point of this kernel" % b_eng,
-            "frac_survey_model": round(gbs * b_survey / b_eng / HBM_PEAK_GBS, 4),
+            "points_per_launch": round(units / launches),
+            "alg_model": "engine work model (DESIGN.md 5): %s" % b_eng,
+            "frac_survey_model": round(gbs_survey / HBM_PEAK_GBS, 4),
             "survey_model": "SURVEY 8(d): %d B per point (a partition's write is overhead)" % b_survey,
             "share_of_step_kernel_time": round(ms / sum(v[1] for v in stats.values() if v[1] > 0), 3),
             "measured": "HIP events around every launch on the engine's stream, one engine lane "
@@ -463,7 +469,7 @@ def main():
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "u8x3 pixels in u32, u32/u64 integer sums, f64 updates",
+            "dtype": "u8 RGB (packed u32 frames, planar u8 working buffers), u32/u64 integer sums, f64 updates",
             "data": "synthetic uniform-random 24-bit RGB frames (SURVEY 8c xorshift64, frame f = seed + f)",
             "config": {"workload": workload, "frames_per_rank_per_step": nf if a.mode == "frames" else None,
                        "frames_per_step": nf if a.mode == "rows" else None,

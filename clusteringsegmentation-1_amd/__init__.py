@@ -486,10 +486,11 @@ def reset_stats(device=0):
 
 
 def get_stats(device=0):
-    """{kind: (launches, total_ms, algorithmic_bytes)} from HIP events on the launch stream."""
+    """{kind: (launches, total_ms, engine-model bytes, points)} from HIP events on the launch stream."""
     res = {}
     for i, name in enumerate(STAT_KINDS):
-        l, ms, b = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double()
+        l, ms, b, u = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         lib().dq_hip_get_stat(device, i, ctypes.byref(l), ctypes.byref(ms), ctypes.byref(b))
-        res[name] = (int(l.value), float(ms.value), float(b.value))
+        lib().dq_hip_get_stat_units(device, i, ctypes.byref(u))
+        res[name] = (int(l.value), float(ms.value), float(b.value), float(u.value))
     return res

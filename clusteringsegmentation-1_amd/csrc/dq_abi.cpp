@@ -547,6 +547,12 @@ int dq_hip_get_stat(int device, int kind, uint64_t* launches, double* ms, double
   return 0;
 }
 
+int dq_hip_get_stat_units(int device, int kind, double* units) {
+  if (kind < 0 || kind >= dq::ST_COUNT) return -1;
+  if (units) *units = engine_for(device).stats[kind].units;
+  return 0;
+}
+
 const char* dq_hip_stat_name(int kind) {
   static const char* names[] = {"pass_init", "pass_split", "pass_kmeans", "pass_klast",
                                 "epilogue", "partition", "map_cells", "map", "plan"};

@@ -35,6 +35,7 @@ inline double host_us() {
 constexpr int BUF_IN = 0, BUF_P0 = 1, BUF_P1 = 2;
 inline int child_buf(int b) { return b == BUF_P0 ? BUF_P1 : BUF_P0; }
 inline size_t align4(size_t x) { return (x + 3) & ~(size_t)3; }
+inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // Split-pass threshold (:473): cut_pos < v <=> v >= thr for integer v.
 int32_t split_threshold(double cut) {
@@ -84,17 +85,18 @@ hipEvent_t Engine::take_event() {
 
 void Engine::timed_begin(hipStream_t stream) {
   if (!timing_) return;
-  PendingEvent pe{take_event(), nullptr, -1, 0.0};
+  PendingEvent pe{take_event(), nullptr, -1, 0.0, 0.0};
   DQ_HIP(hipEventRecord(pe.a, stream));
   pending_.push_back(pe);
 }
 
-void Engine::timed_end(int kind, double bytes, hipStream_t stream) {
+void Engine::timed_end(int kind, double bytes, hipStream_t stream, double units) {
   if (!timing_) return;
   PendingEvent& pe = pending_.back();
   pe.b = take_event();
   pe.kind = kind;
   pe.bytes = bytes;
+  pe.units = units;
   DQ_HIP(hipEventRecord(pe.b, stream));
 }
 
@@ -107,6 +109,7 @@ void Engine::collect_timing() {
     st.launches++;
     st.ms += ms;
     st.bytes += pe.bytes;
+    st.units += pe.units;
     event_pool_.push_back(pe.a);
     event_pool_.push_back(pe.b);
   }
@@ -280,9 +283,11 @@ uint32_t Engine::wait_status(const uint64_t* slot, uint64_t seq, hipStream_t str
   }
 }
 
-const uint32_t* Engine::buf_ptr(int buf, const FrameState& f, int shard) const {
-  if (buf == BUF_IN) return f.in[shard];
-  return (buf == BUF_P0 ? d_p0_ : d_p1_) + f.base[shard];
+// A frame shard in a buffer: the caller's packed frame (BUF_IN), or byte 0 of
+// its R plane in P0 / P1 (planes cap_px_ bytes apart: DESIGN.md 4).
+const uint8_t* Engine::buf_ptr(int buf, const FrameState& f, int shard) const {
+  if (buf == BUF_IN) return reinterpret_cast<const uint8_t*>(f.in[shard]);
+  return reinterpret_cast<const uint8_t*>(buf == BUF_P0 ? d_p0_ : d_p1_) + f.base[shard];
 }
 
 // Tile length of a round of `total` points: whole 4096-point sweeps, about
@@ -351,13 +356,20 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   DQ_CHECK((size_t)nr <= cap_res_, "round larger than the run's record capacity");
 
   uint64_t total = 0, own_total = 0, parent_total = 0;   // local points
+  double own_bytes = 0.0, part_bytes = 0.0;               // engine work model
   for (int a = 0; a < nl; ++a)
     for (int sh = 0; sh < S; ++sh) {
       total += seg(order[a], sh).len;
-      if (a < n_own) own_total += seg(order[a], sh).len;
+      if (a < n_own) {
+        own_total += seg(order[a], sh).len;
+        own_bytes += point_bytes(order[a]) * seg(order[a], sh).len;
+      }
     }
   for (int p : parents)
-    for (int sh = 0; sh < S; ++sh) parent_total += seg(p, sh).len;
+    for (int sh = 0; sh < S; ++sh) {
+      parent_total += seg(p, sh).len;
+      part_bytes += (point_bytes(p) + 3.0) * seg(p, sh).len;
+    }
   const uint64_t tl = round_tile_len(total);
   size_t ntiles = 0, nt_own = 0;
   for (int a = 0; a < nl; ++a) {   // empty records get one empty tile (their epilogue still runs)
@@ -456,7 +468,8 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     for (int sh = 0; sh < S; ++sh) {
       DevNode& d = hn[a * S + sh];
       d.src = buf_ptr(n.buf, fs, sh);
-      d.dst = (child_buf(n.buf) == BUF_P0 ? d_p0_ : d_p1_) + fs.base[sh];
+      d.dst = const_cast<uint8_t*>(buf_ptr(child_buf(n.buf), fs, sh));
+      d.planar = n.buf != BUF_IN;
       const Seg& sg = seg(order[a], sh);
       d.off = sg.off;
       d.len = sg.len;
@@ -547,14 +560,15 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = nullptr;
+  ra.plane = cap_px_;
   const double bytes_all = 4.0 * (double)total;
   const int nt = (int)ntiles;
-  auto pass = [&](int kind, int st, int tiles, double pbytes) {
+  auto pass = [&](int kind, int st, int tiles, double pbytes, double units) {
     ra.it = 0;
     if (tiles > 0) {
       timed_begin(stream);
       launch_pass(kind, ra, tiles, stream);
-      timed_end(st, pbytes, stream);
+      timed_end(st, pbytes, stream, units);
     }
   };
   auto epilogue = [&](int kind, int it) {
@@ -568,14 +582,14 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     timed_end(ST_EPILOGUE, 0.0, stream);
   };
   if (root_round) {
-    pass(PASS_INIT, ST_INIT, nt, bytes_all);
+    pass(PASS_INIT, ST_INIT, nt, bytes_all, (double)total);
     epilogue(PASS_INIT, -1);
   }
-  pass(PASS_SPLIT, ST_SPLIT, (int)nt_own, 4.0 * (double)own_total);
+  pass(PASS_SPLIT, ST_SPLIT, (int)nt_own, own_bytes, (double)own_total);
   if (nptiles > 0) {
     timed_begin(stream);
     launch_partsplit(ra, (int)nptiles, stream);
-    timed_end(ST_PARTITION, 8.0 * (double)parent_total, stream);
+    timed_end(ST_PARTITION, part_bytes, stream, (double)parent_total);
   }
   epilogue(PASS_SPLIT, max_iters);
   R.t_enq = tb1;
@@ -621,9 +635,11 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   R.nl = R.nr = 2 * np;
   R.n_own = 0;
   uint64_t total = 0;
+  double part_bytes = 0.0;
   for (int32_t a : plist) {
     const int id = P.order[a];
     total += seg(id, 0).len;
+    part_bytes += (point_bytes(id) + 3.0) * seg(id, 0).len;
     Node& pn = nodes_[id];
     pn.partitioned = true;
     frames_[pn.frame].splits_queued += 2;
@@ -675,9 +691,9 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   pa.nzero = (uint32_t)((bytes - o_ctr) / 4);
   pa.counts = R.dcounts;
   pa.hcounts = d_counts_h_ + 4 * R.par;
-  pa.p0 = d_p0_;
-  pa.p1 = d_p1_;
-  pa.cap_px = cap_px_;
+  pa.p0 = reinterpret_cast<const uint8_t*>(d_p0_);
+  pa.p1 = reinterpret_cast<const uint8_t*>(d_p1_);
+  pa.cap_bytes = 4 * cap_px_;
   RoundArgs& ra = R.ra;
   ra.tiles = R.dt;
   ra.nodes = R.dn;
@@ -698,12 +714,13 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = R.dcounts;
+  ra.plane = cap_px_;
   timed_begin(stream);
   launch_plan(pa, stream);
   timed_end(ST_PLAN, 0.0, stream);
   timed_begin(stream);
   launch_partsplit(ra, (int)R.ptiles_cap, stream);
-  timed_end(ST_PARTITION, 8.0 * (double)total, stream);
+  timed_end(ST_PARTITION, part_bytes, stream, (double)total);
   timed_begin(stream);
   launch_epilogue(PASS_SPLIT, ra, R.nr, false, stream);
   timed_end(ST_EPILOGUE, 0.0, stream);
@@ -757,7 +774,7 @@ void Engine::kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream) {
   const int st = last ? ST_KLAST : ST_KMEANS;
   RoundArgs& ra = R.ra;
   ra.it = it;
-  const double bytes_all = 4.0 * (double)R.total;
+  const double bytes_all = 3.0 * (double)R.total;   // (exact per node: finish_round)
   if (sharded) {
     timed_begin(stream);
     launch_pass(kind, ra, (int)R.ntiles, stream);
@@ -848,12 +865,24 @@ void Engine::finish_round(int ri, int max_iters, hipStream_t stream) {
     }
     return px;
   };
+  auto swept_bytes = [&](int it) {
+    double bytes = 0.0;
+    for (int a = 0; a < nl; ++a) {
+      const int di = res[a * S].done_it;
+      if (!res[a * S].proven && (di <= 0 || it < di))
+        for (int sh = 0; sh < S; ++sh) bytes += point_bytes(R.order[a]) * seg(R.order[a], sh).len;
+    }
+    return bytes;
+  };
   last_points_full += R.total * (uint64_t)((R.root ? 2 : 1) + max_iters);
   last_points_swept += R.total * (uint64_t)(R.root ? 2 : 1);
   for (int it = 0; it < max_iters; ++it) last_points_swept += swept_in(it);
   if (timing_) {
     DQ_HIP(hipStreamSynchronize(stream));
-    for (auto& e : R.km_events) pending_[e.first].bytes = 4.0 * (double)swept_in(e.second);
+    for (auto& e : R.km_events) {
+      pending_[e.first].bytes = swept_bytes(e.second);
+      pending_[e.first].units = (double)swept_in(e.second);
+    }
     collect_timing();
   }
 
@@ -1068,8 +1097,10 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
       if (sh > 0) f.n[sh - 1] = (uint32_t)b - f.first[sh - 1];
     }
     for (int sh = 0; sh < S; ++sh) {
+      // planar shards start 16-point aligned, 16 points of slack after each
+      // (the sweeps' 16-B plane loads)
       f.base[sh] = (uint32_t)total;
-      total += align4(f.n[sh]) + 4;
+      total += align16(f.n[sh]) + 16;
       const uint32_t* p = j.d_in + f.first[sh];
       if (((uintptr_t)p & 15) != 0 || (f.n[sh] & 3) != 0) align_need += align4(f.n[sh]) + 4;
     }
@@ -1595,7 +1626,7 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       timed_begin(stream);
       if (lds_map) launch_map_lds(dt, nt, kmax, nblocks, stream);
       else launch_map(dt, nt, kmax, nblocks, stream);
-      timed_end(ST_MAP, 8.0 * px, stream);
+      timed_end(ST_MAP, 8.0 * px, stream, px);
     } else {
       // rare path: run the chunk task by task, staging misaligned buffers
       for (int t = 0; t < nt; ++t) {
@@ -1628,7 +1659,7 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
         timed_end(ST_CELLS, 0.0, stream);
         timed_begin(stream);
         launch_map(dt, 1, j.k, nb, stream);
-        timed_end(ST_MAP, 8.0 * (double)j.n, stream);
+        timed_end(ST_MAP, 8.0 * (double)j.n, stream, (double)j.n);
         if (st)
           DQ_HIP(hipMemcpyAsync(j.d_out, d_map_align_ + want, (size_t)j.n * 4, hipMemcpyDeviceToDevice, stream));
       }

@@ -92,7 +92,9 @@ struct FrameJob {
 struct KernelStat {
   uint64_t launches = 0;
   double ms = 0.0;
-  double bytes = 0.0;   // algorithmic bytes (4 B per point read, +4 B written)
+  double bytes = 0.0;   // engine-model bytes (4 B per packed point read,
+                        //   3 B per planar point read or written, 8 B per mapped pixel)
+  double units = 0.0;   // points (pixels) the launches processed
 };
 enum StatKind { ST_INIT = 0, ST_SPLIT, ST_KMEANS, ST_KLAST, ST_EPILOGUE, ST_PARTITION,
                 ST_CELLS, ST_MAP, ST_PLAN, ST_COUNT };
@@ -175,6 +177,7 @@ class Engine {
       stats[i].launches += o.stats[i].launches;
       stats[i].ms += o.stats[i].ms;
       stats[i].bytes += o.stats[i].bytes;
+      stats[i].units += o.stats[i].units;
     }
     o.reset_stats();
   }
@@ -255,9 +258,12 @@ class Engine {
   void replay(FrameState& f);
   void next_active(FrameState& f, std::vector<int>* active);
   void finish_frame(FrameState& f, bool last);
-  const uint32_t* buf_ptr(int buf, const FrameState& f, int shard) const;
+  const uint8_t* buf_ptr(int buf, const FrameState& f, int shard) const;
+  // bytes a pass reads per point of a node: the caller's packed frame (a
+  // root) or the planar working buffers
+  double point_bytes(int node) const { return nodes_[node].buf == 0 ? 4.0 : 3.0; }
   void timed_begin(hipStream_t stream);
-  void timed_end(int kind, double bytes, hipStream_t stream);
+  void timed_end(int kind, double bytes, hipStream_t stream, double units = 0.0);
   void collect_timing();
 
   int device_ = 0;
@@ -353,7 +359,7 @@ class Engine {
   int comm_ranks_ = 1, comm_rank_ = 0;
   std::vector<int> slot_of_, parent_pos_;   // enqueue_host_round scratch, indexed by node id
   std::vector<FrameState> frames_;
-  struct PendingEvent { hipEvent_t a, b; int kind; double bytes; };
+  struct PendingEvent { hipEvent_t a, b; int kind; double bytes, units; };
   std::vector<PendingEvent> pending_;
   std::vector<hipEvent_t> event_pool_;
   hipEvent_t take_event();

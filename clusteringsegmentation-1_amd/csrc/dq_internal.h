@@ -50,14 +50,17 @@ struct alignas(16) Params {
 // node through its record and tiles, see PartTile).
 struct alignas(16) DevNode {
   // --- set by the host when the round starts
-  const uint32_t* src;      // element 0 of the frame (shard) in the buffer holding the node
-  uint32_t* dst;            // element 0 of the frame (shard) in the child buffer
+  const uint8_t* src;       // the frame (shard) in the buffer holding the node: element 0 of
+                            //   the caller's packed u32 frame, or byte 0 of its R plane in
+                            //   P0 / P1 (planar: G, B at + RoundArgs::plane, + 2 plane)
+  uint8_t* dst;             // byte 0 of the frame (shard)'s R plane in the child buffer
   uint32_t off, len;        // local segment, relative to src / dst
   int32_t tile_begin;       // this node's tiles are [tile_begin, tile_end) of the round
   int32_t tile_end;
   int32_t split_pb, split_pe;   // fused split: the parent's PartTiles [pb, pe) of the round
   int32_t split_side;           //   0: this node is the parent's old half, 1: the new half
-  int32_t pad0;                 //   (split_pb < 0: the node has its own split pass)
+                                //   (split_pb < 0: the node has its own split pass)
+  int32_t planar;               // src holds byte planes (0: the caller's packed frame)
   double s;                 // data_weight of the frame (get_double_scale)
   double tw;                // total_weight = weight[old_index]  (:353)
   double tm[3], tv[3];      // total_mean / total_var (root: written by PASS_INIT)

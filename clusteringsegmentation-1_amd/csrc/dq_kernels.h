@@ -49,6 +49,7 @@ struct RoundArgs {
   NodeResult* dres;         // device copy of the final results (read by the next round's plan)
   const uint32_t* counts;   // planned rounds: [tiles, part tiles, aborted] written by
                             //   plan_kernel (grids are upper bounds); nullptr: host-built
+  uint64_t plane;           // bytes between the R, G and B planes of P0 / P1
 };
 
 // A round planned on the device (plan_kernel): the children of every listed
@@ -73,9 +74,9 @@ struct PlanArgs {
   uint32_t nzero;
   uint32_t* counts;         // device: tiles, part tiles, aborted (2: overflow)
   uint32_t* hcounts;        // host-coherent mirror of counts
-  const uint32_t* p0;       // the two working buffers (a child's dst is the
-  const uint32_t* p1;       //   other one of its src)
-  uint64_t cap_px;          // words per working buffer
+  const uint8_t* p0;        // the two working buffers (a child's dst is the
+  const uint8_t* p1;        //   other one of its src)
+  uint64_t cap_bytes;       // bytes per working buffer
 };
 constexpr int kPlanMaxParents = 6144;   // parents per planned round (LDS scans)
 void launch_plan(const PlanArgs& a, hipStream_t stream);

@@ -122,33 +122,6 @@ __device__ __forceinline__ int32_t split_threshold(double cut) {
   return (int32_t)floor(cut) + 1;
 }
 
-// The 2-means decision (:683): a point stays OLD iff lhs < rr*R + rg*G + rb*B
-// (left to right, every product rounded).  Ties and NaN go NEW.
-__device__ __forceinline__ bool stays_old_exact(uint32_t p, const Params& q) {
-  const double R = (double)((p >> 16) & 0xFF);
-  const double G = (double)((p >> 8) & 0xFF);
-  const double B = (double)(p & 0xFF);
-  double d = q.rr * R;
-  d = d + q.rg * G;
-  d = d + q.rb * B;
-  return q.lhs < d;
-}
-
-__device__ __forceinline__ bool stays_old(uint32_t p, const Params& q) {
-  const float R = (float)((p >> 16) & 0xFF);
-  const float G = (float)((p >> 8) & 0xFF);
-  const float B = (float)(p & 0xFF);
-  const float df = __builtin_fmaf(q.rrf, R, __builtin_fmaf(q.rgf, G, __builtin_fmaf(q.rbf, B, -q.lhsf)));
-  const bool sure = __builtin_fabsf(df) > q.eps;
-  bool old = df > 0.0f;
-  if (!__all(sure)) {   // wave-uniform: only waves holding a near-boundary point pay FP64
-    const bool ex = stays_old_exact(p, q);
-    old = sure ? old : ex;
-  }
-  return old;
-}
-
-__device__ __forceinline__ uint32_t vec_elem(const u32x4& v, int e) { return v[e]; }
 
 // Wave w of a workgroup owns the contiguous range [ws, we) of its tile
 // [start, end): four ranges of q = ceil(len / 4096) * 1024 points (the last
@@ -163,84 +136,226 @@ __device__ __forceinline__ void wave_range(uint32_t start, uint32_t end, uint32_
   we = min(ws + q, end);
 }
 
-// This lane's kVecPerThread uint4 of the wave sweep starting at vs (16-B
-// aligned).  FULL: the whole sweep lies inside the range.  Otherwise vectors
-// starting at or past `end` are not loaded; a vector straddling `end` is
-// loaded whole -- every working buffer keeps >= 3 readable words of slack
-// past each frame.
-template <bool FULL, bool NT = false>
-__device__ __forceinline__ void load_sweep(g_cu4* src4, uint32_t vs, uint32_t end,
-                                           u32x4 v[kVecPerThread]) {
+// ---------------------------------------------------------------------------
+// Point sweeps.  The caller's frames hold packed 0x00RRGGBB words (4 B per
+// point).  The working buffers P0 / P1 hold every frame shard as three byte
+// planes R, G, B, RoundArgs::plane bytes apart (3 B per point): a partition
+// writes 3 B per point instead of 4, and every later pass reads 3.  A wave
+// sweeps kWaveSweep points at a time (16-point aligned); each lane keeps 16
+// of them byte-transposed (Sweep): word j of a channel holds the lane's slots
+// 4j .. 4j+3, slot s in byte s & 3 -- the form v_dot4_u32_u8 sums directly.
+// Where slot s of lane l lies (slot_pos):
+//   packed source (16-B loads of 4 words at vs + 4 (64 j + l)):  vs + 256 j + 4 l + e
+//   planar source (one 16-B load per plane at vs + 16 l):        vs + 16 l + s
+struct RawSweep {
+  u32x4 v[kVecPerThread];   // packed: 4 vectors of 4 words; planar: R, G, B (v[3] unused)
+};
+struct Sweep {
+  uint32_t r[kVecPerThread], g[kVecPerThread], b[kVecPerThread];
+};
+
+template <bool PLANAR>
+__device__ __forceinline__ uint32_t slot_pos(uint32_t vs, int s) {
+  return PLANAR ? vs + 16u * lane_id() + (uint32_t)s
+                : vs + 256u * (uint32_t)(s >> 2) + 4u * lane_id() + (uint32_t)(s & 3);
+}
+
+// bit s: slot s lies in [start, end)
+template <bool PLANAR>
+__device__ __forceinline__ uint32_t valid_mask(uint32_t vs, uint32_t start, uint32_t end) {
+  uint32_t m = 0;
 #pragma unroll
-  for (int j = 0; j < kVecPerThread; ++j) {
-    const uint32_t i = vs + 4u * (j * 64 + lane_id());
-    if (FULL || i < end) v[j] = NT ? __builtin_nontemporal_load(src4 + (i >> 2)) : src4[i >> 2];
-    else v[j] = (u32x4){0u, 0u, 0u, 0u};
+  for (int s = 0; s < kVecPerThread * 4; ++s)
+    m |= (uint32_t)((slot_pos<PLANAR>(vs, s) - start) < (end - start)) << s;
+  return m;
+}
+
+// This lane's loads of the sweep at vs.  FULL: the whole sweep lies inside
+// the range.  Otherwise vectors starting at or past `end` are not loaded; a
+// vector straddling `end` is loaded whole (every buffer keeps >= 16 readable
+// bytes of slack past each frame shard).  `src`: the shard's element 0 (a
+// packed frame) or its R plane (planar; G, B at + plane, + 2 plane).
+template <bool PLANAR, bool FULL, bool NT = false>
+__device__ __forceinline__ void fetch_sweep(const uint8_t* src, uint64_t plane, uint32_t vs, uint32_t end,
+                                            RawSweep& x) {
+  if (PLANAR) {
+    const uint32_t i = vs + 16u * lane_id();
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      g_cu4* p = (g_cu4*)(src + (uint64_t)c * plane + i);
+      if (FULL || i < end) x.v[c] = NT ? __builtin_nontemporal_load(p) : *p;
+      else x.v[c] = (u32x4){0u, 0u, 0u, 0u};
+    }
+  } else {
+    g_cu4* s4 = (g_cu4*)src;
+#pragma unroll
+    for (int j = 0; j < kVecPerThread; ++j) {
+      const uint32_t i = vs + 4u * (j * 64 + lane_id());
+      if (FULL || i < end) x.v[j] = NT ? __builtin_nontemporal_load(s4 + (i >> 2)) : s4[i >> 2];
+      else x.v[j] = (u32x4){0u, 0u, 0u, 0u};
+    }
   }
 }
 
-// Decision for one point of a pass (KIND) -- true: the point goes NEW.
-template <int KIND>
-__device__ __forceinline__ bool goes_new(uint32_t p, const Params& q) {
-  if (KIND == PASS_INIT) return true;
-  if (KIND == PASS_SPLIT) return (int32_t)((p >> q.shift) & 0xFF) >= q.thr;
-  return !stays_old(p, q);
+// Raw loads -> channel words (packed: 5 v_perm_b32 per 4 points).
+template <bool PLANAR>
+__device__ __forceinline__ void unpack_sweep(const RawSweep& x, Sweep& w) {
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    if (PLANAR) {
+      w.r[j] = x.v[0][j];
+      w.g[j] = x.v[1][j];
+      w.b[j] = x.v[2][j];
+    } else {
+      const u32x4 m = x.v[j];
+      const uint32_t u01 = __builtin_amdgcn_perm(m[1], m[0], 0x05010400u);  // B0 B1 G0 G1
+      const uint32_t u23 = __builtin_amdgcn_perm(m[3], m[2], 0x05010400u);  // B2 B3 G2 G3
+      w.b[j] = __builtin_amdgcn_perm(u23, u01, 0x05040100u);                // B0 B1 B2 B3
+      w.g[j] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);                // G0 G1 G2 G3
+      w.r[j] = __builtin_amdgcn_perm(m[1], m[0], 0x0C0C0602u) |             // R0 R1 0 0
+               __builtin_amdgcn_perm(m[3], m[2], 0x06020C0Cu);              // 0 0 R2 R3
+    }
+  }
 }
 
-// Lane partial sums of the new side: count, sums and sums of squares of the
-// three channels (a lane sees at most 256 points of a tile: all exact in u32).
-// Four masked pixels (0 when not taken) are byte-transposed with v_perm_b32
-// into one R, one G and one B word, then v_dot4_u32_u8 with 0x01010101 sums
-// them and with themselves sums their squares: 7 sums for ~5 ops per point.
-struct LaneSums {
-  uint32_t cnt = 0, sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
-  uint32_t vcnt = 0;   // points of the lane inside the tile (partition cursors)
-};
+__device__ __forceinline__ uint32_t chan_byte(uint32_t w, int s) { return (w >> (8 * (s & 3))) & 0xFFu; }
 
-__device__ __forceinline__ void add4(const uint32_t m[4], LaneSums& s) {
-  const uint32_t u01 = __builtin_amdgcn_perm(m[1], m[0], 0x05010400u);  // B0 B1 G0 G1
-  const uint32_t u23 = __builtin_amdgcn_perm(m[3], m[2], 0x05010400u);  // B2 B3 G2 G3
-  const uint32_t bq = __builtin_amdgcn_perm(u23, u01, 0x05040100u);     // B0 B1 B2 B3
-  const uint32_t gq = __builtin_amdgcn_perm(u23, u01, 0x07060302u);     // G0 G1 G2 G3
-  const uint32_t rq = __builtin_amdgcn_perm(m[1], m[0], 0x0C0C0602u) |  // R0 R1 0 0
-                      __builtin_amdgcn_perm(m[3], m[2], 0x06020C0Cu);   // 0 0 R2 R3
-  s.sr = __builtin_amdgcn_udot4(rq, 0x01010101u, s.sr, false);
-  s.sg = __builtin_amdgcn_udot4(gq, 0x01010101u, s.sg, false);
-  s.sb = __builtin_amdgcn_udot4(bq, 0x01010101u, s.sb, false);
-  s.qr = __builtin_amdgcn_udot4(rq, rq, s.qr, false);
-  s.qg = __builtin_amdgcn_udot4(gq, gq, s.qg, false);
-  s.qb = __builtin_amdgcn_udot4(bq, bq, s.qb, false);
+// Slots whose byte on the cut axis (shift 16: R, 8: G, 0: B) is >= thr: the
+// split pass's NEW side (cut_pos < v_axis, :438-559).  thr in [0, 256].
+__device__ __forceinline__ uint32_t cut_new_mask(const Sweep& w, uint32_t shift, int32_t thr) {
+  // the axis words by two v_perm_b32 with uniform selectors (a select of the
+  // channel arrays becomes an indexed access through scratch memory)
+  const uint32_t s1 = shift == 8u ? 0x07060504u : 0x03020100u, s2 = shift == 0u ? 0x07060504u : 0x03020100u;
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    const uint32_t x = __builtin_amdgcn_perm(w.b[j], __builtin_amdgcn_perm(w.g[j], w.r[j], s1), s2);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      m |= ((uint32_t)(thr - 1 - (int32_t)chan_byte(x, e)) >> 31) << (4 * j + e);
+  }
+  return m;
 }
 
-// The split pass's new side: count, sums (:438-559) and sums of squares (the
-// results of a split proven final at its epilogue, cut_is_fixed_point).
+// The 2-means decision (:683) for every slot: bit s of the result = slot s
+// stays OLD.  FP32 filter in 32-bit integer arithmetic (no 64-bit compare
+// masks): with a finite eps, df is finite, sign(df) > 0 <=> -bits(df) has
+// bit 31 set (a -0 result has |df| <= eps and takes the exact path), and
+// |df| <= eps <=> bits(|df|) - bits(eps) - 1 has bit 31 set.  Valid slots the
+// filter cannot decide (every slot, when the node's filter is off) take the
+// exact FP64 expression; that branch is wave-uniform.
+__device__ __forceinline__ bool stays_old_exact3(uint32_t r, uint32_t g, uint32_t b, const Params& q) {
+  const double R = (double)r, G = (double)g, B = (double)b;
+  double d = q.rr * R;
+  d = d + q.rg * G;
+  d = d + q.rb * B;
+  return q.lhs < d;
+}
+
+__device__ __forceinline__ uint32_t old_mask(const Sweep& w, uint32_t validm, const Params& q, bool exact_all) {
+  const uint32_t epsb = __float_as_uint(q.eps);
+  uint32_t om = 0;
+  // 4 slots (one channel word) at a time, each group's FP64 fallback before
+  // the next group: live ranges stay at one group's
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    uint32_t o4 = 0, u4 = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float R = (float)chan_byte(w.r[j], e), G = (float)chan_byte(w.g[j], e), B = (float)chan_byte(w.b[j], e);
+      const float df = __builtin_fmaf(q.rrf, R, __builtin_fmaf(q.rgf, G, __builtin_fmaf(q.rbf, B, -q.lhsf)));
+      const uint32_t db = __float_as_uint(df);
+      o4 |= ((0u - db) >> 31) << e;
+      u4 |= (((db & 0x7FFFFFFFu) - epsb - 1u) >> 31) << e;
+    }
+    if (exact_all) u4 = 0xFu;
+    u4 &= (validm >> (4 * j)) & 0xFu;
+    if (__any(u4 != 0)) {   // wave-uniform
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (__any((u4 >> e) & 1u)) {
+          const bool ex = stays_old_exact3(chan_byte(w.r[j], e), chan_byte(w.g[j], e), chan_byte(w.b[j], e), q);
+          if ((u4 >> e) & 1u) o4 = (o4 & ~(1u << e)) | ((ex ? 1u : 0u) << e);
+        }
+      }
+    }
+    om |= o4 << (4 * j);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return om & validm;
+}
+
+// Lane partial sums: count, sums and sums of squares of the three channels
+// over the slots of a mask (a lane sees at most 256 points of a tile: all
+// exact in u32).  Per 4 slots the mask becomes 0/1 byte weights (4 bits *
+// 0x204081 puts bit i at bit 8i), then v_dot4_u32_u8 of each channel word
+// with the weights gives its sum, and of the masked word with itself its
+// sum of squares.
 struct SplitSums {
   uint32_t cnt = 0, sr = 0, sg = 0, sb = 0, qr = 0, qg = 0, qb = 0;
 };
+struct LaneSums : SplitSums {
+  uint32_t vcnt = 0;   // points of the lane inside the tile (partition cursors)
+};
 
-
-template <int KIND, bool FULL>
-__device__ __forceinline__ void sweep_sums(const u32x4 v[kVecPerThread], uint32_t vs,
-                                           uint32_t start, uint32_t end, const Params& q,
-                                           LaneSums& s) {
-  if (FULL) s.vcnt += kVecPerThread * 4;
+template <bool ALL = false>
+__device__ __forceinline__ void add_sums(const Sweep& w, uint32_t m, SplitSums& s) {
+  s.cnt += ALL ? (uint32_t)(kVecPerThread * 4) : (uint32_t)__builtin_popcount(m);
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
-    const uint32_t i0 = vs + 4u * (j * 64 + lane_id());
-    uint32_t m[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t p = vec_elem(v[j], e);
-      bool take = goes_new<KIND>(p, q);
-      if (!FULL) {
-        const bool valid = (i0 + e - start) < (end - start);
-        take = take && valid;
-        s.vcnt += valid ? 1u : 0u;
-      }
-      m[e] = take ? p : 0u;
-      s.cnt += take ? 1u : 0u;
+    const uint32_t wt = ALL ? 0x01010101u : ((((m >> (4 * j)) & 0xFu) * 0x204081u) & 0x01010101u);
+    const uint32_t mk = wt * 0xFFu;
+    s.sr = __builtin_amdgcn_udot4(w.r[j], wt, s.sr, false);
+    s.sg = __builtin_amdgcn_udot4(w.g[j], wt, s.sg, false);
+    s.sb = __builtin_amdgcn_udot4(w.b[j], wt, s.sb, false);
+    s.qr = __builtin_amdgcn_udot4(w.r[j] & mk, w.r[j], s.qr, false);
+    s.qg = __builtin_amdgcn_udot4(w.g[j] & mk, w.g[j], s.qg, false);
+    s.qb = __builtin_amdgcn_udot4(w.b[j] & mk, w.b[j], s.qb, false);
+  }
+}
+
+// One sweep of a statistics pass: the NEW side's sums (PASS_INIT: every point).
+template <int KIND, bool PLANAR, bool FULL>
+__device__ __forceinline__ void sweep_sums(const Sweep& w, uint32_t vs, uint32_t start, uint32_t end,
+                                           const Params& q, bool exact_all, LaneSums& s) {
+  const uint32_t vm = FULL ? 0xFFFFu : valid_mask<PLANAR>(vs, start, end);
+  s.vcnt += FULL ? (uint32_t)(kVecPerThread * 4) : (uint32_t)__builtin_popcount(vm);
+  if (KIND == PASS_INIT) {
+    if (FULL) add_sums<true>(w, vm, s);
+    else add_sums(w, vm, s);
+  } else if (KIND == PASS_SPLIT) {
+    add_sums(w, vm & cut_new_mask(w, (uint32_t)q.shift, q.thr), s);
+  } else {
+    add_sums(w, vm & ~old_mask(w, vm, q, exact_all), s);
+  }
+}
+
+// A wave's sweeps over [ws, we) of a pass (pass_kernel, kpass_kernel), the
+// next sweep's loads issued before this sweep's arithmetic.
+template <int KIND, bool PLANAR>
+__device__ __forceinline__ void wave_pass(const uint8_t* src, uint64_t plane, uint32_t ws, uint32_t we,
+                                          const Params& q, LaneSums& s) {
+  const bool exact_all = !(q.eps < __builtin_inff());   // FP32 filter off for this node
+  uint32_t vs = ws & ~15u;
+  bool full = vs >= ws && vs + kWaveSweep <= we;
+  RawSweep x;
+  if (vs < we) {
+    if (full) fetch_sweep<PLANAR, true>(src, plane, vs, we, x);
+    else fetch_sweep<PLANAR, false>(src, plane, vs, we, x);
+  }
+  while (vs < we) {
+    Sweep w;
+    unpack_sweep<PLANAR>(x, w);
+    const uint32_t nvs = vs + kWaveSweep;
+    const bool nfull = nvs + kWaveSweep <= we;
+    if (nvs < we) {
+      if (nfull) fetch_sweep<PLANAR, true>(src, plane, nvs, we, x);
+      else fetch_sweep<PLANAR, false>(src, plane, nvs, we, x);
     }
-    add4(m, s);
+    if (full) sweep_sums<KIND, PLANAR, true>(w, vs, ws, we, q, exact_all, s);
+    else sweep_sums<KIND, PLANAR, false>(w, vs, ws, we, q, exact_all, s);
+    vs = nvs;
+    full = nfull;
   }
 }
 
@@ -374,29 +489,24 @@ __device__ bool node_update(DevNode* w, NodeResult* r, const uint64_t t[F_NUM], 
 // segment, so every point of the workgroup shares the node's parameters and
 // the sums need no per-point binning: packed lane partials -> wave sums ->
 // LDS -> one 32-B partial per tile.
+// Waves per SIMD the pass kernels are compiled for (VGPR budget 512 / n).
+#ifndef DQ_PASS_WAVES
+#define DQ_PASS_WAVES 4
+#endif
 template <int KIND>
-__global__ __launch_bounds__(kBlock) void pass_kernel(RoundArgs a) {
+__global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void pass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const DevNode& nd = a.nodes[t.node];
   if ((KIND == PASS_KMEANS || KIND == PASS_KLAST) && nd.done_it != 0) return;   // final
-  g_cu4* src4 = as_g4(nd.src);
   const Params q = nd.prm;
   constexpr int kNF = F_NUM;
 
   __shared__ uint32_t red[kBlock / 64][8];
   LaneSums s;
-  u32x4 v[kVecPerThread];
   uint32_t ws, we;
   wave_range(t.start, t.end, wave_id(), ws, we);
-  for (uint32_t vs = ws & ~3u; vs < we; vs += kWaveSweep) {
-    if (vs >= ws && vs + kWaveSweep <= we) {   // wave-uniform
-      load_sweep<true>(src4, vs, we, v);
-      sweep_sums<KIND, true>(v, vs, ws, we, q, s);
-    } else {
-      load_sweep<false>(src4, vs, we, v);
-      sweep_sums<KIND, false>(v, vs, ws, we, q, s);
-    }
-  }
+  if (nd.planar) wave_pass<KIND, true>(nd.src, a.plane, ws, we, q, s);
+  else wave_pass<KIND, false>(nd.src, a.plane, ws, we, q, s);
 
   uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
 #pragma unroll
@@ -778,7 +888,7 @@ __device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int rec
 }
 
 template <int KIND>
-__global__ __launch_bounds__(kBlock) void kpass_kernel(RoundArgs a) {
+__global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void kpass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const int rec = t.node;
   const DevNode& nd = a.nodes[rec];
@@ -787,24 +897,15 @@ __global__ __launch_bounds__(kBlock) void kpass_kernel(RoundArgs a) {
       arrive(a.ctr + a.it, (uint32_t)rec, (uint32_t)a.nn, false, a.hstat + a.it, a.seq);
     return;
   }
-  g_cu4* src4 = as_g4(nd.src);
   const Params q = nd.prm;
   __shared__ uint32_t red[kBlock / 64][8];
   __shared__ int slast;
   __shared__ NodeResult sres;
   LaneSums s;
-  u32x4 v[kVecPerThread];
   uint32_t ws, we;
   wave_range(t.start, t.end, wave_id(), ws, we);
-  for (uint32_t vs = ws & ~3u; vs < we; vs += kWaveSweep) {
-    if (vs >= ws && vs + kWaveSweep <= we) {   // wave-uniform
-      load_sweep<true>(src4, vs, we, v);
-      sweep_sums<KIND, true>(v, vs, ws, we, q, s);
-    } else {
-      load_sweep<false>(src4, vs, we, v);
-      sweep_sums<KIND, false>(v, vs, ws, we, q, s);
-    }
-  }
+  if (nd.planar) wave_pass<KIND, true>(nd.src, a.plane, ws, we, q, s);
+  else wave_pass<KIND, false>(nd.src, a.plane, ws, we, q, s);
   uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
 #pragma unroll
   for (int k = 0; k < F_NUM; ++k) f[k] = wave_sum_u32(f[k]);
@@ -828,77 +929,6 @@ __global__ __launch_bounds__(kBlock) void kpass_kernel(RoundArgs a) {
                                    __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(nd.tile_end - nd.tile_begin) - 1;
   __syncthreads();
   if (slast && wave_id() == 0) kmeans_epilogue_wave<KIND>(a, rec, &sres);
-}
-
-// The 2-means decisions of one sweep as lane bit masks: bit s of oldm = slot
-// s stays OLD (:683), bit s of validm = slot s lies inside [start, end).
-// FP32 filter in 32-bit integer arithmetic (no 64-bit compare masks): with a
-// finite eps, df is finite, sign(df) > 0 <=> -bits(df) has bit 31 set (a -0
-// result has |df| <= eps and takes the exact path), and |df| <= eps <=>
-// bits(|df|) - bits(eps) - 1 has bit 31 set.  Points the filter cannot decide
-// (or every point, when the node's filter is off) take the exact FP64
-// expression; that branch is wave-uniform.
-template <bool FULL>
-__device__ __forceinline__ void decide_sweep(const u32x4 v[kVecPerThread], uint32_t vs,
-                                             uint32_t start, uint32_t end, const Params& q,
-                                             bool exact_all, uint32_t& oldm, uint32_t& validm) {
-  constexpr int kSlots = kVecPerThread * 4;
-  uint32_t om = 0, un = 0, vm = FULL ? 0xFFFFu : 0u;
-  const uint32_t epsb = __float_as_uint(q.eps);
-#pragma unroll
-  for (int j = 0; j < kVecPerThread; ++j) {
-    const uint32_t i0 = vs + 4u * (j * 64 + lane_id());
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int sidx = j * 4 + e;
-      const uint32_t p = vec_elem(v[j], e);
-      const float R = (float)((p >> 16) & 0xFF);
-      const float G = (float)((p >> 8) & 0xFF);
-      const float B = (float)(p & 0xFF);
-      const float df = __builtin_fmaf(q.rrf, R, __builtin_fmaf(q.rgf, G, __builtin_fmaf(q.rbf, B, -q.lhsf)));
-      const uint32_t db = __float_as_uint(df);
-      om |= ((0u - db) >> 31) << sidx;
-      un |= (((db & 0x7FFFFFFFu) - epsb - 1u) >> 31) << sidx;
-      if (!FULL) {
-        const uint32_t i = i0 + e;
-        vm |= ((uint32_t)((i - start) < (end - start))) << sidx;
-      }
-    }
-  }
-  if (exact_all) un = 0xFFFFu;
-  if (__any(un != 0)) {
-#pragma unroll
-    for (int sidx = 0; sidx < kSlots; ++sidx) {
-      if ((un >> sidx) & 1u) {
-        const bool ex = stays_old_exact(vec_elem(v[sidx >> 2], sidx & 3), q);
-        om = (om & ~(1u << sidx)) | ((ex ? 1u : 0u) << sidx);
-      }
-    }
-  }
-  oldm = om & vm;
-  validm = vm;
-}
-
-// The same masks for a node whose final decision is its cut (DevNode::
-// proven): OLD iff byte < thr.
-template <bool FULL>
-__device__ __forceinline__ void cut_sweep(const u32x4 v[kVecPerThread], uint32_t vs, uint32_t start,
-                                          uint32_t end, uint32_t shift, int32_t thr,
-                                          uint32_t& oldm, uint32_t& validm) {
-  uint32_t om = 0, vm = FULL ? 0xFFFFu : 0u;
-#pragma unroll
-  for (int j = 0; j < kVecPerThread; ++j) {
-    const uint32_t i0 = vs + 4u * (j * 64 + lane_id());
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int sidx = j * 4 + e;
-      const uint32_t b = (vec_elem(v[j], e) >> shift) & 0xFFu;
-      om |= ((uint32_t)((int32_t)b - thr) >> 31) << sidx;
-      if (!FULL) vm |= ((uint32_t)((i0 + e - start) < (end - start))) << sidx;
-    }
-  }
-  oldm = om & vm;
-  validm = vm;
 }
 
 // ---------------------------------------------------------------------------
@@ -1012,15 +1042,10 @@ __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
   if (v != 0 && lane_id() == 0) atomicAdd(c.w0 + c.k * kTileWaves + c.w, v);
 }
 
-// Occupancy / double-buffering of partsplit (measured per 8 x 4K round,
-// tools/prof_variants.sh): 3 waves/SIMD with the next sweep's loads in
-// flight 137.8 us; 4 waves/SIMD (<= 128 VGPRs) with prefetch 126.7 us,
-// without 124.1 us; 5 waves spills VGPRs (182 us).
+// Occupancy of partsplit: 4 waves per SIMD (LDS staging 25 KB per
+// workgroup, <= 128 VGPRs).
 #ifndef DQ_PS_WAVES
 #define DQ_PS_WAVES 4
-#endif
-#ifndef DQ_PS_PREFETCH
-#define DQ_PS_PREFETCH 0
 #endif
 // Cache policy of partsplit's streams (a parent's points are read once, its
 // children's written once): nontemporal loads, store cache-policy bits
@@ -1030,178 +1055,353 @@ __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
 #ifndef DQ_PS_STORE_AUX
 #define DQ_PS_STORE_AUX 0
 #endif
-// This wave's points of one sweep, slot by slot, ranked by ballot; raw
-// buffer stores (SGPR descriptor + 32-bit offset).  In a full sweep every
-// slot is valid: a lane's rank among the new points is its lane id minus
-// its rank among the old ones (one ballot, one mbcnt pair).  Partial sweeps:
-// out-of-range offsets are dropped by the buffer bounds check, so invalid
-// slots get one.  PRE: also count, per lane, the children's split-new points
-// written below the child's chunk end (ex / ey).
-template <bool PRE>
-__device__ __forceinline__ void store_sweep(const u32x4 v[kVecPerThread], uint32_t oldm, uint32_t newm,
-                                            bool full, __amdgpu_buffer_rsrc_t drs, uint32_t l,
-                                            uint32_t xcut, uint32_t ycut, uint32_t& oc, uint32_t& nc,
-                                            uint32_t ex, uint32_t ey, uint32_t& ax, uint32_t& ay) {
-  constexpr int kSlots = kVecPerThread * 4;
-  if (full) {
+
+// partsplit works on byte masks: word j of a SweepMask holds 0x01 in byte e
+// iff slot 4j + e is in the set -- the 0/1 byte weights v_dot4 sums with,
+// and what the SWAR cut comparison produces (partsplit was VALU-bound with
+// per-slot bit masks: ~69 VALU per point, the cuts alone 19).
+struct SweepMask {
+  uint32_t m[kVecPerThread];
+};
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+
+// Bytes of x that are >= thr, as 0x01 bytes; k = (256 - thr) * 0x00010001,
+// thr in [0, 256].  Bytes 0, 2 and 1, 3 spread into 16-bit lanes; b + 256 -
+// thr < 512 sets bit 8 iff b >= thr.
+__device__ __forceinline__ uint32_t ge_bytes(uint32_t x, uint32_t k) {
+  const uint32_t lo = pk_add_u16(__builtin_amdgcn_perm(0u, x, 0x0C020C00u), k);   // b0, b2
+  const uint32_t hi = pk_add_u16(__builtin_amdgcn_perm(0u, x, 0x0C030C01u), k);   // b1, b3
+  return __builtin_amdgcn_perm(hi, lo, 0x07030501u) & 0x01010101u;
+}
+
+// Word j of the cut axis' channel (shift 16: R, 8: G, 0: B) by two v_perm_b32
+// with uniform selectors (a select between the channel arrays is compiled as
+// an indexed access through scratch memory).
+__device__ __forceinline__ uint32_t axis_word(const Sweep& w, int j, uint32_t shift) {
+  const uint32_t s1 = shift == 8u ? 0x07060504u : 0x03020100u;   // R or G
+  const uint32_t s2 = shift == 0u ? 0x07060504u : 0x03020100u;   // that or B
+  return __builtin_amdgcn_perm(w.b[j], __builtin_amdgcn_perm(w.g[j], w.r[j], s1), s2);
+}
+
+// Slots whose byte on the cut axis is >= thr: the split pass's NEW side.
+__device__ __forceinline__ SweepMask cut_new_bytes(const Sweep& w, uint32_t shift, int32_t thr) {
+  const uint32_t k = (uint32_t)(256 - thr) * 0x00010001u;
+  SweepMask m;
 #pragma unroll
-    for (int sidx = 0; sidx < kSlots; ++sidx) {
-      const bool o = (oldm >> sidx) & 1u;
+  for (int j = 0; j < kVecPerThread; ++j) m.m[j] = ge_bytes(axis_word(w, j, shift), k);
+  return m;
+}
+
+__device__ __forceinline__ SweepMask bits_to_bytes(uint32_t b16) {
+  SweepMask m;
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) m.m[j] = ((((b16 >> (4 * j)) & 0xFu) * 0x204081u) & 0x01010101u);
+  return m;
+}
+
+__device__ __forceinline__ bool slot_in(const SweepMask& m, int s) {
+  return ((m.m[s >> 2] >> (8 * (s & 3))) & 0xFFu) != 0u;
+}
+
+__device__ __forceinline__ uint32_t mask_count(const SweepMask& m) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) c += (uint32_t)__builtin_popcount(m.m[j]);
+  return c;
+}
+
+// Count, sums and sums of squares over the slots of a byte mask.
+__device__ __forceinline__ void add_sums_bytes(const Sweep& w, const SweepMask& m, SplitSums& s) {
+  s.cnt += mask_count(m);
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    const uint32_t wt = m.m[j], mk = (wt << 8) - wt;   // 0x01 -> 0xFF per byte
+    s.sr = __builtin_amdgcn_udot4(w.r[j], wt, s.sr, false);
+    s.sg = __builtin_amdgcn_udot4(w.g[j], wt, s.sg, false);
+    s.sb = __builtin_amdgcn_udot4(w.b[j], wt, s.sb, false);
+    s.qr = __builtin_amdgcn_udot4(w.r[j] & mk, w.r[j], s.qr, false);
+    s.qg = __builtin_amdgcn_udot4(w.g[j] & mk, w.g[j], s.qg, false);
+    s.qb = __builtin_amdgcn_udot4(w.b[j] & mk, w.b[j], s.qb, false);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-staged stores: a wave writes each sweep's points as bytes into its own
+// LDS staging -- per plane, one region per run (old / new) whose byte i is
+// the child position cb + i, cb the 16-B aligned start of the run's first
+// unwritten chunk -- then stores every completed 16-B chunk with one
+// buffer_store_dwordx4 per plane and moves the partial last chunk to the
+// front.  Versus one byte store per point and plane this cuts the vector-
+// memory instructions of a sweep from 48 to ~3-6 (the address unit bounded
+// the byte-store form: TA busy 81 %).  A chunk holding the run's first
+// position (shared with the neighbouring wave's run) and the run's last
+// partial chunk are written byte by byte.
+constexpr uint32_t kStageRun = 1056;                // bytes per (wave, plane, run): 15 + 1024 + slack
+constexpr uint32_t kStagePlane = 2 * kStageRun;     // old region, new region
+constexpr uint32_t kStageWave = 3 * kStagePlane;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct PlaneRsrc {
+  __amdgpu_buffer_rsrc_t r, g, b;
+};
+
+// A wave's two runs (wave-uniform): child position of staging byte 0, the
+// next staging byte (the new run's region starts at kStageRun), the wave's
+// first position.  The run's next child position is cb + p (- kStageRun).
+struct Stage {
+  uint32_t cbo, cbn, po, pn, loo, lon;
+};
+
+// This wave's points of one sweep into the staging, slot by slot, ranked by
+// ballot (a full sweep: a lane's rank among the new points is its lane id
+// minus its rank among the old ones).  PRE: also count, per lane, the
+// children's split-new points (xm / ym) at child positions below ex / ey.
+template <bool PRE>
+__device__ __forceinline__ void stage_sweep(const Sweep& w, const SweepMask& om, const SweepMask& nm, bool full,
+                                            uint8_t* st, Stage& g, uint32_t l, const SweepMask& xm,
+                                            const SweepMask& ym, uint32_t ex, uint32_t ey, uint32_t& ax,
+                                            uint32_t& ay) {
+  constexpr int kSlots = kVecPerThread * 4;
+  // PRE thresholds relative to the regions (ex >= cbo, ey >= cbn: chunk ends
+  // at or past the runs' next positions, or ~0)
+  const uint32_t exs = ex - g.cbo, eys = ey - g.cbn;
+  auto put = [&](int s, uint32_t lp) {
+    const int j = s >> 2, sh = 8 * (s & 3);
+    st[lp] = (uint8_t)(w.r[j] >> sh);
+    st[kStagePlane + lp] = (uint8_t)(w.g[j] >> sh);
+    st[2 * kStagePlane + lp] = (uint8_t)(w.b[j] >> sh);
+    if (PRE) {
+      ax += (uint32_t)(slot_in(xm, s) && lp < exs);
+      ay += (uint32_t)(slot_in(ym, s) && lp - kStageRun < eys);
+    }
+  };
+  if (full) {   // (wave-uniform)
+    const uint32_t po0 = g.po;
+    uint32_t t = g.pn + l;
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      const bool o = slot_in(om, s);
       const uint64_t bo = __ballot(o);
       const uint32_t ro = mbcnt64(bo);
-      const uint32_t idx = o ? oc + ro : nc + (l - ro);
-      __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
-                                            (int)(idx * 4u), 0, DQ_PS_STORE_AUX);
-      if (PRE) {
-        ax += (xcut >> sidx) & (uint32_t)(idx < ex);
-        ay += (ycut >> sidx) & (uint32_t)(idx < ey) & 1u;
-      }
+      put(s, o ? g.po + ro : t - ro);
       const uint32_t co = (uint32_t)__popcll(bo);
-      oc += co;
-      nc += 64u - co;
+      g.po += co;
+      t += 64u - co;
     }
+    g.pn += (uint32_t)kWaveSweep - (g.po - po0);   // every slot valid: old + new = 1024
   } else {
 #pragma unroll
-    for (int sidx = 0; sidx < kSlots; ++sidx) {
-      const bool o = (oldm >> sidx) & 1u, n = (newm >> sidx) & 1u;
+    for (int s = 0; s < kSlots; ++s) {
+      const bool o = slot_in(om, s), n = slot_in(nm, s);
       const uint64_t bo = __ballot(o), bn = __ballot(n);
-      uint32_t idx = o ? oc + mbcnt64(bo) : nc + mbcnt64(bn);
-      idx = (o || n) ? idx : 0x3FFFFFFFu;
-      __builtin_amdgcn_raw_buffer_store_b32(vec_elem(v[sidx >> 2], sidx & 3), drs,
-                                            (int)(idx * 4u), 0, DQ_PS_STORE_AUX);
-      if (PRE) {
-        ax += (xcut >> sidx) & (uint32_t)(idx < ex);
-        ay += (ycut >> sidx) & (uint32_t)(idx < ey) & 1u;
-      }
-      oc += (uint32_t)__popcll(bo);
-      nc += (uint32_t)__popcll(bn);
+      if (o || n) put(s, o ? g.po + mbcnt64(bo) : g.pn + mbcnt64(bn));
+      g.po += (uint32_t)__popcll(bo);
+      g.pn += (uint32_t)__popcll(bn);
     }
   }
+}
+
+// Lanes 0-15 / 16-31 write the staged bytes i of the old / new run's first
+// chunk whose child positions lie in [max(cb, lo), hi).
+__device__ __forceinline__ void stage_bytes(const uint8_t* st, const PlaneRsrc& d, const Stage& g,
+                                            uint32_t hi_o, uint32_t hi_n, uint32_t l) {
+  const uint32_t run = (l >> 4) & 1u, i = l & 15u;
+  const uint32_t pos = (run ? g.cbn : g.cbo) + i;
+  const uint32_t lo = run ? g.lon : g.loo, hi = run ? hi_n : hi_o;
+  if (l < 32u && pos >= lo && pos < hi) {
+    const uint32_t lp = run * kStageRun + i;
+    __builtin_amdgcn_raw_buffer_store_b8(st[lp], d.r, (int)pos, 0, DQ_PS_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b8(st[kStagePlane + lp], d.g, (int)pos, 0, DQ_PS_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b8(st[2 * kStagePlane + lp], d.b, (int)pos, 0, DQ_PS_STORE_AUX);
+  }
+}
+
+// After a sweep: the completed chunks of both runs, then the partial chunks
+// moved to the front of their regions.
+__device__ __forceinline__ void stage_flush(uint8_t* st, const PlaneRsrc& d, Stage& g, uint32_t l) {
+  wave_lds_sync();
+  const uint32_t nfo = g.po >> 4, nfn = (g.pn - kStageRun) >> 4;
+  for (uint32_t q = l; q < nfo + nfn; q += 64u) {
+    const bool run = q >= nfo;
+    const uint32_t k16 = 16u * (run ? q - nfo : q);
+    const uint32_t pos = (run ? g.cbn : g.cbo) + k16;
+    const uint32_t lp = (run ? kStageRun : 0u) + k16;
+    if (pos >= (run ? g.lon : g.loo)) {
+      const u32x4 vr = *reinterpret_cast<const u32x4*>(st + lp);
+      const u32x4 vg = *reinterpret_cast<const u32x4*>(st + kStagePlane + lp);
+      const u32x4 vb = *reinterpret_cast<const u32x4*>(st + 2 * kStagePlane + lp);
+      __builtin_amdgcn_raw_buffer_store_b128(vr, d.r, (int)pos, 0, DQ_PS_STORE_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(vg, d.g, (int)pos, 0, DQ_PS_STORE_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(vb, d.b, (int)pos, 0, DQ_PS_STORE_AUX);
+    }
+  }
+  // a completed first chunk that starts below the wave's first position
+  const uint32_t ho = (nfo > 0u && g.cbo < g.loo) ? g.cbo + 16u : 0u;
+  const uint32_t hn = (nfn > 0u && g.cbn < g.lon) ? g.cbn + 16u : 0u;
+  if (ho | hn) stage_bytes(st, d, g, ho, hn, l);
+  if (nfo | nfn) {   // the partial chunks to the front
+    const uint32_t run = (l >> 4) & 1u, i = l & 15u;
+    const uint32_t nf = run ? nfn : nfo;
+    const uint32_t src = (run ? kStageRun : 0u) + 16u * nf + i;
+    const bool mv = l < 32u && nf > 0u;
+    uint8_t cr = 0, cg = 0, cb = 0;
+    wave_lds_sync();
+    if (mv) {
+      cr = st[src];
+      cg = st[kStagePlane + src];
+      cb = st[2 * kStagePlane + src];
+    }
+    wave_lds_sync();
+    if (mv) {
+      const uint32_t dst = (run ? kStageRun : 0u) + i;
+      st[dst] = cr;
+      st[kStagePlane + dst] = cg;
+      st[2 * kStagePlane + dst] = cb;
+    }
+    g.cbo += 16u * nfo;
+    g.po -= 16u * nfo;
+    g.cbn += 16u * nfn;
+    g.pn -= 16u * nfn;
+  }
+  wave_lds_sync();
+}
+
+// The kernel's loop for one source format of the parent.
+// (records and tiles through global-address-space views: generic pointers
+// read from a PartTile made these flat loads)
+typedef const __attribute__((address_space(1))) DevNode g_cnode;
+typedef const __attribute__((address_space(1))) Tile g_ctile;
+template <bool PLANAR>
+__device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g_ctile* tp,
+                                              const DevNode* nodes, uint32_t* wparts, uint64_t plane,
+                                              uint8_t* st, SplitSums& so, SplitSums& sn) {
+  const uint32_t w = wave_id(), l = lane_id();
+  uint32_t start, end;   // this wave's range of the parent tile (wave-uniform)
+  wave_range(__builtin_amdgcn_readfirstlane(tp->start), __builtin_amdgcn_readfirstlane(tp->end), w, start, end);
+  // the child's planes of the frame shard: every index < off + len < 2^30
+  const int nrec = (int)(nd.off + nd.len);
+  PlaneRsrc d;
+  d.r = __builtin_amdgcn_make_buffer_rsrc(nd.dst, (short)0, nrec, 0x00020000);
+  d.g = __builtin_amdgcn_make_buffer_rsrc(nd.dst + plane, (short)0, nrec, 0x00020000);
+  d.b = __builtin_amdgcn_make_buffer_rsrc(nd.dst + 2 * plane, (short)0, nrec, 0x00020000);
+  Params q;   // (field by field: an address-space-qualified struct has no copy for the host pass)
+  q.lhs = nd.prm.lhs;
+  q.rr = nd.prm.rr;
+  q.rg = nd.prm.rg;
+  q.rb = nd.prm.rb;
+  q.lhsf = nd.prm.lhsf;
+  q.rrf = nd.prm.rrf;
+  q.rgf = nd.prm.rgf;
+  q.rbf = nd.prm.rbf;
+  q.eps = nd.prm.eps;
+  q.thr = nd.prm.thr;
+  q.shift = nd.prm.shift;
+  q.pad = 0;
+  const uint32_t n_old = nd.len - nd.n_new_local;
+  const uint32_t oc0 = nd.off + tp->old_base[w];
+  const uint32_t nc0 = nd.off + n_old + tp->new_base[w];
+  const bool exact_all = !(q.eps < __builtin_inff());   // FP32 filter off for this node
+  const bool cut = nd.proven != 0;
+  const uint32_t sh0 = (uint32_t)pt.shift[0], sh1 = (uint32_t)pt.shift[1];
+  const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
+  ChunkAcc cx, cy;
+  chunk_init(cx, nodes, wparts, pt.child[0], oc0);
+  chunk_init(cy, nodes, wparts, pt.child[1], nc0);
+  Stage g;
+  g.cbo = oc0 & ~15u;
+  g.po = oc0 & 15u;
+  g.loo = oc0;
+  g.cbn = nc0 & ~15u;
+  g.pn = kStageRun + (nc0 & 15u);
+  g.lon = nc0;
+
+  RawSweep x;
+  uint32_t vs = start & ~15u;
+  bool full = vs >= start && vs + kWaveSweep <= end;
+  if (vs < end) {
+    if (full) fetch_sweep<PLANAR, true, DQ_PS_NTLOAD>(nd.src, plane, vs, end, x);
+    else fetch_sweep<PLANAR, false, DQ_PS_NTLOAD>(nd.src, plane, vs, end, x);
+  }
+  while (vs < end) {
+    Sweep sw;
+    unpack_sweep<PLANAR>(x, sw);
+    const uint32_t nvs = vs + kWaveSweep;
+    const bool nfull = nvs + kWaveSweep <= end;
+    if (nvs < end) {   // the next sweep's loads in flight during this one
+      if (nfull) fetch_sweep<PLANAR, true, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
+      else fetch_sweep<PLANAR, false, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
+    }
+    // the parent's final decision: its cut when proven, else its last 2-means plane
+    SweepMask om, nm;
+    if (full) {
+      if (cut) {
+        nm = cut_new_bytes(sw, (uint32_t)q.shift, q.thr);
+#pragma unroll
+        for (int j = 0; j < kVecPerThread; ++j) om.m[j] = nm.m[j] ^ 0x01010101u;
+      } else {
+        om = bits_to_bytes(old_mask(sw, 0xFFFFu, q, exact_all));
+#pragma unroll
+        for (int j = 0; j < kVecPerThread; ++j) nm.m[j] = om.m[j] ^ 0x01010101u;
+      }
+    } else {
+      const uint32_t validm = valid_mask<PLANAR>(vs, start, end);
+      const uint32_t oldm = cut ? validm & ~cut_new_mask(sw, (uint32_t)q.shift, q.thr)
+                                : old_mask(sw, validm, q, exact_all);
+      om = bits_to_bytes(oldm);
+      nm = bits_to_bytes(validm & ~oldm);
+    }
+    // the children's split pass on the same registers (cut_pos < v_axis <=>
+    // v_axis >= thr): each child's new-side slots, counted and summed
+    SweepMask xm = cut_new_bytes(sw, sh0, thr0), ym = cut_new_bytes(sw, sh1, thr1);
+#pragma unroll
+    for (int j = 0; j < kVecPerThread; ++j) {
+      xm.m[j] &= om.m[j];   // new for the old child
+      ym.m[j] &= nm.m[j];   // new for the new child
+    }
+    add_sums_bytes(sw, xm, so);
+    add_sums_bytes(sw, ym, sn);
+    // this wave's points.  A sweep writes at most kWaveSweep points to each
+    // child: when neither child's current chunk can end inside it (fast
+    // sweep), only the lanes' new counts are kept; otherwise every slot's run
+    // is split exactly.
+    const uint32_t oc = g.cbo + g.po, nc = g.cbn + g.pn - kStageRun;
+    const bool fast = oc + kWaveSweep <= cx.end && nc + kWaveSweep <= cy.end;
+    uint32_t ax = 0, ay = 0;
+    if (fast) stage_sweep<false>(sw, om, nm, full, st, g, l, xm, ym, 0u, 0u, ax, ay);
+    else stage_sweep<true>(sw, om, nm, full, st, g, l, xm, ym, cx.end, cy.end, ax, ay);
+    chunk_sweep(cx, oc, g.cbo + g.po, mask_count(xm), ax);
+    chunk_sweep(cy, nc, g.cbn + g.pn - kStageRun, mask_count(ym), ay);
+    stage_flush(st, d, g, l);
+    vs = nvs;
+    full = nfull;
+  }
+  stage_bytes(st, d, g, g.cbo + g.po, g.cbn + g.pn - kStageRun, l);   // the runs' last partial chunks
+  chunk_finish(cx);
+  chunk_finish(cy);
 }
 
 __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArgs a) {
   if (a.counts && blockIdx.x >= a.counts[1]) return;   // planned round: grid is an upper bound
   const PartTile pt = a.ptiles[blockIdx.x];
-  const Tile* tp = pt.tile;
-  const DevNode& nd = *pt.parent;
-  const uint32_t w = wave_id(), l = lane_id();
-  uint32_t start, end;   // this wave's range of the parent tile
-  wave_range(tp->start, tp->end, w, start, end);
-  g_cu4* src4 = as_g4(nd.src);
-  // child buffer of the frame shard: every index < off + len < 2^30
-  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-      nd.dst, (short)0, (int)((nd.off + nd.len) * 4u), 0x00020000);
-  const Params q = nd.prm;
-  const uint32_t n_old = nd.len - nd.n_new_local;
-  uint32_t oc = nd.off + tp->old_base[w];
-  uint32_t nc = nd.off + n_old + tp->new_base[w];
-  const bool exact_all = !(q.eps < __builtin_inff());   // FP32 filter off for this node
-  const bool cut = nd.proven != 0;
-  const uint32_t sh0 = (uint32_t)pt.shift[0], sh1 = (uint32_t)pt.shift[1];
-  const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
+  g_cnode& nd = *(g_cnode*)pt.parent;
+  g_ctile* tp = (g_ctile*)pt.tile;
   SplitSums so, sn;
-  ChunkAcc cx, cy;
-  chunk_init(cx, a.nodes, a.wparts, pt.child[0], oc);
-  chunk_init(cy, a.nodes, a.wparts, pt.child[1], nc);
-
-  u32x4 v[kVecPerThread];
-  uint32_t vs = start & ~3u;
-  bool full = vs >= start && vs + kWaveSweep <= end;
-  if (vs < end) {
-    if (full) load_sweep<true, DQ_PS_NTLOAD>(src4, vs, end, v);
-    else load_sweep<false, DQ_PS_NTLOAD>(src4, vs, end, v);
-  }
-  while (vs < end) {
-    uint32_t oldm, validm;
-    if (cut) {   // proven parent: its final halves are the cut's
-      if (full) cut_sweep<true>(v, vs, start, end, (uint32_t)q.shift, q.thr, oldm, validm);
-      else cut_sweep<false>(v, vs, start, end, (uint32_t)q.shift, q.thr, oldm, validm);
-    } else {
-      if (full) decide_sweep<true>(v, vs, start, end, q, exact_all, oldm, validm);
-      else decide_sweep<false>(v, vs, start, end, q, exact_all, oldm, validm);
-    }
-    const uint32_t newm = validm & ~oldm;
-    // --- the children's split pass on the same registers (cut_pos < v_axis
-    //     <=> v_axis >= thr): per lane, a bit per slot below each child's
-    //     threshold, then the children's new-side slots as masks; counts by
-    //     popcount, sums by v_dot4 against byte weights spread from 4 mask
-    //     bits (b * 0x204081 puts bit i at bit 8i), the byte transposes shared
-    //     by both children
-    uint32_t lt0 = 0, lt1 = 0;
-#pragma unroll
-    for (int j = 0; j < kVecPerThread; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int sidx = j * 4 + e;
-        const uint32_t p = vec_elem(v[j], e);
-        lt0 |= ((uint32_t)((int32_t)((p >> sh0) & 0xFF) - thr0) >> 31) << sidx;
-        lt1 |= ((uint32_t)((int32_t)((p >> sh1) & 0xFF) - thr1) >> 31) << sidx;
-      }
-    const uint32_t xcut = oldm & ~lt0, ycut = newm & ~lt1;   // slots new for the old / new child
-    so.cnt += (uint32_t)__builtin_popcount(xcut);
-    sn.cnt += (uint32_t)__builtin_popcount(ycut);
-#pragma unroll
-    for (int j = 0; j < kVecPerThread; ++j) {
-      const u32x4 x = v[j];
-      const uint32_t u01 = __builtin_amdgcn_perm(x[1], x[0], 0x05010400u);  // B0 B1 G0 G1
-      const uint32_t u23 = __builtin_amdgcn_perm(x[3], x[2], 0x05010400u);  // B2 B3 G2 G3
-      const uint32_t bq = __builtin_amdgcn_perm(u23, u01, 0x05040100u);     // B0 B1 B2 B3
-      const uint32_t gq = __builtin_amdgcn_perm(u23, u01, 0x07060302u);     // G0 G1 G2 G3
-      const uint32_t rq = __builtin_amdgcn_perm(x[1], x[0], 0x0C0C0602u) |  // R0 R1 0 0
-                          __builtin_amdgcn_perm(x[3], x[2], 0x06020C0Cu);   // 0 0 R2 R3
-      const uint32_t wx = (((xcut >> (4 * j)) & 0xFu) * 0x204081u) & 0x01010101u;
-      const uint32_t wy = (((ycut >> (4 * j)) & 0xFu) * 0x204081u) & 0x01010101u;
-      const uint32_t mx = wx * 0xFFu, my = wy * 0xFFu;
-      so.sr = __builtin_amdgcn_udot4(rq, wx, so.sr, false);
-      so.sg = __builtin_amdgcn_udot4(gq, wx, so.sg, false);
-      so.sb = __builtin_amdgcn_udot4(bq, wx, so.sb, false);
-      so.qr = __builtin_amdgcn_udot4(rq & mx, rq, so.qr, false);
-      so.qg = __builtin_amdgcn_udot4(gq & mx, gq, so.qg, false);
-      so.qb = __builtin_amdgcn_udot4(bq & mx, bq, so.qb, false);
-      sn.sr = __builtin_amdgcn_udot4(rq, wy, sn.sr, false);
-      sn.sg = __builtin_amdgcn_udot4(gq, wy, sn.sg, false);
-      sn.sb = __builtin_amdgcn_udot4(bq, wy, sn.sb, false);
-      sn.qr = __builtin_amdgcn_udot4(rq & my, rq, sn.qr, false);
-      sn.qg = __builtin_amdgcn_udot4(gq & my, gq, sn.qg, false);
-      sn.qb = __builtin_amdgcn_udot4(bq & my, bq, sn.qb, false);
-    }
-    // --- next sweep's loads in flight during the stores
-    const uint32_t nvs = vs + kWaveSweep;
-    const bool nfull = nvs >= start && nvs + kWaveSweep <= end;
-#if DQ_PS_PREFETCH
-    u32x4 vn[kVecPerThread];
-    if (nvs < end) {
-      if (nfull) load_sweep<true, DQ_PS_NTLOAD>(src4, nvs, end, vn);
-      else load_sweep<false, DQ_PS_NTLOAD>(src4, nvs, end, vn);
-    }
-#endif
-    // --- this wave's points (store_sweep).  A sweep writes at most kWaveSweep points to each child: when neither
-    // child's current chunk can end inside it (fast sweep), only the lanes'
-    // new counts are kept; otherwise every slot's run is split exactly.
-    const bool fast = oc + kWaveSweep <= cx.end && nc + kWaveSweep <= cy.end;
-    const uint32_t oc0 = oc, nc0 = nc;
-    uint32_t ax = 0, ay = 0;
-    if (fast) store_sweep<false>(v, oldm, newm, full, drs, l, xcut, ycut, oc, nc, 0u, 0u, ax, ay);
-    else store_sweep<true>(v, oldm, newm, full, drs, l, xcut, ycut, oc, nc, cx.end, cy.end, ax, ay);
-    chunk_sweep(cx, oc0, oc, (uint32_t)__builtin_popcount(xcut), ax);
-    chunk_sweep(cy, nc0, nc, (uint32_t)__builtin_popcount(ycut), ay);
-#if DQ_PS_PREFETCH
-#pragma unroll
-    for (int j = 0; j < kVecPerThread; ++j) v[j] = vn[j];
-#else
-    if (nvs < end) {
-      if (nfull) load_sweep<true, DQ_PS_NTLOAD>(src4, nvs, end, v);
-      else load_sweep<false, DQ_PS_NTLOAD>(src4, nvs, end, v);
-    }
-#endif
-    vs = nvs;
-    full = nfull;
-  }
-
-  chunk_finish(cx);
-  chunk_finish(cy);
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
+  uint8_t* st = stage + wave_id() * kStageWave;
+  if (nd.planar) partsplit_run<true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
+  else partsplit_run<false>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
 
   __shared__ uint32_t red[kTileWaves][16];
+  const uint32_t w = wave_id(), l = lane_id();
   uint32_t f[16] = {so.cnt, so.sr, so.sg, so.sb, so.qr, so.qg, so.qb, 0u,
                     sn.cnt, sn.sr, sn.sg, sn.sb, sn.qr, sn.qg, sn.qb, 0u};
 #pragma unroll
@@ -1254,52 +1454,71 @@ __device__ __forceinline__ void plan_cut(const NodeResult& r, int side, int32_t*
 
 // One child record: the parent's old (side 0) or new (side 1) half
 // (run_round's fill for a node fused into its parent's partition).
+// (Fields are stored one by one: a DevNode built in registers and copied as
+// a whole went through scratch memory.)
 __device__ void plan_child(const PlanArgs& a, const DevNode& P, const NodeResult& r, int side,
                            int32_t rec, uint32_t off, uint32_t len, int32_t tb, int32_t pb, int32_t pe) {
-  DevNode d;
-  d.src = P.dst;
-  const uint32_t* pd = P.dst;
-  const bool in_p0 = pd >= a.p0 && pd < a.p0 + a.cap_px;
-  d.dst = const_cast<uint32_t*>(in_p0 ? a.p1 + (pd - a.p0) : a.p0 + (pd - a.p1));
-  d.off = off;
-  d.len = len;
-  d.tile_begin = tb;
+  // everything read first (the stores below may not be reordered with loads
+  // of possibly aliasing memory); channels as scalars, not an indexed array
+  const uint8_t* pd = P.dst;
+  const double ps = P.s;
+  const double tw = side ? r.nw : r.ow;
+  const double* mp = side ? r.nm : r.om;
+  const double* vp = side ? r.nv : r.ov;
+  const double m0 = mp[0], m1 = mp[1], m2 = mp[2];
+  const double v0 = vp[0], v1 = vp[1], v2 = vp[2];
+  const int32_t pthr = P.prm.thr, pax = (16 - P.prm.shift) >> 3;
+  int32_t lo[3] = {P.box_lo[0], P.box_lo[1], P.box_lo[2]};
+  int32_t hi[3] = {P.box_hi[0], P.box_hi[1], P.box_hi[2]};
+  const bool proven = r.proven != 0;
+
+  DevNode* d = a.cn + rec;
+  d->src = pd;
+  const bool in_p0 = pd >= a.p0 && pd < a.p0 + a.cap_bytes;
+  d->dst = const_cast<uint8_t*>(in_p0 ? a.p1 + (pd - a.p0) : a.p0 + (pd - a.p1));
+  d->off = off;
+  d->len = len;
+  d->tile_begin = tb;
   const uint32_t tln = plan_tile_len(len, a.tl, a.node_tiles);
-  d.tile_end = tb + (int32_t)plan_ntiles(len, a.tl, a.node_tiles);
-  d.split_pb = pb;
-  d.split_pe = pe;
-  d.split_side = side;
-  d.pad0 = 0;
-  d.s = P.s;
-  d.tw = side ? r.nw : r.ow;
-  for (int c = 0; c < 3; ++c) {
-    d.tm[c] = side ? r.nm[c] : r.om[c];
-    d.tv[c] = side ? r.nv[c] : r.ov[c];
-  }
-  int32_t thr, shift;
-  plan_cut(r, side, &thr, &shift);   // the cut of :388-403
-  Params q;
-  q.lhs = q.rr = q.rg = q.rb = 0.0;
-  q.lhsf = q.rrf = q.rgf = q.rbf = q.eps = 0.0f;
-  q.thr = thr;
-  q.shift = shift;
-  q.pad = 0;
-  d.prm = q;
-  for (int c = 0; c < 4; ++c) d.prev[c] = 0;
-  d.n_new_local = 0;
-  d.iter = 0;
-  d.done_it = 0;
-  d.tile_len = tln;
-  d.proven = 0;
-  d.pad2[0] = d.pad2[1] = d.pad2[2] = 0;
+  d->tile_end = tb + (int32_t)plan_ntiles(len, a.tl, a.node_tiles);
+  d->split_pb = pb;
+  d->split_pe = pe;
+  d->split_side = side;
+  d->planar = 1;
+  d->s = ps;
+  d->tw = tw;
+  d->tm[0] = m0;
+  d->tm[1] = m1;
+  d->tm[2] = m2;
+  d->tv[0] = v0;
+  d->tv[1] = v1;
+  d->tv[2] = v2;
+  // the cut of :388-403 (plan_cut)
+  double maxv = v0, cut = m0;
+  int axis = 0;
+  if (maxv < v1) { maxv = v1; axis = 1; cut = m1; }
+  if (maxv < v2) { axis = 2; cut = m2; }
+  d->prm.lhs = d->prm.rr = d->prm.rg = d->prm.rb = 0.0;
+  d->prm.lhsf = d->prm.rrf = d->prm.rgf = d->prm.rbf = d->prm.eps = 0.0f;
+  d->prm.thr = split_threshold(cut);
+  d->prm.shift = 16 - 8 * axis;
+  d->prm.pad = 0;
+  for (int c = 0; c < 4; ++c) d->prev[c] = 0;
+  d->n_new_local = 0;
+  d->iter = 0;
+  d->done_it = 0;
+  d->tile_len = tln;
+  d->proven = 0;
+  d->pad2[0] = d->pad2[1] = d->pad2[2] = 0;
   // the box: the parent's, clipped at the parent's cut when its halves are the cut's
-  const int pax = (16 - P.prm.shift) >> 3;
-  for (int c = 0; c < 3; ++c) { d.box_lo[c] = P.box_lo[c]; d.box_hi[c] = P.box_hi[c]; }
-  if (r.proven) {
-    if (side) d.box_lo[pax] = max(P.box_lo[pax], P.prm.thr);
-    else d.box_hi[pax] = min(P.box_hi[pax], P.prm.thr - 1);
+  for (int c = 0; c < 3; ++c) {
+    if (proven && c == pax) {
+      if (side) lo[c] = max(lo[c], pthr);
+      else hi[c] = min(hi[c], pthr - 1);
+    }
+    d->box_lo[c] = lo[c];
+    d->box_hi[c] = hi[c];
   }
-  a.cn[rec] = d;
 }
 
 // grid: nb_rec + nb_tile workgroups.  Every workgroup checks that all listed
@@ -1322,20 +1541,30 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
   // clear [LaunchCtr | wparts | rdone] (grid-stride)
   for (uint32_t i = blockIdx.x * kPlanBlock + tid; i < a.nzero; i += gridDim.x * kPlanBlock) a.zero[i] = 0u;
   __syncthreads();
-  // (1) every parent final? exclusive scans of the tile counts, chunk by chunk
+  // (1) every parent final? exclusive scans of the tile counts, chunk by
+  //     chunk; a lane takes kPlanPer consecutive parents of a chunk (all their
+  //     loads in flight together)
+  constexpr int kPlanPer = 4;
   uint32_t run_t = 0, run_p = 0;
   bool bad = false;
-  for (int32_t c0 = 0; c0 < np; c0 += kPlanBlock) {
-    const int32_t i = c0 + (int32_t)tid;
-    uint32_t t = 0, q = 0;
-    if (i < np) {
-      const DevNode& P = a.pn[parent(i)];
-      bad |= P.done_it == 0;
-      const uint32_t nn = P.n_new_local;
-      t = plan_ntiles(P.len - nn, a.tl, a.node_tiles) + plan_ntiles(nn, a.tl, a.node_tiles);
-      q = (uint32_t)(P.tile_end - P.tile_begin);
+  for (int32_t c0 = 0; c0 < np; c0 += kPlanBlock * kPlanPer) {
+    const int32_t i0 = c0 + (int32_t)tid * kPlanPer;
+    uint32_t t[kPlanPer], q[kPlanPer];
+    uint32_t lt = 0, lp = 0;
+#pragma unroll
+    for (int e = 0; e < kPlanPer; ++e) {
+      t[e] = q[e] = 0;
+      if (i0 + e < np) {
+        const DevNode& P = a.pn[parent(i0 + e)];
+        bad |= P.done_it == 0;
+        const uint32_t nn = P.n_new_local;
+        t[e] = plan_ntiles(P.len - nn, a.tl, a.node_tiles) + plan_ntiles(nn, a.tl, a.node_tiles);
+        q[e] = (uint32_t)(P.tile_end - P.tile_begin);
+      }
+      lt += t[e];
+      lp += q[e];
     }
-    uint32_t it = t, ip = q;
+    uint32_t it = lt, ip = lp;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(it, o, 64), v = __shfl_up(ip, o, 64);
@@ -1343,11 +1572,16 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     }
     if (lane == 63) { s_w[wv][0] = it; s_w[wv][1] = ip; }
     __syncthreads();
-    uint32_t bt = run_t, bp = run_p;
+    uint32_t bt = run_t + it - lt, bp = run_p + ip - lp;
     for (uint32_t w = 0; w < wv; ++w) { bt += s_w[w][0]; bp += s_w[w][1]; }
-    if (i < np) {
-      s_cb[i] = bt + it - t;
-      s_pb[i] = bp + ip - q;
+#pragma unroll
+    for (int e = 0; e < kPlanPer; ++e) {
+      if (i0 + e < np) {
+        s_cb[i0 + e] = bt;
+        s_pb[i0 + e] = bp;
+      }
+      bt += t[e];
+      bp += q[e];
     }
     for (int w = 0; w < kPlanBlock / 64; ++w) { run_t += s_w[w][0]; run_p += s_w[w][1]; }
     __syncthreads();   // (s_w reuse)
@@ -1399,27 +1633,30 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     if (side) k -= t0;
     const uint32_t off = side ? P.off + lo : P.off, len = side ? nn : lo;
     const uint32_t tln = plan_tile_len(len, a.tl, a.node_tiles);
-    Tile tt;
-    tt.node = 2 * i + side;
-    tt.start = off + k * tln;
-    tt.end = off + min(len, (k + 1) * tln);
-    tt.pad = 0;
-    for (int w = 0; w < kTileWaves; ++w) { tt.old_base[w] = 0; tt.new_base[w] = 0; }
-    a.ct[j] = tt;
+    Tile* tt = a.ct + j;
+    tt->node = 2 * i + side;
+    tt->start = off + k * tln;
+    tt->end = off + min(len, (k + 1) * tln);
+    tt->pad = 0;
+    for (int w = 0; w < kTileWaves; ++w) { tt->old_base[w] = 0; tt->new_base[w] = 0; }
   }
   if (j < run_p) {
     const int32_t i = find(s_pb, j);
     const int32_t ai = parent(i);
     const DevNode& P = a.pn[ai];
     const NodeResult& r = a.pres[ai];
-    PartTile pt;
-    pt.tile = a.ptiles + P.tile_begin + (j - s_pb[i]);
-    pt.parent = a.pn + ai;
-    plan_cut(r, 0, &pt.thr[0], &pt.shift[0]);
-    plan_cut(r, 1, &pt.thr[1], &pt.shift[1]);
-    pt.child[0] = 2 * i;
-    pt.child[1] = 2 * i + 1;
-    a.cpt[j] = pt;
+    PartTile* pt = a.cpt + j;
+    pt->tile = a.ptiles + P.tile_begin + (j - s_pb[i]);
+    pt->parent = a.pn + ai;
+    int32_t thr0, sh0, thr1, sh1;
+    plan_cut(r, 0, &thr0, &sh0);
+    plan_cut(r, 1, &thr1, &sh1);
+    pt->thr[0] = thr0;
+    pt->thr[1] = thr1;
+    pt->shift[0] = sh0;
+    pt->shift[1] = sh1;
+    pt->child[0] = 2 * i;
+    pt->child[1] = 2 * i + 1;
   }
 }
 

@@ -183,11 +183,15 @@ int dq_hip_get_lanes(void);
 
 /* ---- per-kernel timing (HIP events on the launch stream) -----------------
  * kinds: 0 init pass, 1 split pass, 2 2-means pass, 3 last 2-means pass,
- * 4 epilogue, 5 partition, 6 map cells, 7 map.  bytes = algorithmic bytes. */
+ * 4 epilogue, 5 partition, 6 map cells, 7 map, 8 plan.  bytes = the engine
+ * work model's bytes (4 B per point read from the caller's
+ * packed frame, 3 B per point read or written in the planar working
+ * buffers, 8 B per mapped pixel); units = points (pixels) processed. */
 void dq_hip_set_timing(int device, int on);
 void dq_hip_reset_stats(int device);
 int dq_hip_get_stat(int device, int kind, uint64_t *launches, double *ms,
                     double *bytes);
+int dq_hip_get_stat_units(int device, int kind, double *units);
 const char *dq_hip_stat_name(int kind);
 
 #ifdef __cplusplus

@@ -112,10 +112,150 @@ __global__ __launch_bounds__(256) void pcopy_lds(const uint32_t* __restrict__ sr
   }
 }
 
+// Planar u8 layout (R, G, B planes of `stride` bytes): lane l holds the 16
+// points [vs + 16 l, +16) as one 16-B load per plane; each point is written
+// as one byte per plane into one of the wave's two runs (ballot-ranked,
+// slot by slot: 3 byte stores per slot).
+__global__ __launch_bounds__(256) void pcopy3(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                              uint32_t T, uint32_t stride) {
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint32_t t0 = blockIdx.x * T;
+  const uint32_t share = T / 4;
+  const uint32_t r0 = t0 + w * share;
+  uint32_t oc = r0, nc = r0 + share - 1;
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFF0, 0x00020000);
+  for (uint32_t vs = 0; vs < share; vs += 1024) {
+    const uint4 R = *reinterpret_cast<const uint4*>(src + r0 + vs + 16 * l);
+    const uint4 G = *reinterpret_cast<const uint4*>(src + stride + r0 + vs + 16 * l);
+    const uint4 B = *reinterpret_cast<const uint4*>(src + 2 * stride + r0 + vs + 16 * l);
+    const uint32_t rw[4] = {R.x, R.y, R.z, R.w}, gw[4] = {G.x, G.y, G.z, G.w}, bw[4] = {B.x, B.y, B.z, B.w};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const uint32_t r = rw[s >> 2] >> (8 * (s & 3)), g = gw[s >> 2] >> (8 * (s & 3)), b = bw[s >> 2] >> (8 * (s & 3));
+      const bool o = (r ^ (g >> 3)) & 1u;
+      const uint64_t bo = __ballot(o);
+      const uint32_t ro = __builtin_amdgcn_mbcnt_hi((uint32_t)(bo >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bo, 0u));
+      const uint32_t idx = o ? oc + ro : nc - (l - ro);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)r, rs, (int)idx, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)g, rs, (int)(idx + stride), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b, rs, (int)(idx + 2 * stride), 0, 0);
+      const uint32_t co = (uint32_t)__popcll(bo);
+      oc += co;
+      nc -= 64u - co;
+    }
+  }
+}
+
+// pcopy3 with the wave's sweep ranked into LDS first (3 planes x 1024 B per
+// wave), then written with dword stores where 4 LDS bytes land in one run on
+// a 4-B aligned destination, else bytes (run heads and tails).
+__global__ __launch_bounds__(256) void pcopy3_lds(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                  uint32_t T, uint32_t stride) {
+  __shared__ uint8_t stage[4][3][1024 + 16];
+  const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const uint32_t t0 = blockIdx.x * T;
+  const uint32_t share = T / 4;
+  const uint32_t r0 = t0 + w * share;
+  uint32_t oc = r0, nc = r0 + share;   // new run written upward from the region's second half (shape only)
+  nc = r0 + share / 2;
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFF0, 0x00020000);
+  for (uint32_t vs = 0; vs < share; vs += 1024) {
+    const uint4 R = *reinterpret_cast<const uint4*>(src + r0 + vs + 16 * l);
+    const uint4 G = *reinterpret_cast<const uint4*>(src + stride + r0 + vs + 16 * l);
+    const uint4 B = *reinterpret_cast<const uint4*>(src + 2 * stride + r0 + vs + 16 * l);
+    const uint32_t rw[4] = {R.x, R.y, R.z, R.w}, gw[4] = {G.x, G.y, G.z, G.w}, bw[4] = {B.x, B.y, B.z, B.w};
+    uint32_t om = 0;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const uint32_t r = rw[s >> 2] >> (8 * (s & 3)), g = gw[s >> 2] >> (8 * (s & 3));
+      om |= ((r ^ (g >> 3)) & 1u) << s;
+    }
+    const uint32_t co = __builtin_popcount(om);
+    uint32_t inc = co;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { const uint32_t u = __shfl_up(inc, o, 64); if (l >= (uint32_t)o) inc += u; }
+    const uint32_t tot_old = __shfl(inc, 63, 64);
+    uint32_t po = inc - co, pn = tot_old + (l * 16 - (inc - co));
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool o = (om >> s) & 1u;
+      const uint32_t at = o ? po : pn;
+      stage[w][0][at] = (uint8_t)(rw[s >> 2] >> (8 * (s & 3)));
+      stage[w][1][at] = (uint8_t)(gw[s >> 2] >> (8 * (s & 3)));
+      stage[w][2][at] = (uint8_t)(bw[s >> 2] >> (8 * (s & 3)));
+      po += o; pn += !o;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // runs: LDS [0, tot_old) -> dst[oc ...], [tot_old, 1024) -> dst[nc ...]
+    // dword d of the destination covers bytes [4d, 4d+4): lanes take the
+    // dwords overlapping each run (aligned middle: one b32 store per plane)
+#pragma unroll
+    for (int run = 0; run < 2; ++run) {
+      const uint32_t ls = run ? tot_old : 0, le = run ? 1024 : tot_old;   // LDS range
+      const uint32_t d0 = run ? nc : oc;                                  // destination of ls
+      if (le == ls) continue;
+      const uint32_t first = d0 & ~3u, last = d0 + (le - ls);             // dwords [first, last)
+      for (uint32_t q = first + 4 * l; q < last; q += 256) {
+        const bool whole = q >= d0 && q + 4 <= last;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if (whole) {
+            const uint8_t* sp = &stage[w][c][ls + (q - d0)];
+            const uint32_t x = sp[0] | (sp[1] << 8) | (sp[2] << 16) | ((uint32_t)sp[3] << 24);
+            __builtin_amdgcn_raw_buffer_store_b32(x, rs, (int)(q + c * stride), 0, 0);
+          } else {
+            for (uint32_t e = 0; e < 4; ++e) {
+              const uint32_t dd = q + e;
+              if (dd >= d0 && dd < last)
+                __builtin_amdgcn_raw_buffer_store_b8(stage[w][c][ls + (dd - d0)], rs, (int)(dd + c * stride), 0, 0);
+            }
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    oc += tot_old;
+    nc += 1024 - tot_old;
+  }
+}
+
+// streaming read (the INIT pass's access): 16-B loads, one tile per workgroup
+__global__ __launch_bounds__(256) void read16(const uint4* __restrict__ a, uint32_t T4, uint32_t* out) {
+  const uint4* p = a + (size_t)blockIdx.x * T4;
+  uint32_t acc = 0;
+  for (uint32_t i = threadIdx.x; i < T4; i += 256) {
+    const uint4 v = p[i];
+    acc += v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
   const size_t N = argc > 1 ? strtoull(argv[1], 0, 10) : 66355200;   // 8 x 4K
   uint32_t *a, *b;
   CK(hipMalloc(&a, N * 4)); CK(hipMalloc(&b, N * 4));
+  {  // INIT's situation: a buffer last touched before ~1 GB of other traffic
+    uint32_t* flush;
+    const size_t FL = (size_t)1 << 30;
+    CK(hipMalloc(&flush, FL));
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (uint32_t T : {16384u, 65536u}) {
+      for (int cold = 1; cold >= 0; --cold) {
+        float tot = 0;
+        for (int r = 0; r < 10; ++r) {
+          if (cold) CK(hipMemsetAsync(flush, r, FL));
+          CK(hipEventRecord(e0));
+          read16<<<(unsigned)(N / T), 256>>>((const uint4*)a, T / 4, b);
+          CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+          float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+          tot += ms;
+        }
+        const double us = tot * 1e3 / 10;
+        printf("read16 T=%u %s %8.1f us  %7.1f GB/s (read)\n", T, cold ? "cold" : "warm", us, 4.0 * N / (us * 1e-6) / 1e9);
+      }
+    }
+    CK(hipFree(flush));
+  }
   CK(hipMemset(a, 0x5A, N * 4));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto run = [&](const char* name, auto fn) {
@@ -138,6 +278,14 @@ int main(int argc, char** argv) {
   for (uint32_t T : {8192u, 16384u, 65536u}) {
     char nm[64]; snprintf(nm, 64, "pcopy_lds T=%u", T);
     run(nm, [&] { pcopy_lds<<<(unsigned)(N / T), 256>>>(a, b, T); });
+  }
+  // planar: 6 B per point (time comparable with the 8-B packed lines above)
+  const uint32_t stride = (uint32_t)((N + 255) & ~(size_t)255);
+  for (uint32_t T : {16384u, 65536u}) {
+    char nm[64]; snprintf(nm, 64, "pcopy3 (planar) T=%u", T);
+    run(nm, [&] { pcopy3<<<(unsigned)(N / T), 256>>>((const uint8_t*)a, (uint8_t*)b, T, stride); });
+    snprintf(nm, 64, "pcopy3_lds (planar) T=%u", T);
+    run(nm, [&] { pcopy3_lds<<<(unsigned)(N / T), 256>>>((const uint8_t*)a, (uint8_t*)b, T, stride); });
   }
   return 0;
 }

@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-pmc}; shift || true
 O=$R/gpurun_out/$TAG
 mkdir -p $O
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-timing --no-c3 $*"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-timing --no-c3 --no-rowtile --no-verify $*"
 K="--kernel-include-regex (partsplit|pass_kernel|map_|epilogue|build_cells)"
 cd /tmp
 run() {   # name counters...
@@ -20,5 +20,6 @@ run fetch FETCH_SIZE
 run write WRITE_SIZE
 [ -n "$PMC_FULL" ] && run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 [ -n "$PMC_FULL" ] && run sq2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT
+[ -n "$PMC_FULL" ] && run lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES
 [ -n "$PMC_FULL" ] && run ta TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_HIT_sum TCC_MISS_sum
 true; echo pmc done

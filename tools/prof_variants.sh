@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/profv; mkdir -p $O; cd /tmp
 for v in base "$@"; do
   L=$R/clusteringsegmentation-1_amd/libdivquant_hip.so
   [ "$v" != base ] && L=$R/clusteringsegmentation-1_amd/variants/$v/libdivquant_hip.so
-  DQ_HIP_LIB=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/$v -o p --output-format csv -- python3 $R/bench.py --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-c3 --no-timing > $O/$v.log 2>&1
+  DQ_HIP_LIB=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/$v -o p --output-format csv -- python3 $R/bench.py --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-c3 --no-rowtile --no-verify --no-timing > $O/$v.log 2>&1
   echo "== $v $(python3 -c "import json;d=json.loads(open('$O/$v.log').read().strip().splitlines()[-1]);print(d['ms_per_step'])" 2>/dev/null)"
   python3 -c "
 import csv
