@@ -1830,12 +1830,17 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
   r.z = slot[3] | (slot[4] << 16);
   r.w = slot[5] | (slot[6] << 16);
   reinterpret_cast<uint4*>(tk.cell_rec)[cell] = r;
+  // compact record (K <= 1024): bit 31 -- one candidate, its colour in bits
+  // 0-23 (every filter is an exact elimination, so it is every colour's
+  // answer); bits 31:30 = 01 -- 2 or 3 candidates, 10-bit indices (unused
+  // slots repeat the first); 00 -- count << 16 | cell (count 63: whole palette)
   uint32_t c32;
-  if (fcount >= 1 && fcount <= 3) {
-    const uint32_t j0 = slot[0];
-    const uint32_t j1 = fcount > 1 ? slot[1] : j0;
+  if (fcount == 1) {
+    c32 = 0x80000000u | spal_c[slot[0]];
+  } else if (fcount >= 2 && fcount <= 3) {
+    const uint32_t j0 = slot[0], j1 = slot[1];
     const uint32_t j2 = fcount > 2 ? slot[2] : j0;
-    c32 = (fcount << 30) | j0 | (j1 << 10) | (j2 << 20);
+    c32 = 0x40000000u | j0 | (j1 << 10) | (j2 << 20);
   } else {
     c32 = ((brute ? 63u : fcount) << 16) | cell;
   }
@@ -1985,14 +1990,24 @@ __global__ __launch_bounds__(kBlock) void map_kernel(const MapTask* __restrict__
 // Map with the compact cell table in LDS (K <= 1024): one workgroup of
 // kMapLdsBlock threads per CU stages its task's 32768 compact records
 // (128 KB), the sorted palette and the start LUT, then maps its share of the
-// task's pixels, 8 per lane per iteration.  The 1-3 inline candidates of a
-// cell are evaluated branch-free.  Pixels of cells with more candidates are
-// queued in LDS (per wave, in slot order) and resolved cooperatively: lane i
-// takes queue entry i and scans that cell's list (one 16-B load for the
-// first 8 indices); the results return through the queue.  Queue overflow
-// (more than 64 such pixels in one wave-iteration) falls back to a per-lane
-// loop.  Same keys and the same answer as map_kernel.
+// task's pixels, 8 per lane per iteration.
+//   * A cell with ONE candidate (64 % of the cells for a 256-colour palette of
+//     uniform frames) holds its answer colour in the record: such a pixel
+//     needs no other LDS read (the candidate reads below are exec-masked, so
+//     their lanes cost no LDS cycles; the LDS bank conflicts of the random
+//     palette reads were ~2.5x the map's active LDS time).
+//   * 2-3 inline candidates are evaluated branch-free.
+//   * Pixels of cells with more candidates are queued in LDS (per wave, in
+//     slot order) and resolved cooperatively: lane i takes queue entry i and
+//     scans that cell's list; the results return through the queue.  Queue
+//     overflow (more than 64 such pixels in one wave-iteration) falls back to
+//     a per-lane loop.
+// Same keys and the same answer as map_kernel.
 constexpr int kMapQ = 64;
+// The map's output stores: nontemporal (streamed past the caches) or default
+#ifndef DQ_MAP_NT
+#define DQ_MAP_NT 1
+#endif
 __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __restrict__ tasks,
                                                               int ntasks) {
   int ti = 0;
@@ -2018,7 +2033,7 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
       spal[i] = make_uint2(q, c2 << 12);   // c2 < 2^20: the key's distance field, pre-shifted
     }
     g_cu16* glut = (g_cu16*)tk.lut;
-    for (int i = threadIdx.x; i < 766; i += kMapLdsBlock) slut[i] = glut[i];
+    for (int i = threadIdx.x; i < 766; i += kMapLdsBlock) slut[i] = (uint16_t)(4u * glut[i] + 1u);   // S = 4s + 1
   }
   __syncthreads();
   const uint32_t lane = lane_id();
@@ -2032,27 +2047,42 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   // (c2 - 2 dot) << 12 | sad, as (c2 << 12) - (dot << 13) + sad: the low 12
   // bits of the first two terms are zero and sad < 4096, so the OR is an add
   // and folds into v_sad_u16's accumulator (same 32-bit key as map_kernel)
+  // (c2 << 12) - (dot << 13) as one v_mad_i32_i24 (dot < 2^18).  The factor
+  // is -8192 at run time but not a compile-time constant (k < 2^30), or the
+  // compiler turns the multiply back into a shift and a subtract.
+  const int32_t m8192 = -(int32_t)(8192u | ((uint32_t)k >> 30));
   auto key = [&](uint32_t p, uint32_t S, uint32_t j) -> uint32_t {
     const uint2 en = spal[j];
-    const uint32_t hi = en.y - (__builtin_amdgcn_udot4(p, en.x, 0u, false) << 13);
+    const uint32_t hi = en.y + (uint32_t)__mul24((int)__builtin_amdgcn_udot4(p, en.x, 0u, false), m8192);
     return __builtin_amdgcn_sad_u16(4u * j, S, hi);
   };
   auto answer = [&](uint32_t S, uint32_t best) -> uint32_t {
     return spal[entry_from_sad<false>(S, best & 0xFFFu)].x;
   };
-  // the record of p's cell: byte offset 4 * cell = (R'' << 10) + (G'' << 5) + B''
-  // with X'' = (X >> 3) << 2, the bytes of m = (p >> 1) & 0x7C7C7C
+  // the record of p's cell (the top byte of p is ignored everywhere): byte
+  // offset 4 * cell = (R'' << 10) + (G'' << 5) + B'' with X'' = (X >> 3) << 2,
+  // the bytes of m = (p >> 1) & 0x7C7C7C
   static_assert(kCellBits == 5, "cell record offset assumes 5 bits per channel");
   auto cell_rec = [&](uint32_t p) -> uint32_t {
     const uint32_t m = (p >> 1) & 0x7C7C7Cu;
     const uint32_t off = ((m >> 16) << 10) + __builtin_amdgcn_udot4(m, 0x00002001u, 0u, false);
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(stab) + off);
   };
-  auto start_of = [&](uint32_t p) -> uint32_t {   // p < 2^24: R + G + B in one dot4
-    return 4u * slut[__builtin_amdgcn_udot4(p, 0x00010101u, 0u, false)] + 1u;
+  auto start_of = [&](uint32_t p) -> uint32_t {   // R + G + B in one dot4
+    return slut[__builtin_amdgcn_udot4(p, 0x00010101u, 0u, false)];
   };
-  // the exact answer for a pixel of an overflow cell (record r)
-  auto resolve = [&](uint32_t p, uint32_t S, uint32_t r) -> uint32_t {
+  // the exact answer for a pixel of a cell with 2 or more candidates
+  auto resolve = [&](uint32_t p, uint32_t r) -> uint32_t {
+    const uint32_t S = start_of(p);
+    if (r & 0x40000000u) {   // 2-3 inline candidates (unused slots repeat the first)
+      const uint32_t j0 = r & 0x3FFu, j1 = (r >> 10) & 0x3FFu, j2 = (r >> 20) & 0x3FFu;
+      const uint32_t q0 = spal[j0].x, q1 = spal[j1].x, q2 = spal[j2].x;
+      const uint32_t k0 = key(p, S, j0), k1 = key(p, S, j1), k2 = key(p, S, j2);
+      // keys of distinct entries differ (the tie field is |4j - S|, S odd):
+      // the answer is the winning candidate's own entry
+      const uint32_t best = min(k0, min(k1, k2));
+      return best == k0 ? q0 : (best == k1 ? q1 : q2);
+    }
     const uint32_t cnt = (r >> 16) & 0x3Fu;
     uint32_t best = 0xFFFFFFFFu;
     if (cnt == 63u) {
@@ -2092,59 +2122,77 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
         nb = in4[2 * gn + 1];
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { px[e] = a[e] & 0xFFFFFFu; px[4 + e] = b[e] & 0xFFFFFFu; }
+      for (int e = 0; e < 4; ++e) { px[e] = a[e]; px[4 + e] = b[e]; }
     }
-    uint32_t res[kMapPx], rec[kMapPx], Ss[kMapPx];
+    uint32_t res[kMapPx], rec[kMapPx];
+#pragma unroll
+    for (int e = 0; e < kMapPx; ++e) rec[e] = cell_rec(px[e]);
 #pragma unroll
     for (int e = 0; e < kMapPx; ++e) {
-      rec[e] = cell_rec(px[e]);
-      Ss[e] = start_of(px[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < kMapPx; ++e) {
-      // keys of distinct entries differ (the tie field is |4j - S|, S odd), so
-      // the answer is the winning candidate's own entry: no second palette read
-      const uint32_t p = px[e], S = Ss[e], r = rec[e];
+      // branch-free (every pixel's reads in flight together); a pixel whose
+      // cell is not 2-3 inline candidates reads entry 0 and LUT entry 0 --
+      // one broadcast address, no bank conflicts -- and keeps its answer
+      const uint32_t r0 = rec[e];
+      const bool inl = (r0 >> 30) == 1u;
+      const uint32_t r = inl ? r0 : 0u, p = inl ? px[e] : 0u;
+      const uint32_t S = start_of(p);
       const uint32_t j0 = r & 0x3FFu, j1 = (r >> 10) & 0x3FFu, j2 = (r >> 20) & 0x3FFu;
       const uint32_t q0 = spal[j0].x, q1 = spal[j1].x, q2 = spal[j2].x;
       const uint32_t k0 = key(p, S, j0), k1 = key(p, S, j1), k2 = key(p, S, j2);
+      // keys of distinct entries differ (the tie field is |4j - S|, S odd):
+      // the answer is the winning candidate's own entry
       const uint32_t best = min(k0, min(k1, k2));
-      res[e] = best == k0 ? q0 : (best == k1 ? q1 : q2);
+      const uint32_t qi = best == k0 ? q0 : (best == k1 ? q1 : q2);
+      res[e] = inl ? qi : (r0 & 0xFFFFFFu);   // (one candidate: its colour)
     }
-    // overflow cells: queue (slot order), resolve cooperatively, read back
-    uint32_t qpos[kMapPx];
-    uint32_t qn = 0;
+    // cells with more candidates: queue (lane order: an exclusive scan of the
+    // lanes' counts), resolve cooperatively, read back
+    uint32_t ovm = 0;
 #pragma unroll
-    for (int e = 0; e < kMapPx; ++e) {
-      const bool ov = have && (rec[e] >> 30) == 0;
-      const uint64_t m = __ballot(ov);
-      const uint32_t pos = qn + mbcnt64(m);
-      qpos[e] = ov ? pos : 0xFFFFFFFFu;
-      if (ov && pos < (uint32_t)kMapQ) wq[pos] = px[e];
-      qn += (uint32_t)__popcll(m);
+    for (int e = 0; e < kMapPx; ++e) ovm |= (uint32_t)((rec[e] >> 30) == 0) << e;
+    if (!have) ovm = 0;
+    const uint32_t cnt = (uint32_t)__builtin_popcount(ovm);
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += u;
     }
+    const uint32_t qn = __shfl(inc, 63, 64);
     if (qn > 0) {   // wave-uniform
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t pos0 = inc - cnt;   // this lane's first queue position
+      {
+        uint32_t pos = pos0;
+#pragma unroll
+        for (int e = 0; e < kMapPx; ++e) {
+          const bool ov = (ovm >> e) & 1u;
+          if (ov && pos < (uint32_t)kMapQ) wq[pos] = px[e];
+          pos += ov ? 1u : 0u;
+        }
+      }
+      wave_lds_sync();
       if (lane < min(qn, (uint32_t)kMapQ)) {
         const uint32_t p = wq[lane];
-        wq[lane] = resolve(p, start_of(p), cell_rec(p));
+        wq[lane] = resolve(p, cell_rec(p));
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      wave_lds_sync();
+      uint32_t pos = pos0;
 #pragma unroll
       for (int e = 0; e < kMapPx; ++e) {
-        if (qpos[e] < (uint32_t)kMapQ) res[e] = wq[qpos[e]];
-        else if (qpos[e] != 0xFFFFFFFFu) res[e] = resolve(px[e], Ss[e], rec[e]);   // queue full
+        const bool ov = (ovm >> e) & 1u;
+        if (ov) res[e] = pos < (uint32_t)kMapQ ? wq[pos] : resolve(px[e], rec[e]);   // (queue full: in lane)
+        pos += ov ? 1u : 0u;
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+      wave_lds_sync();
     }
     if (have) {
+#if DQ_MAP_NT
+      __builtin_nontemporal_store((u32x4){res[0], res[1], res[2], res[3]}, out4 + 2 * g);
+      __builtin_nontemporal_store((u32x4){res[4], res[5], res[6], res[7]}, out4 + 2 * g + 1);
+#else
       out4[2 * g] = (u32x4){res[0], res[1], res[2], res[3]};
       out4[2 * g + 1] = (u32x4){res[4], res[5], res[6], res[7]};
+#endif
     }
   }
   // tail (n % kMapPx points): the task's first workgroup, whole palette
