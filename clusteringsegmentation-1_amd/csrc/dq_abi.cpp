@@ -12,12 +12,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
-#include <vector>
-#include <thread>
 #include <vector>
 
 #include "../../include/DivQuantHeader.h"
@@ -67,6 +68,95 @@ void report_empty(int num_empty) {
   if (num_empty) std::fprintf(stderr, "# empty clusters: %d\n", num_empty);   // :1067-1069
 }
 
+// Persistent host threads for the batch lanes 1..L-1 (a std::thread per lane
+// per call cost tens of microseconds of every call's host time).  run()
+// hands job(i) to worker i, runs job(0) on the caller and returns when all
+// are done; workers spin briefly on the generation word before sleeping.
+class LaneWorkers {
+ public:
+  void run(int n, const std::function<void(int)>& job) {
+    std::lock_guard<std::mutex> call(call_mu_);
+    while ((int)threads_.size() < n - 1) {
+      const int id = (int)threads_.size() + 1;
+      threads_.emplace_back([this, id] { loop(id); });
+      threads_.back().detach();
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &job;
+      nact_ = n;
+      pending_.store(n - 1, std::memory_order_relaxed);
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    job(0);
+    for (uint64_t spin = 0; pending_.load(std::memory_order_acquire) != 0; ++spin) {
+      if (spin < (1u << 16)) {
+        __builtin_ia32_pause();
+      } else {
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [this] { return pending_.load(std::memory_order_acquire) == 0; });
+      }
+    }
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      uint64_t g = gen_.load(std::memory_order_acquire);
+      for (uint32_t spin = 0; g == seen && spin < (1u << 14); ++spin) {
+        __builtin_ia32_pause();
+        g = gen_.load(std::memory_order_acquire);
+      }
+      if (g == seen) {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+        g = gen_.load(std::memory_order_acquire);
+      }
+      seen = g;
+      const std::function<void(int)>* job;
+      int n;
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        job = job_;
+        n = nact_;
+      }
+      if (id < n) {
+        (*job)(id);
+        if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+          std::lock_guard<std::mutex> l(mu_);
+          done_cv_.notify_all();
+        }
+      }
+    }
+  }
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<int> pending_{0};
+  const std::function<void(int)>* job_ = nullptr;
+  int nact_ = 0;
+  std::vector<std::thread> threads_;
+};
+
+// The stream a device-pointer entry runs on: the caller's, or (NULL) the
+// engine's non-blocking stream made to wait for the legacy default stream
+// first -- the caller's inputs may still be in flight there (a torch
+// host-to-device copy on the default stream, say).
+hipStream_t dev_stream(Engine& e, void* stream) {
+  if (stream) return (hipStream_t)stream;
+  hipEvent_t ev = e.ready_event();
+  DQ_HIP(hipEventRecord(ev, nullptr));
+  DQ_HIP(hipStreamWaitEvent(e.stream(), ev, 0));
+  return e.stream();
+}
+
+LaneWorkers& lane_workers() {
+  static LaneWorkers* w = new LaneWorkers();   // (never destroyed: its threads are detached)
+  return *w;
+}
+
 }  // namespace
 
 // =========================================================================
@@ -92,7 +182,7 @@ int dq_hip_cluster_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* k
   j.n = n;
   j.k = (int)*k;
   j.ct = ct;
-  e.run(&j, 1, max_iters, false, (hipStream_t)stream);
+  e.run(&j, 1, max_iters, false, dev_stream(e, stream));
   *k = (uint32_t)j.k_out;
   return j.num_empty;
 }
@@ -108,7 +198,7 @@ int dq_hip_quant_weighted_dev(int device, const uint32_t* d_in, uint32_t n, uint
   j.d_out = d_out;
   j.k = (int)*k;
   j.ct = ct;
-  e.run_weighted(j, max_iters, d_out != nullptr, (hipStream_t)stream);
+  e.run_weighted(j, max_iters, d_out != nullptr, dev_stream(e, stream));
   *k = (uint32_t)j.k_out;
   return j.num_empty;
 }
@@ -119,7 +209,7 @@ int dq_hip_map_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out
   if (n == 0) return 0;
   Engine& e = engine_for(device);
   std::lock_guard<std::mutex> g(e.mutex());
-  e.map(d_in, n, d_out, ct, k, (hipStream_t)stream);
+  e.map(d_in, n, d_out, ct, k, dev_stream(e, stream));
   return 0;
 }
 
@@ -140,7 +230,7 @@ int dq_hip_block_hist_dev(int device, const uint32_t* d_in, uint32_t width, uint
     return -1;
   Engine& e = engine_for(device);
   std::lock_guard<std::mutex> g(e.mutex());
-  hipStream_t st = stream ? (hipStream_t)stream : e.stream();
+  hipStream_t st = dev_stream(e, stream);
   e.map(d_in, width * height, d_quant, palette, npal, st);
   // the tie queues are private to this call (stream-ordered allocation): the
   // kernels are still running when the call returns, and another call may
@@ -162,7 +252,7 @@ static bool bgr24_shape_ok(uint32_t width, uint32_t height, uint32_t stride) {
 static hipStream_t engine_stream(int device, void* stream) {
   Engine& e = engine_for(device);
   DQ_HIP(hipSetDevice(device));
-  return stream ? (hipStream_t)stream : e.stream();
+  return dev_stream(e, stream);
 }
 
 int dq_hip_pack_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t width, uint32_t height,
@@ -209,34 +299,28 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
   Engine& e0 = engine_for(device);
   if (lanes <= 1) {
     std::lock_guard<std::mutex> g(e0.mutex());
-    e0.run(jobs.data(), nframes, max_iters, true, (hipStream_t)stream);
+    e0.run(jobs.data(), nframes, max_iters, true, dev_stream(e0, stream));
   } else {
     // frames [f0(l), f0(l+1)) on lane l; every lane first waits for the
     // caller's stream (the frames may have been produced there)
     DQ_HIP(hipSetDevice(device));
-    hipEvent_t ready;
-    DQ_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    hipEvent_t ready = e0.ready_event();
     DQ_HIP(hipEventRecord(ready, (hipStream_t)stream));
-    std::vector<std::thread> th;
-    for (int l = lanes - 1; l >= 0; --l) {
+    for (int l = 1; l < lanes; ++l) {   // lanes inherit lane 0's switches
+      Engine& e = engine_for(device, l);
+      e.set_fixed_point(e0.fixed_point());
+      e.set_plan(e0.plan());
+      e.set_timing(e0.timing());
+    }
+    const std::function<void(int)> work = [&](int l) {
       const int f0 = nframes * l / lanes, f1 = nframes * (l + 1) / lanes;
       Engine& e = engine_for(device, l);
-      if (l > 0) {   // lanes inherit lane 0's switches
-        e.set_fixed_point(e0.fixed_point());
-        e.set_plan(e0.plan());
-        e.set_timing(e0.timing());
-      }
-      auto work = [&e, &jobs, f0, f1, max_iters, ready, device]() {
-        DQ_HIP(hipSetDevice(device));
-        std::lock_guard<std::mutex> g(e.mutex());
-        DQ_HIP(hipStreamWaitEvent(e.stream(), ready, 0));
-        e.run(jobs.data() + f0, f1 - f0, max_iters, true, e.stream());
-      };
-      if (l > 0) th.emplace_back(work);
-      else work();
-    }
-    for (auto& t : th) t.join();
-    DQ_HIP(hipEventDestroy(ready));
+      DQ_HIP(hipSetDevice(device));
+      std::lock_guard<std::mutex> g(e.mutex());
+      DQ_HIP(hipStreamWaitEvent(e.stream(), ready, 0));
+      e.run(jobs.data() + f0, f1 - f0, max_iters, true, e.stream());
+    };
+    lane_workers().run(lanes, work);
     // lane 0 reports for the batch: the last frame's diagnostics, summed counters
     Engine& el = engine_for(device, lanes - 1);
     std::lock_guard<std::mutex> g(e0.mutex());
@@ -289,7 +373,7 @@ int dq_hip_quant_rows_dev(int device, int nframes, const uint32_t* const* d_in,
     jobs[i].width = width ? width[i] : 0;
     jobs[i].n_global = n_global ? n_global[i] : 0;
   }
-  e.run(jobs.data(), nframes, max_iters, true, (hipStream_t)stream);
+  e.run(jobs.data(), nframes, max_iters, true, dev_stream(e, stream));
   int empty = 0;
   for (int i = 0; i < nframes; ++i) {
     k_out[i] = (uint32_t)jobs[i].k_out;

@@ -137,6 +137,11 @@ class Engine {
   uint32_t* scratch_words(size_t n);
 
   hipStream_t stream() const { return stream_; }
+  // An event the batch call records on the caller's stream for its lanes.
+  hipEvent_t ready_event() {
+    if (!ready_ev_) DQ_HIP(hipEventCreateWithFlags(&ready_ev_, hipEventDisableTiming));
+    return ready_ev_;
+  }
 
   // Row-tile sharding across processes (one GPU each): an RCCL communicator
   // over which every pass's node totals are allreduced.
@@ -337,6 +342,7 @@ class Engine {
   uint32_t* d_mapstage_ = nullptr;
   uint32_t* d_mapstage_view_ = nullptr;   // device view of h_mapstage_ (host-coherent)
   hipEvent_t map_ev_ = nullptr;           // the last upload of h_mapstage_
+  hipEvent_t ready_ev_ = nullptr;         // ready_event()
   bool map_pending_ = false;
   size_t cap_mapstage_ = 0;
   void ensure_map_stage(size_t nmaps);

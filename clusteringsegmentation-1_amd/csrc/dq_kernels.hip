@@ -1047,6 +1047,11 @@ __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
 #ifndef DQ_PS_WAVES
 #define DQ_PS_WAVES 4
 #endif
+// the next sweep's loads issued before this sweep's work (1) or after it (0;
+// measured 104 vs 108 us per 8 x 4K launch)
+#ifndef DQ_PS_PREFETCH
+#define DQ_PS_PREFETCH 0
+#endif
 // Cache policy of partsplit's streams (a parent's points are read once, its
 // children's written once): nontemporal loads, store cache-policy bits
 #ifndef DQ_PS_NTLOAD
@@ -1336,10 +1341,12 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     unpack_sweep<PLANAR>(x, sw);
     const uint32_t nvs = vs + kWaveSweep;
     const bool nfull = nvs + kWaveSweep <= end;
+#if DQ_PS_PREFETCH
     if (nvs < end) {   // the next sweep's loads in flight during this one
       if (nfull) fetch_sweep<PLANAR, true, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
       else fetch_sweep<PLANAR, false, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
     }
+#endif
     // the parent's final decision: its cut when proven, else its last 2-means plane
     SweepMask om, nm;
     if (full) {
@@ -1381,6 +1388,12 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     chunk_sweep(cx, oc, g.cbo + g.po, mask_count(xm), ax);
     chunk_sweep(cy, nc, g.cbn + g.pn - kStageRun, mask_count(ym), ay);
     stage_flush(st, d, g, l);
+#if !DQ_PS_PREFETCH
+    if (nvs < end) {
+      if (nfull) fetch_sweep<PLANAR, true, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
+      else fetch_sweep<PLANAR, false, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
+    }
+#endif
     vs = nvs;
     full = nfull;
   }

@@ -2,7 +2,9 @@
  * dq_hip.h -- the thin C ABI of libdivquant_hip.so (MI355X / gfx950).
  *
  * Plain pointers and sizes only (no torch, no HIP types in the signatures;
- * `stream` is a hipStream_t passed as void*, NULL = the library's stream).
+ * `stream` is a hipStream_t passed as void*; NULL = the library's stream,
+ * which first waits for the work already queued on the default stream, so
+ * inputs written there -- a framework's host-to-device copy -- are seen).
  * The reference-signature wrappers (include/DivQuantHeader.h,
  * include/quant_util.h) are implemented on top of these entry points; an FFI
  * (ctypes, cgo, JNI...) can bind them directly -- see INTEGRATION.md.
