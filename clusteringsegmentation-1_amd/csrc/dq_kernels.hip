@@ -923,7 +923,13 @@ __global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void kpass_kernel(RoundArgs 
     for (int w = 0; w < kBlock / 64; ++w) x += red[w][threadIdx.x];
     __hip_atomic_store(a.parts[blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __syncthreads();   // (every wave's stores drained)
+  // every wave's partial / count stores complete before the workgroup counts
+  // itself in: __syncthreads() alone emits no vmcnt(0) here, and a store
+  // still in flight when the last arriver reads the partials gave it the
+  // previous iteration's value (run-to-run differences with many 2-means
+  // iterations)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0)
     slast = __hip_atomic_fetch_add(a.rdone + (size_t)a.it * a.nn + rec, 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(nd.tile_end - nd.tile_begin) - 1;
@@ -1050,7 +1056,7 @@ __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
 // the next sweep's loads issued before this sweep's work (1) or after it (0;
 // measured 104 vs 108 us per 8 x 4K launch)
 #ifndef DQ_PS_PREFETCH
-#define DQ_PS_PREFETCH 0
+#define DQ_PS_PREFETCH 1
 #endif
 // Cache policy of partsplit's streams (a parent's points are read once, its
 // children's written once): nontemporal loads, store cache-policy bits
@@ -1159,6 +1165,33 @@ struct PlaneRsrc {
   __amdgpu_buffer_rsrc_t r, g, b;
 };
 
+// A buffer offset past every range (< 2^31 bytes + 64): the buffer range
+// check drops the store / returns 0 for the load, so a lane opts out of an
+// access without a branch.
+constexpr uint32_t kOOB = 0xF0000000u;
+
+// This lane's loads of the sweep at vs through buffer resources over the
+// parent's segment (planar: the R, G, B planes; packed: the frame words in
+// r), branch-free: vectors starting at or past `end` read kOOB (zeros).  A
+// planar vector straddling `end` is loaded whole (16 B of slack per shard).
+template <bool PLANAR>
+__device__ __forceinline__ void fetch_sweep_rs(const PlaneRsrc& s, uint32_t vs, uint32_t end, RawSweep& x) {
+  if (PLANAR) {
+    const uint32_t i = vs + 16u * lane_id();
+    const int o = (int)(i < end ? i : kOOB);
+    x.v[0] = __builtin_amdgcn_raw_buffer_load_b128(s.r, o, 0, DQ_PS_NTLOAD ? 2 : 0);
+    x.v[1] = __builtin_amdgcn_raw_buffer_load_b128(s.g, o, 0, DQ_PS_NTLOAD ? 2 : 0);
+    x.v[2] = __builtin_amdgcn_raw_buffer_load_b128(s.b, o, 0, DQ_PS_NTLOAD ? 2 : 0);
+  } else {
+#pragma unroll
+    for (int j = 0; j < kVecPerThread; ++j) {
+      const uint32_t i = vs + 4u * (j * 64 + lane_id());
+      x.v[j] = __builtin_amdgcn_raw_buffer_load_b128(s.r, (int)(i < end ? 4u * i : kOOB), 0,
+                                                     DQ_PS_NTLOAD ? 2 : 0);
+    }
+  }
+}
+
 // A wave's two runs (wave-uniform): child position of staging byte 0, the
 // next staging byte (the new run's region starts at kStageRun), the wave's
 // first position.  The run's next child position is cb + p (- kStageRun).
@@ -1222,33 +1255,45 @@ __device__ __forceinline__ void stage_bytes(const uint8_t* st, const PlaneRsrc& 
   const uint32_t run = (l >> 4) & 1u, i = l & 15u;
   const uint32_t pos = (run ? g.cbn : g.cbo) + i;
   const uint32_t lo = run ? g.lon : g.loo, hi = run ? hi_n : hi_o;
-  if (l < 32u && pos >= lo && pos < hi) {
-    const uint32_t lp = run * kStageRun + i;
-    __builtin_amdgcn_raw_buffer_store_b8(st[lp], d.r, (int)pos, 0, DQ_PS_STORE_AUX);
-    __builtin_amdgcn_raw_buffer_store_b8(st[kStagePlane + lp], d.g, (int)pos, 0, DQ_PS_STORE_AUX);
-    __builtin_amdgcn_raw_buffer_store_b8(st[2 * kStagePlane + lp], d.b, (int)pos, 0, DQ_PS_STORE_AUX);
-  }
+  const uint32_t lp = run * kStageRun + i;   // (lanes 32-63 read a staged byte, store nothing)
+  const uint32_t o = (l < 32u && pos >= lo && pos < hi) ? pos : kOOB;
+  __builtin_amdgcn_raw_buffer_store_b8(st[lp], d.r, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b8(st[kStagePlane + lp], d.g, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b8(st[2 * kStagePlane + lp], d.b, (int)o, 0, DQ_PS_STORE_AUX);
 }
 
-// After a sweep: the completed chunks of both runs, then the partial chunks
-// moved to the front of their regions.
+// Chunk q of a flush (q < nfo: the old run's, else the new run's), stored by
+// every lane: a lane with no chunk, or whose chunk starts below its run's
+// first position (stage_bytes writes that one), stores at kOOB (dropped by
+// the buffer range check).  No branch around the stores: the compiler's
+// vmcnt bookkeeping then sees a fixed count of vector-memory operations per
+// sweep and waits for the prefetched loads only (a data-dependent store
+// count made every wait a vmcnt(0) that drained the sweep's stores too).
+__device__ __forceinline__ void flush_chunk(const uint8_t* st, const PlaneRsrc& d, const Stage& g,
+                                            uint32_t q, uint32_t nfo, uint32_t nf) {
+  const bool run = q >= nfo;
+  const uint32_t k16 = 16u * (run ? q - nfo : q);
+  const uint32_t pos = (run ? g.cbn : g.cbo) + k16;
+  const bool ok = q < nf && pos >= (run ? g.lon : g.loo);
+  const uint32_t lp = ok ? (run ? kStageRun : 0u) + k16 : 0u;
+  const uint32_t o = ok ? pos : kOOB;
+  const u32x4 vr = *reinterpret_cast<const u32x4*>(st + lp);
+  const u32x4 vg = *reinterpret_cast<const u32x4*>(st + kStagePlane + lp);
+  const u32x4 vb = *reinterpret_cast<const u32x4*>(st + 2 * kStagePlane + lp);
+  __builtin_amdgcn_raw_buffer_store_b128(vr, d.r, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(vg, d.g, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(vb, d.b, (int)o, 0, DQ_PS_STORE_AUX);
+}
+
+// After a sweep: the completed chunks of both runs (at most 65: <= 15 + 15
+// staged bytes before the sweep + its 1024), then the partial chunks moved to
+// the front of their regions.
 __device__ __forceinline__ void stage_flush(uint8_t* st, const PlaneRsrc& d, Stage& g, uint32_t l) {
   wave_lds_sync();
   const uint32_t nfo = g.po >> 4, nfn = (g.pn - kStageRun) >> 4;
-  for (uint32_t q = l; q < nfo + nfn; q += 64u) {
-    const bool run = q >= nfo;
-    const uint32_t k16 = 16u * (run ? q - nfo : q);
-    const uint32_t pos = (run ? g.cbn : g.cbo) + k16;
-    const uint32_t lp = (run ? kStageRun : 0u) + k16;
-    if (pos >= (run ? g.lon : g.loo)) {
-      const u32x4 vr = *reinterpret_cast<const u32x4*>(st + lp);
-      const u32x4 vg = *reinterpret_cast<const u32x4*>(st + kStagePlane + lp);
-      const u32x4 vb = *reinterpret_cast<const u32x4*>(st + 2 * kStagePlane + lp);
-      __builtin_amdgcn_raw_buffer_store_b128(vr, d.r, (int)pos, 0, DQ_PS_STORE_AUX);
-      __builtin_amdgcn_raw_buffer_store_b128(vg, d.g, (int)pos, 0, DQ_PS_STORE_AUX);
-      __builtin_amdgcn_raw_buffer_store_b128(vb, d.b, (int)pos, 0, DQ_PS_STORE_AUX);
-    }
-  }
+  const uint32_t nf = nfo + nfn;
+  flush_chunk(st, d, g, l, nfo, nf);
+  if (nf > 64u) flush_chunk(st, d, g, 64u + l, nfo, nf);   // (wave-uniform, rare)
   // a completed first chunk that starts below the wave's first position
   const uint32_t ho = (nfo > 0u && g.cbo < g.loo) ? g.cbo + 16u : 0u;
   const uint32_t hn = (nfn > 0u && g.cbn < g.lon) ? g.cbn + 16u : 0u;
@@ -1329,24 +1374,36 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   g.pn = kStageRun + (nc0 & 15u);
   g.lon = nc0;
 
-  RawSweep x;
+  // the parent's segment (hoisted: a pointer read from the record inside the
+  // loop was re-loaded every sweep behind a vmcnt(0))
+  PlaneRsrc s;
+  {
+    const uint8_t* src = nd.src;
+    const uint32_t ext = nd.off + nd.len;
+    if (PLANAR) {
+      const int nb = (int)(ext + 16u);   // (16 B of slack after every shard)
+      s.r = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, nb, 0x00020000);
+      s.g = __builtin_amdgcn_make_buffer_rsrc((void*)(src + plane), (short)0, nb, 0x00020000);
+      s.b = __builtin_amdgcn_make_buffer_rsrc((void*)(src + 2 * plane), (short)0, nb, 0x00020000);
+    } else {
+      s.r = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(4u * ext), 0x00020000);
+      s.g = s.b = s.r;
+    }
+  }
+  RawSweep x, xn;
   uint32_t vs = start & ~15u;
   bool full = vs >= start && vs + kWaveSweep <= end;
-  if (vs < end) {
-    if (full) fetch_sweep<PLANAR, true, DQ_PS_NTLOAD>(nd.src, plane, vs, end, x);
-    else fetch_sweep<PLANAR, false, DQ_PS_NTLOAD>(nd.src, plane, vs, end, x);
-  }
+  fetch_sweep_rs<PLANAR>(s, vs, end, x);
   while (vs < end) {
-    Sweep sw;
-    unpack_sweep<PLANAR>(x, sw);
     const uint32_t nvs = vs + kWaveSweep;
     const bool nfull = nvs + kWaveSweep <= end;
 #if DQ_PS_PREFETCH
-    if (nvs < end) {   // the next sweep's loads in flight during this one
-      if (nfull) fetch_sweep<PLANAR, true, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
-      else fetch_sweep<PLANAR, false, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
-    }
+    // the next sweep's loads in flight during this one (past the end: kOOB,
+    // no memory access -- a fixed load count per sweep)
+    fetch_sweep_rs<PLANAR>(s, nvs, end, xn);
 #endif
+    Sweep sw;
+    unpack_sweep<PLANAR>(x, sw);
     // the parent's final decision: its cut when proven, else its last 2-means plane
     SweepMask om, nm;
     if (full) {
@@ -1388,11 +1445,10 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     chunk_sweep(cx, oc, g.cbo + g.po, mask_count(xm), ax);
     chunk_sweep(cy, nc, g.cbn + g.pn - kStageRun, mask_count(ym), ay);
     stage_flush(st, d, g, l);
-#if !DQ_PS_PREFETCH
-    if (nvs < end) {
-      if (nfull) fetch_sweep<PLANAR, true, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
-      else fetch_sweep<PLANAR, false, DQ_PS_NTLOAD>(nd.src, plane, nvs, end, x);
-    }
+#if DQ_PS_PREFETCH
+    x = xn;
+#else
+    if (nvs < end) fetch_sweep_rs<PLANAR>(s, nvs, end, x);
 #endif
     vs = nvs;
     full = nfull;
