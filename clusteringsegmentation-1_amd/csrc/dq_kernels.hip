@@ -1063,6 +1063,19 @@ __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
 #ifndef DQ_PS_NTLOAD
 #define DQ_PS_NTLOAD 0
 #endif
+// timing experiments only (wrong results): partsplit stores dropped
+#ifndef DQ_PS_ABLATE_STORE
+#define DQ_PS_ABLATE_STORE 0
+#endif
+#ifndef DQ_PS_ABLATE_STAGE   // staged bytes all to 16 LDS bytes (no bank spread)
+#define DQ_PS_ABLATE_STAGE 0
+#endif
+#ifndef DQ_PS_ABLATE_PART   // no staging / flush / stores at all
+#define DQ_PS_ABLATE_PART 0
+#endif
+#ifndef DQ_PS_ABLATE_SUMS
+#define DQ_PS_ABLATE_SUMS 0
+#endif
 #ifndef DQ_PS_STORE_AUX
 #define DQ_PS_STORE_AUX 0
 #endif
@@ -1214,6 +1227,7 @@ __device__ __forceinline__ void stage_sweep(const Sweep& w, const SweepMask& om,
   const uint32_t exs = ex - g.cbo, eys = ey - g.cbn;
   auto put = [&](int s, uint32_t lp) {
     const int j = s >> 2, sh = 8 * (s & 3);
+    if (DQ_PS_ABLATE_STAGE) lp &= 15u;
     st[lp] = (uint8_t)(w.r[j] >> sh);
     st[kStagePlane + lp] = (uint8_t)(w.g[j] >> sh);
     st[2 * kStagePlane + lp] = (uint8_t)(w.b[j] >> sh);
@@ -1256,7 +1270,7 @@ __device__ __forceinline__ void stage_bytes(const uint8_t* st, const PlaneRsrc& 
   const uint32_t pos = (run ? g.cbn : g.cbo) + i;
   const uint32_t lo = run ? g.lon : g.loo, hi = run ? hi_n : hi_o;
   const uint32_t lp = run * kStageRun + i;   // (lanes 32-63 read a staged byte, store nothing)
-  const uint32_t o = (l < 32u && pos >= lo && pos < hi) ? pos : kOOB;
+  const uint32_t o = (l < 32u && pos >= lo && pos < hi && !DQ_PS_ABLATE_STORE) ? pos : kOOB;
   __builtin_amdgcn_raw_buffer_store_b8(st[lp], d.r, (int)o, 0, DQ_PS_STORE_AUX);
   __builtin_amdgcn_raw_buffer_store_b8(st[kStagePlane + lp], d.g, (int)o, 0, DQ_PS_STORE_AUX);
   __builtin_amdgcn_raw_buffer_store_b8(st[2 * kStagePlane + lp], d.b, (int)o, 0, DQ_PS_STORE_AUX);
@@ -1276,7 +1290,7 @@ __device__ __forceinline__ void flush_chunk(const uint8_t* st, const PlaneRsrc& 
   const uint32_t pos = (run ? g.cbn : g.cbo) + k16;
   const bool ok = q < nf && pos >= (run ? g.lon : g.loo);
   const uint32_t lp = ok ? (run ? kStageRun : 0u) + k16 : 0u;
-  const uint32_t o = ok ? pos : kOOB;
+  const uint32_t o = (ok && !DQ_PS_ABLATE_STORE) ? pos : kOOB;
   const u32x4 vr = *reinterpret_cast<const u32x4*>(st + lp);
   const u32x4 vg = *reinterpret_cast<const u32x4*>(st + kStagePlane + lp);
   const u32x4 vb = *reinterpret_cast<const u32x4*>(st + 2 * kStagePlane + lp);
@@ -1325,6 +1339,146 @@ __device__ __forceinline__ void stage_flush(uint8_t* st, const PlaneRsrc& d, Sta
   wave_lds_sync();
 }
 
+// ---------------------------------------------------------------------------
+// Word staging (DQ_PS_STAGE4, default): one 32-bit word per point in the
+// caller's packed 0x00RRGGBB form instead of one byte per point and plane --
+// one ds_write_b32 per point where the byte form needs three ds_write_b8
+// (LDS instruction issue bounded the byte form: its staging and flush cost
+// as much time as the loads); the flush reads a 16-point chunk with four
+// ds_read_b128 and splits it into the three 16-B plane vectors with
+// unpack_sweep's v_perm form.  Region-relative index i lives at word
+// s4_word(i) = i ^ ((i >> 4) & 12): the 16-B blocks of chunk k are rotated by
+// XOR with (k >> 2) & 3, which makes the flush's ds_read_b128 (one chunk per
+// lane, 64-B stride) conflict-free while a slot's ranked writes (consecutive
+// indices) stay conflict-free inside each chunk.  Index semantics as in the
+// byte form, but both runs' indices are region-relative.
+#ifndef DQ_PS_STAGE4
+#define DQ_PS_STAGE4 0
+#endif
+constexpr uint32_t kS4Run = 1056;                // words per (wave, run) region: 15 + 1024 + slack
+constexpr uint32_t kS4Wave = 2 * kS4Run * 4;     // bytes per wave (old region, new region)
+
+__device__ __forceinline__ uint32_t s4_word(uint32_t i) { return i ^ ((i >> 4) & 12u); }
+
+// slot s of the sweep as a packed word (B in byte 0, G in 1, R in 2)
+__device__ __forceinline__ uint32_t slot_word(const Sweep& w, int s) {
+  const int j = s >> 2, e = s & 3;
+  const uint32_t gb = __builtin_amdgcn_perm(w.g[j], w.b[j], e < 2 ? 0x05010400u : 0x07030602u);   // B G B G
+  return __builtin_amdgcn_perm(w.r[j], gb, (e & 1) ? ((e < 2) ? 0x0C050302u : 0x0C070302u)
+                                                   : ((e < 2) ? 0x0C040100u : 0x0C060100u));
+}
+
+struct Stage4 {
+  uint32_t cbo, cbn, po, pn, loo, lon;   // pn: new-region-relative (the byte form adds kStageRun)
+};
+
+template <bool PRE>
+__device__ __forceinline__ void stage4_sweep(const Sweep& w, const SweepMask& om, const SweepMask& nm, bool full,
+                                             uint32_t* st, Stage4& g, uint32_t l, const SweepMask& xm,
+                                             const SweepMask& ym, uint32_t ex, uint32_t ey, uint32_t& ax,
+                                             uint32_t& ay) {
+  constexpr int kSlots = kVecPerThread * 4;
+  const uint32_t exs = ex - g.cbo, eys = ey - g.cbn;
+  auto put = [&](int s, bool o, uint32_t i) {
+    st[(o ? 0u : kS4Run) + s4_word(i)] = slot_word(w, s);
+    if (PRE) {
+      ax += (uint32_t)(slot_in(xm, s) && i < exs);
+      ay += (uint32_t)(slot_in(ym, s) && i < eys);
+    }
+  };
+  if (full) {   // (wave-uniform)
+    const uint32_t po0 = g.po;
+    uint32_t t = g.pn + l;
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      const bool o = slot_in(om, s);
+      const uint64_t bo = __ballot(o);
+      const uint32_t ro = mbcnt64(bo);
+      put(s, o, o ? g.po + ro : t - ro);
+      const uint32_t co = (uint32_t)__popcll(bo);
+      g.po += co;
+      t += 64u - co;
+    }
+    g.pn += (uint32_t)kWaveSweep - (g.po - po0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+      const bool o = slot_in(om, s), n = slot_in(nm, s);
+      const uint64_t bo = __ballot(o), bn = __ballot(n);
+      if (o || n) put(s, o, o ? g.po + mbcnt64(bo) : g.pn + mbcnt64(bn));
+      g.po += (uint32_t)__popcll(bo);
+      g.pn += (uint32_t)__popcll(bn);
+    }
+  }
+}
+
+// Lanes 0-15 / 16-31 write the staged points i of the old / new run's first
+// chunk whose child positions lie in [max(cb, lo), hi), byte by byte.
+__device__ __forceinline__ void stage4_bytes(const uint32_t* st, const PlaneRsrc& d, const Stage4& g,
+                                             uint32_t hi_o, uint32_t hi_n, uint32_t l) {
+  const uint32_t run = (l >> 4) & 1u, i = l & 15u;
+  const uint32_t pos = (run ? g.cbn : g.cbo) + i;
+  const uint32_t lo = run ? g.lon : g.loo, hi = run ? hi_n : hi_o;
+  const uint32_t v = st[run * kS4Run + s4_word(i)];   // (lanes 32-63 read one, store nothing)
+  const uint32_t o = (l < 32u && pos >= lo && pos < hi && !DQ_PS_ABLATE_STORE) ? pos : kOOB;
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> 16), d.r, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> 8), d.g, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, d.b, (int)o, 0, DQ_PS_STORE_AUX);
+}
+
+// Chunk q of a flush, every lane storing (kOOB: no chunk / a first chunk
+// that stage4_bytes writes), as flush_chunk.
+__device__ __forceinline__ void flush4_chunk(const uint32_t* st, const PlaneRsrc& d, const Stage4& g,
+                                             uint32_t q, uint32_t nfo, uint32_t nf) {
+  const bool run = q >= nfo;
+  const uint32_t k = run ? q - nfo : q;
+  const uint32_t pos = (run ? g.cbn : g.cbo) + 16u * k;
+  const bool ok = q < nf && pos >= (run ? g.lon : g.loo);
+  const uint32_t kk = ok ? k : 0u, key = (kk >> 2) & 3u;
+  const uint32_t* c = st + (run ? kS4Run : 0u) + 16u * kk;
+  RawSweep x;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) x.v[b] = *reinterpret_cast<const u32x4*>(c + 4u * ((uint32_t)b ^ key));
+  Sweep w;
+  unpack_sweep<false>(x, w);
+  const uint32_t o = (ok && !DQ_PS_ABLATE_STORE) ? pos : kOOB;
+  __builtin_amdgcn_raw_buffer_store_b128((u32x4){w.r[0], w.r[1], w.r[2], w.r[3]}, d.r, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128((u32x4){w.g[0], w.g[1], w.g[2], w.g[3]}, d.g, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128((u32x4){w.b[0], w.b[1], w.b[2], w.b[3]}, d.b, (int)o, 0, DQ_PS_STORE_AUX);
+}
+
+__device__ __forceinline__ void stage4_flush(uint32_t* st, const PlaneRsrc& d, Stage4& g, uint32_t l) {
+  wave_lds_sync();
+  const uint32_t nfo = g.po >> 4, nfn = g.pn >> 4;
+  const uint32_t nf = nfo + nfn;
+  flush4_chunk(st, d, g, l, nfo, nf);
+  if (nf > 64u) flush4_chunk(st, d, g, 64u + l, nfo, nf);   // (wave-uniform, rare)
+  const uint32_t ho = (nfo > 0u && g.cbo < g.loo) ? g.cbo + 16u : 0u;
+  const uint32_t hn = (nfn > 0u && g.cbn < g.lon) ? g.cbn + 16u : 0u;
+  if (ho | hn) stage4_bytes(st, d, g, ho, hn, l);
+  if (nfo | nfn) {   // the partial chunks to the front
+    const uint32_t run = (l >> 4) & 1u, i = l & 15u;
+    const uint32_t nfr = run ? nfn : nfo;
+    const bool mv = l < 32u && nfr > 0u;
+    uint32_t v = 0;
+    wave_lds_sync();
+    if (mv) v = st[run * kS4Run + s4_word(16u * nfr + i)];
+    wave_lds_sync();
+    if (mv) st[run * kS4Run + s4_word(i)] = v;
+    g.cbo += 16u * nfo;
+    g.po -= 16u * nfo;
+    g.cbn += 16u * nfn;
+    g.pn -= 16u * nfn;
+  }
+  wave_lds_sync();
+}
+
+#if DQ_PS_STAGE4
+typedef uint32_t StageMem;
+#else
+typedef uint8_t StageMem;
+#endif
+
 // The kernel's loop for one source format of the parent.
 // (records and tiles through global-address-space views: generic pointers
 // read from a PartTile made these flat loads)
@@ -1333,7 +1487,7 @@ typedef const __attribute__((address_space(1))) Tile g_ctile;
 template <bool PLANAR>
 __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g_ctile* tp,
                                               const DevNode* nodes, uint32_t* wparts, uint64_t plane,
-                                              uint8_t* st, SplitSums& so, SplitSums& sn) {
+                                              StageMem* st, SplitSums& so, SplitSums& sn) {
   const uint32_t w = wave_id(), l = lane_id();
   uint32_t start, end;   // this wave's range of the parent tile (wave-uniform)
   wave_range(__builtin_amdgcn_readfirstlane(tp->start), __builtin_amdgcn_readfirstlane(tp->end), w, start, end);
@@ -1366,12 +1520,18 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   ChunkAcc cx, cy;
   chunk_init(cx, nodes, wparts, pt.child[0], oc0);
   chunk_init(cy, nodes, wparts, pt.child[1], nc0);
+#if DQ_PS_STAGE4
+  Stage4 g;
+  constexpr uint32_t kPnOff = 0;   // (new-region-relative indices)
+#else
   Stage g;
+  constexpr uint32_t kPnOff = kStageRun;
+#endif
   g.cbo = oc0 & ~15u;
   g.po = oc0 & 15u;
   g.loo = oc0;
   g.cbn = nc0 & ~15u;
-  g.pn = kStageRun + (nc0 & 15u);
+  g.pn = kPnOff + (nc0 & 15u);
   g.lon = nc0;
 
   // the parent's segment (hoisted: a pointer read from the record inside the
@@ -1394,10 +1554,16 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   uint32_t vs = start & ~15u;
   bool full = vs >= start && vs + kWaveSweep <= end;
   fetch_sweep_rs<PLANAR>(s, vs, end, x);
+#if DQ_PS_PREFETCH == 2
+  RawSweep xnn;
+  fetch_sweep_rs<PLANAR>(s, vs + kWaveSweep, end, xn);
+#endif
   while (vs < end) {
     const uint32_t nvs = vs + kWaveSweep;
     const bool nfull = nvs + kWaveSweep <= end;
-#if DQ_PS_PREFETCH
+#if DQ_PS_PREFETCH == 2
+    fetch_sweep_rs<PLANAR>(s, nvs + kWaveSweep, end, xnn);
+#elif DQ_PS_PREFETCH
     // the next sweep's loads in flight during this one (past the end: kOOB,
     // no memory access -- a fixed load count per sweep)
     fetch_sweep_rs<PLANAR>(s, nvs, end, xn);
@@ -1431,21 +1597,43 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
       xm.m[j] &= om.m[j];   // new for the old child
       ym.m[j] &= nm.m[j];   // new for the new child
     }
-    add_sums_bytes(sw, xm, so);
-    add_sums_bytes(sw, ym, sn);
+    if (!DQ_PS_ABLATE_SUMS) {
+      add_sums_bytes(sw, xm, so);
+      add_sums_bytes(sw, ym, sn);
+    }
     // this wave's points.  A sweep writes at most kWaveSweep points to each
     // child: when neither child's current chunk can end inside it (fast
     // sweep), only the lanes' new counts are kept; otherwise every slot's run
     // is split exactly.
-    const uint32_t oc = g.cbo + g.po, nc = g.cbn + g.pn - kStageRun;
+    const uint32_t oc = g.cbo + g.po, nc = g.cbn + g.pn - kPnOff;
     const bool fast = oc + kWaveSweep <= cx.end && nc + kWaveSweep <= cy.end;
     uint32_t ax = 0, ay = 0;
+    if (DQ_PS_ABLATE_PART) {   // (timing experiment: no partition at all)
+      so.cnt += mask_count(om);
+      sn.cnt += mask_count(nm);
+      x = xn;
+      vs = nvs;
+      full = nfull;
+      continue;
+    }
+#if DQ_PS_STAGE4
+    if (fast) stage4_sweep<false>(sw, om, nm, full, st, g, l, xm, ym, 0u, 0u, ax, ay);
+    else stage4_sweep<true>(sw, om, nm, full, st, g, l, xm, ym, cx.end, cy.end, ax, ay);
+#else
     if (fast) stage_sweep<false>(sw, om, nm, full, st, g, l, xm, ym, 0u, 0u, ax, ay);
     else stage_sweep<true>(sw, om, nm, full, st, g, l, xm, ym, cx.end, cy.end, ax, ay);
+#endif
     chunk_sweep(cx, oc, g.cbo + g.po, mask_count(xm), ax);
-    chunk_sweep(cy, nc, g.cbn + g.pn - kStageRun, mask_count(ym), ay);
+    chunk_sweep(cy, nc, g.cbn + g.pn - kPnOff, mask_count(ym), ay);
+#if DQ_PS_STAGE4
+    stage4_flush(st, d, g, l);
+#else
     stage_flush(st, d, g, l);
-#if DQ_PS_PREFETCH
+#endif
+#if DQ_PS_PREFETCH == 2
+    x = xn;
+    xn = xnn;
+#elif DQ_PS_PREFETCH
     x = xn;
 #else
     if (nvs < end) fetch_sweep_rs<PLANAR>(s, nvs, end, x);
@@ -1453,7 +1641,11 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     vs = nvs;
     full = nfull;
   }
+#if DQ_PS_STAGE4
+  stage4_bytes(st, d, g, g.cbo + g.po, g.cbn + g.pn, l);   // the runs' last partial chunks
+#else
   stage_bytes(st, d, g, g.cbo + g.po, g.cbn + g.pn - kStageRun, l);   // the runs' last partial chunks
+#endif
   chunk_finish(cx);
   chunk_finish(cy);
 }
@@ -1464,8 +1656,13 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
   g_cnode& nd = *(g_cnode*)pt.parent;
   g_ctile* tp = (g_ctile*)pt.tile;
   SplitSums so, sn;
+#if DQ_PS_STAGE4
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kTileWaves * kS4Wave / 4];
+  StageMem* st = stage + wave_id() * (kS4Wave / 4);
+#else
   __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
-  uint8_t* st = stage + wave_id() * kStageWave;
+  StageMem* st = stage + wave_id() * kStageWave;
+#endif
   if (nd.planar) partsplit_run<true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
   else partsplit_run<false>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
 

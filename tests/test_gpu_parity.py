@@ -317,6 +317,26 @@ def test_fixed_point_finalisation_is_exact(gpu):
         gpu.set_planned_rounds(True)
 
 
+def test_repeated_runs_identical(gpu):
+    """Run-to-run determinism under many fused 2-means launches (fixed points
+    off: every node runs all its iterations through kpass_kernel's
+    last-arriver epilogue).  A partial store still in flight when the record's
+    last workgroup summed the partials once made repeated calls differ."""
+    px = fx.load_png_u32(fx.os.path.join(fx.GOLDEN, "png", "batman.png"))[0]
+    try:
+        gpu.set_fixed_point(False)
+        first = None
+        for _ in range(4):
+            out, ct = _quant_dev(gpu, px, 256)
+            got = (out, np.asarray(ct), gpu.last_trace(256).copy())
+            if first is None:
+                first = got
+                continue
+            assert all(np.array_equal(x, y) for x, y in zip(got, first))
+    finally:
+        gpu.set_fixed_point(True)
+
+
 def test_batch_over_lanes(gpu):
     """A batch of frames in one call is split over engine lanes (own stream,
     own host thread each): every frame bit-exact against the oracle, and the

@@ -1,15 +1,22 @@
-# usage: bash tools/prof_variants.sh v1 v2 ... : per-kernel averages (rocprofv3 kernel stats) of
-# `bench.py --lanes 1` for the in-tree library (base) and each variants/<v>/ library
+#!/bin/bash
+# Kernel stats (rocprofv3) of the one-lane bench for library variants built by
+# tools/build_variant.sh: bash tools/prof_variants.sh TAG NAME [NAME ...]
+# ("default" = the in-tree library).  Prints each kernel's average per variant.
 set -e -o pipefail
 export TMPDIR=/tmp
-R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/profv; mkdir -p $O; cd /tmp
-for v in base "$@"; do
-  L=$R/clusteringsegmentation-1_amd/libdivquant_hip.so
-  [ "$v" != base ] && L=$R/clusteringsegmentation-1_amd/variants/$v/libdivquant_hip.so
-  DQ_HIP_LIB=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/$v -o p --output-format csv -- python3 $R/bench.py --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-c3 --no-rowtile --no-verify --no-timing > $O/$v.log 2>&1
-  echo "== $v $(python3 -c "import json;d=json.loads(open('$O/$v.log').read().strip().splitlines()[-1]);print(d['ms_per_step'])" 2>/dev/null)"
-  python3 -c "
-import csv
-for r in list(csv.DictReader(open('$O/$v/p_kernel_stats.csv')))[:9]:
-    print('  %-60s %5s calls %9.1f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs'])/1e3))"
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=$1; shift
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd /tmp
+for v in "$@"; do
+  if [ "$v" = default ]; then unset DQ_HIP_LIB; else export DQ_HIP_LIB=$R/clusteringsegmentation-1_amd/variants/$v.so; fi
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_$v -o k --output-format csv -- python3 $R/bench.py --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-c3 --no-rowtile --no-verify > $O/prof_$v.log 2>&1
+  python3 - $O/prof_$v $v <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True)[0]
+rows = [r for r in csv.DictReader(open(f)) if 'copyBuffer' not in r['Name']]
+print('%-10s ' % sys.argv[2] + '  '.join('%s %.1f' % (r['Name'].split('(')[0].replace('void ', '').replace('dq::', '')[:18],
+      float(r['AverageNs']) / 1e3) for r in rows[:6]))
+PY
 done
