@@ -167,13 +167,25 @@ def map_colors_mps(pixels, colortable):
     return out
 
 
-def quant_varpart_fast(pixels, num_clusters, max_iters=10, device=0, all_pixels_unique=1):
+def quant_varpart_fast(pixels, num_clusters, max_iters=10, device=0, all_pixels_unique=1, num_bits=8,
+                       dec_factor=1, num_rows=1, num_cols=None):
     """quant_varpart_fast (DivQuantCluster.cpp:1099-1179): the non-empty
     cluster colours in cluster-index order (not deduplicated); uniform-weight
-    path, or the weighted one for all_pixels_unique=0."""
+    path, or the weighted one for all_pixels_unique=0; num_bits < 8 /
+    dec_factor > 1 take cut_bits and the decimated colour table over a
+    num_rows x num_cols frame (:1139-1146)."""
     import torch
     _require_gpu()
     px = torch.from_numpy(_u32(pixels).reshape(-1).view(np.int32)).to(f"cuda:{device}")
+    if num_bits != 8 or dec_factor != 1 or num_rows != 1 or (num_cols not in (None, px.numel())):
+        ct = np.zeros(num_clusters, np.uint32)
+        k = ctypes.c_uint32(num_clusters)
+        rc = lib().dq_hip_varpart_dev(device, _dptr(px), px.numel(), num_rows,
+                                      px.numel() if num_cols is None else num_cols, ctypes.byref(k), _ptr(ct),
+                                      num_bits, dec_factor, max_iters, all_pixels_unique, None)
+        if rc < 0:
+            raise DivQuantError("dq_hip_varpart_dev: bad arguments (%d)" % rc)
+        return ct[:k.value].copy()
     if all_pixels_unique:
         ct, _ = cluster_device(px, num_clusters, max_iters=max_iters, device=device)
         return ct

@@ -25,6 +25,7 @@
 #include "../../include/dq_hip.h"
 #include "../../include/quant_util.h"
 #include "dq_engine.h"
+#include "dq_weighted.h"
 
 #include <rccl/rccl.h>
 #include <map>
@@ -201,6 +202,45 @@ int dq_hip_quant_weighted_dev(int device, const uint32_t* d_in, uint32_t n, uint
   e.run_weighted(j, max_iters, d_out != nullptr, dev_stream(e, stream));
   *k = (uint32_t)j.k_out;
   return j.num_empty;
+}
+
+static hipStream_t engine_stream(int device, void* stream);
+
+int dq_hip_varpart_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t rows, uint32_t cols,
+                       uint32_t* k, uint32_t* ct, int num_bits, int dec_factor, int max_iters,
+                       int uniq, void* stream) {
+  if (!d_in || !k || !ct || n == 0 || *k == 0 || max_iters < 1 || num_bits < 1 || num_bits > 8 ||
+      dec_factor < 1 || rows == 0 || cols == 0)
+    return -1;
+  // the reference's index ic + ir*numRows must stay inside the input (:124)
+  const uint64_t nr = (rows + (uint64_t)dec_factor - 1) / dec_factor;
+  const uint64_t nc = (cols + (uint64_t)dec_factor - 1) / dec_factor;
+  if ((nc - 1) * dec_factor + (nr - 1) * dec_factor * (uint64_t)rows >= n) return -2;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  dq::FrameJob j;
+  j.d_in = d_in;
+  j.n = n;
+  j.k = (int)*k;
+  j.ct = ct;
+  j.num_bits = num_bits;
+  j.dec = dec_factor;
+  j.rows = rows;
+  j.cols = cols;
+  if (uniq && num_bits == 8 && dec_factor == 1) e.run(&j, 1, max_iters, false, dev_stream(e, stream));
+  else e.run_weighted(j, max_iters, false, dev_stream(e, stream));
+  *k = (uint32_t)j.k_out;
+  return j.num_empty;
+}
+
+int dq_hip_cut_bits_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out, int nbr,
+                        int nbg, int nbb, void* stream) {
+  if (!d_in || !d_out || nbr < 1 || nbr > 8 || nbg < 1 || nbg > 8 || nbb < 1 || nbb > 8) return -1;
+  if (n == 0) return 0;
+  hipStream_t st = engine_stream(device, stream);
+  dq::launch_cut_gather(d_in, d_out, 1, n, 1, 1, (uint32_t)(8 - nbr), (uint32_t)(8 - nbg),
+                        (uint32_t)(8 - nbb), st);
+  return 0;
 }
 
 int dq_hip_map_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* d_out,
@@ -701,14 +741,10 @@ void quant_varpart_fast(const uint32_t numPixels, const uint32_t* inPixels, uint
                         uint32_t* colortablePtr, const int num_bits, const int dec_factor,
                         const int max_iters, const int allPixelsUnique) {
   (void)tmpPixels;
-  (void)numRows;
-  (void)numCols;
-  if (!validate_num_bits((uchar)num_bits))
+  if (!validate_num_bits((uchar)num_bits))   // (:1115-1118 asserts)
     dq::die("quant_varpart_fast", __FILE__, __LINE__, "invalid num_bits");
-  if (num_bits != 8 || dec_factor != 1)
-    dq::die("quant_varpart_fast", __FILE__, __LINE__,
-            "num_bits != 8 or dec_factor != 1 (cut_bits/decimation path) is out of scope; "
-            "quant_recurse never uses it (quant_util.cpp:31-36)");
+  if (dec_factor <= 0)   // calc_color_table's message (:103-108); the reference then runs on garbage
+    dq::die("quant_varpart_fast", __FILE__, __LINE__, "Decimation factor should be positive");
   if (max_iters < 1)
     dq::die("quant_varpart_fast", __FILE__, __LINE__, "max_iters < 1 is not supported");
   Engine& e = engine_for(current_device());
@@ -720,7 +756,13 @@ void quant_varpart_fast(const uint32_t numPixels, const uint32_t* inPixels, uint
   j.n = numPixels;
   j.k = (int)*numClustersPtr;
   j.ct = colortablePtr;
-  if (allPixelsUnique) e.run(&j, 1, max_iters, false, st);
+  j.num_bits = num_bits;
+  j.dec = dec_factor;
+  j.rows = numRows;
+  j.cols = numCols;
+  // uniform weights only for unique 8-bit undecimated input (:1130-1132);
+  // else calc_color_table (after cut_bits unless !unique && 8 bits, :1133-1146)
+  if (allPixelsUnique && num_bits == 8 && dec_factor == 1) e.run(&j, 1, max_iters, false, st);
   else e.run_weighted(j, max_iters, false, st);
   report_empty(j.num_empty);
   const int k = j.k_out;

@@ -1039,10 +1039,11 @@ void Engine::finish_frame(FrameState& f, bool last) {
         for (int c = 0; c < 3; ++c) last_means[3 * ic + c] = nd.mean[c];
         last_sizes[ic] = (int64_t)nd.glen;
       }
-      if (nd.glen > 0) {
-        const uint32_t R = (uint8_t)(nd.mean[0] + 0.5);
-        const uint32_t G = (uint8_t)(nd.mean[1] + 0.5);
-        const uint32_t B = (uint8_t)(nd.mean[2] + 0.5);
+      if (nd.glen > 0) {   // round, then shift back up (:1030, :1050-1052)
+        const uint32_t sh = (uint32_t)(8 - job.num_bits);
+        const uint32_t R = (uint32_t)(uint8_t)(nd.mean[0] + 0.5) << sh;
+        const uint32_t G = (uint32_t)(uint8_t)(nd.mean[1] + 0.5) << sh;
+        const uint32_t B = (uint32_t)(uint8_t)(nd.mean[2] + 0.5) << sh;
         job.ct[out++] = (R << 16) | (G << 8) | B;
       } else {
         ++empty;
@@ -1263,8 +1264,19 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
   DQ_CHECK(job.nshard == 1 && (job.n_global == 0 || job.n_global == job.n),
            "the weighted path takes whole frames in one process");
   DQ_HIP(hipSetDevice(device_));
+  DQ_CHECK(job.num_bits >= 1 && job.num_bits <= 8 && job.dec >= 1, "num_bits in [1,8], dec_factor >= 1");
   if (!stream) stream = stream_;
-  const uint32_t n = job.n;
+  // calc_color_table's points: every dec-th row and column of the rows x cols
+  // frame (the whole input when dec = 1 and rows = 1), cut to num_bits
+  const uint64_t rows = job.rows ? job.rows : 1, cols = job.cols ? job.cols : job.n;
+  const uint64_t nr = (rows + job.dec - 1) / job.dec, nc = (cols + job.dec - 1) / job.dec;
+  const bool gather = job.num_bits != 8 || job.dec != 1 || rows != 1 || cols != job.n;
+  if (gather) {   // the reference's index ic + ir*numRows must stay inside in[0..n)
+    const uint64_t last = (nc - 1) * job.dec + (nr - 1) * job.dec * rows;
+    DQ_CHECK(last < job.n, "calc_color_table would read past the input (index ic + ir*numRows, :124)");
+    DQ_CHECK(nr * nc <= 0xFFFFFFF0ull, "too many points");
+  }
+  const uint32_t n = gather ? (uint32_t)(nr * nc) : job.n;
   ensure_round(2 * (size_t)job.k + 64, 1024, 0, 0, max_iters, stream);   // staging, results
   // scratch: colour table, unique colours + weights, two id buffers (P0/P1)
   const size_t need_scratch = color_table_scratch_bytes(n);
@@ -1283,10 +1295,17 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     cap_w_ = n;
   }
   ensure_pixels((size_t)n + 4);
-  // norm_factor = 1 / (ceil(numRows / dec) * ceil(numCols / dec)), numRows = 1 (:184)
-  const double norm = 1.0 / (std::ceil(1 / 1.0) * std::ceil((double)n / 1.0));
+  // norm_factor = 1 / (ceil(numRows / dec) * ceil(numCols / dec)) (:184)
+  const double norm = 1.0 / (std::ceil((double)rows / (double)job.dec) * std::ceil((double)cols / (double)job.dec));
+  const uint32_t* pts = job.d_in;
+  if (gather) {   // cut_bits (DivQuantUni.cpp:28-100) + the decimated walk, into P1 (free until the rounds)
+    const uint32_t sh = (uint32_t)(8 - job.num_bits);
+    launch_cut_gather(job.d_in, d_p1_, (uint32_t)nr, (uint32_t)nc, (uint32_t)job.dec, (uint32_t)rows,
+                      sh, sh, sh, stream);
+    pts = d_p1_;
+  }
   uint32_t nu = 0;
-  const int rc = launch_color_table(job.d_in, n, norm, d_wscratch_, cap_wscratch_, d_wcol_, d_ww_, &nu, stream);
+  const int rc = launch_color_table(pts, n, norm, d_wscratch_, cap_wscratch_, d_wcol_, d_ww_, &nu, stream);
   DQ_CHECK(rc == 0, "colour table failed");
   launch_iota(d_p0_, nu, stream);
 

@@ -83,6 +83,13 @@ struct FrameJob {
   int nshard = 1;                    // row ranges of d_in processed as separate shards
   uint32_t width = 0;                // row length: shard boundaries on whole rows (0: any)
   uint64_t n_global = 0;             // points of the whole frame over all processes (0: n)
+  // quant_varpart_fast's cut_bits / decimation inputs (weighted path only,
+  // DivQuantCluster.cpp:1139-1146): channels cut to num_bits, every dec-th
+  // row and column of a rows x cols frame read with the reference's numRows
+  // stride (calc_color_table :124); cols 0: n; centres << (8 - num_bits).
+  int num_bits = 8;
+  int dec = 1;
+  uint32_t rows = 1, cols = 0;
   // outputs
   int k_out = 0;                     // colours written to ct
   int num_empty = 0;                 // empty clusters (:1067-1069)

@@ -36,6 +36,13 @@ struct WArgs {
   int32_t max_iters;
   int32_t fixed_point;
 };
+// cut_bits + calc_color_table's decimated walk (DivQuantUni.cpp:28-100,
+// DivQuantMapColors.cpp:120-125): out[t] for t = a*nc + b (a < nr, b < nc) is
+// in[b*dec + a*dec*stride] with each channel shifted right by sr / sg / sb --
+// the reference's loop order and its numRows stride.  The caller checks that
+// every index lies inside the input.
+void launch_cut_gather(const uint32_t* in, uint32_t* out, uint32_t nr, uint32_t nc, uint32_t dec,
+                       uint32_t stride, uint32_t sr, uint32_t sg, uint32_t sb, hipStream_t stream);
 // dst[i] = i (the root's point ids)
 void launch_iota(uint32_t* dst, uint32_t n, hipStream_t stream);
 // DivQuantCluster<false,*,true>'s split of every node (one workgroup each).

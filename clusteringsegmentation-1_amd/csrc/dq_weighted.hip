@@ -380,6 +380,28 @@ __global__ void iota_kernel(uint32_t* __restrict__ dst, uint32_t n) {
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) dst[i] = i;
 }
 
+// One output point per lane, grid-stride: the row / column split of t is one
+// 32-bit division per point (nr * nc < 2^32); an HBM gather (4 B read at the
+// decimated index, 4 B written), not worth an LDS stage.
+__global__ __launch_bounds__(256) void cut_gather_kernel(const uint32_t* in,
+                                                         uint32_t* out, uint32_t nr,
+                                                         uint32_t nc, uint32_t dec, uint32_t stride,
+                                                         uint32_t sr, uint32_t sg, uint32_t sb) {
+  const uint32_t n = nr * nc;
+  for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < n; t += gridDim.x * 256u) {
+    const uint32_t a = t / nc, b = t - a * nc;
+    const uint64_t i = (uint64_t)b * dec + (uint64_t)a * dec * stride;
+    const uint32_t p = __builtin_nontemporal_load(in + i);
+    out[t] = ((((p >> 16) & 0xFFu) >> sr) << 16) | ((((p >> 8) & 0xFFu) >> sg) << 8) | ((p & 0xFFu) >> sb);
+  }
+}
+
+void launch_cut_gather(const uint32_t* in, uint32_t* out, uint32_t nr, uint32_t nc, uint32_t dec,
+                       uint32_t stride, uint32_t sr, uint32_t sg, uint32_t sb, hipStream_t stream) {
+  if ((uint64_t)nr * nc == 0) return;
+  cut_gather_kernel<<<dim3(grid_for(nr * nc)), dim3(256), 0, stream>>>(in, out, nr, nc, dec, stride, sr, sg, sb);
+}
+
 void launch_iota(uint32_t* dst, uint32_t n, hipStream_t stream) {
   if (n == 0) return;
   iota_kernel<<<dim3(grid_for(n)), dim3(256), 0, stream>>>(dst, n);

@@ -148,6 +148,24 @@ int dq_hip_cluster_dev(int device, const uint32_t *d_in, uint32_t n,
 int dq_hip_quant_weighted_dev(int device, const uint32_t *d_in, uint32_t n,
                               uint32_t *d_out, uint32_t *k, uint32_t *ct,
                               int max_iters, void *stream);
+/* quant_varpart_fast semantics (DivQuantCluster.cpp:1099-1179) on device
+ * pixels for every (num_bits, dec_factor, allPixelsUnique): uniform weights
+ * when uniq && num_bits == 8 && dec_factor == 1, else cut_bits to num_bits
+ * (DivQuantUni.cpp:28-100; skipped when !uniq && num_bits == 8), the
+ * decimated calc_color_table walk over a rows x cols frame with the
+ * reference's numRows stride (DivQuantMapColors.cpp:120-125) and the weighted
+ * clustering, centres shifted back by 8 - num_bits (:1050-1052).  ct gets
+ * the table in cluster-index order (not deduped, not mapped).  Returns the
+ * number of empty clusters, -1 on bad arguments, -2 when the walk would read
+ * past n (the reference reads out of bounds there).  Synchronous on return. */
+int dq_hip_varpart_dev(int device, const uint32_t *d_in, uint32_t n, uint32_t rows,
+                       uint32_t cols, uint32_t *k, uint32_t *ct, int num_bits,
+                       int dec_factor, int max_iters, int uniq, void *stream);
+/* cut_bits (DivQuantUni.cpp:28-100) on device pixels: each channel shifted
+ * right by 8 - its bit count (1..8); d_out may equal d_in.  Stream-ordered. */
+int dq_hip_cut_bits_dev(int device, const uint32_t *d_in, uint32_t n, uint32_t *d_out,
+                        int num_bits_red, int num_bits_green, int num_bits_blue,
+                        void *stream);
 int dq_hip_map_dev(int device, const uint32_t *d_in, uint32_t n,
                    uint32_t *d_out, const uint32_t *ct, int k, void *stream);
 

@@ -353,7 +353,16 @@ int dqo_quant_recurse(uint32_t n, const uint32_t* in, uint32_t* out,
 // G*30013 + B*27011) & 0x7fffffff) % 20023 ascending and, inside a bucket,
 // by first occurrence DESCENDING (chains are prepended, :154-158).  Returns the
 // number of colours.  (numRows = 1, dec_factor = 1: the quant_recurse call.)
+static int color_table_norm(uint32_t n, const uint32_t* in, uint32_t* colours, double* weights,
+                            double norm);
+
 int dqo_color_table(uint32_t n, const uint32_t* in, uint32_t* colours, double* weights) {
+  const double norm = 1.0 / (std::ceil(1 / 1.0) * std::ceil(n / 1.0));   // :184
+  return color_table_norm(n, in, colours, weights, norm);
+}
+
+static int color_table_norm(uint32_t n, const uint32_t* in, uint32_t* colours, double* weights,
+                            double norm) {
   struct E { uint32_t c, first, count, hash; };
   std::unordered_map<uint32_t, uint32_t> at;
   std::vector<E> es;
@@ -370,7 +379,6 @@ int dqo_color_table(uint32_t n, const uint32_t* in, uint32_t* colours, double* w
   std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
     return es[a].hash != es[b].hash ? es[a].hash < es[b].hash : es[a].first > es[b].first;
   });
-  const double norm = 1.0 / (std::ceil(1 / 1.0) * std::ceil(n / 1.0));   // :184
   for (size_t i = 0; i < ord.size(); ++i) {
     colours[i] = es[ord[i]].c;
     weights[i] = norm * es[ord[i]].count;                                  // :195
@@ -380,9 +388,22 @@ int dqo_color_table(uint32_t n, const uint32_t* in, uint32_t* colours, double* w
 
 // DivQuantCluster<false,*,true> restated over (colour, weight) points.
 // Outputs as dqo_cluster; sizes and the trace count points (unique colours).
+// num_bits < 8 (cut_bits input): final centres shifted left by 8 - num_bits
+// (DivQuantCluster.cpp:1030, :1050-1052).
+static int cluster_weighted_bits(uint32_t num_points, const uint32_t* data, const double* wts,
+                                 uint32_t* k_inout, uint32_t* ct, int max_iters, double* means_out,
+                                 int64_t* sizes_out, int64_t* trace_out, int num_bits);
+
 int dqo_cluster_weighted(uint32_t num_points, const uint32_t* data, const double* wts,
                          uint32_t* k_inout, uint32_t* ct, int max_iters, double* means_out,
                          int64_t* sizes_out, int64_t* trace_out) {
+  return cluster_weighted_bits(num_points, data, wts, k_inout, ct, max_iters, means_out, sizes_out,
+                               trace_out, 8);
+}
+
+static int cluster_weighted_bits(uint32_t num_points, const uint32_t* data, const double* wts,
+                                 uint32_t* k_inout, uint32_t* ct, int max_iters, double* means_out,
+                                 int64_t* sizes_out, int64_t* trace_out, int num_bits) {
   if (num_points == 0 || *k_inout == 0 || max_iters < 1) return -1;
   const int K = (int)*k_inout;
   struct P { uint32_t c; double w; };
@@ -504,14 +525,67 @@ int dqo_cluster_weighted(uint32_t num_points, const uint32_t* data, const double
       for (int a = 0; a < 3; ++a) means_out[3 * ic + a] = cl[ic].mean[a];
     if (sizes_out) sizes_out[ic] = cl[ic].size;
     if (cl[ic].size > 0) {
-      const uint32_t R = (uint8_t)(cl[ic].mean[0] + 0.5);
-      const uint32_t G = (uint8_t)(cl[ic].mean[1] + 0.5);
-      const uint32_t B = (uint8_t)(cl[ic].mean[2] + 0.5);
+      const uint32_t sh = (uint32_t)(8 - num_bits);
+      const uint32_t R = (uint32_t)(uint8_t)(cl[ic].mean[0] + 0.5) << sh;
+      const uint32_t G = (uint32_t)(uint8_t)(cl[ic].mean[1] + 0.5) << sh;
+      const uint32_t B = (uint32_t)(uint8_t)(cl[ic].mean[2] + 0.5) << sh;
       ct[out++] = (R << 16) | (G << 8) | B;
     }
   }
   *k_inout = (uint32_t)out;
   return K - out;
+}
+
+// cut_bits restated (DivQuantUni.cpp:28-100): each channel shifted right by
+// 8 - num_bits (the whole-word form at :63-77 gives the same words).
+void dqo_cut_bits(const uint32_t* in, uint32_t n, uint32_t* out, int nbr, int nbg, int nbb) {
+  const uint32_t sr = 8 - nbr, sg = 8 - nbg, sb = 8 - nbb;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t p = in[i];
+    out[i] = ((((p >> 16) & 0xFF) >> sr) << 16) | ((((p >> 8) & 0xFF) >> sg) << 8) | ((p & 0xFF) >> sb);
+  }
+}
+
+// calc_color_table with decimation (DivQuantMapColors.cpp:82-203): the points
+// visited are in[ic + ir*numRows] for ir = 0, dec, .. < numRows (outer) and ic
+// = 0, dec, .. < numCols (inner) -- the reference's numRows stride (:124) kept
+// -- and norm = 1 / (ceil(numRows/dec) * ceil(numCols/dec)) (:184).  Returns
+// the number of colours, or -1 if an index reaches n (the reference reads past
+// its buffer there).
+int dqo_color_table_dec(uint32_t n, const uint32_t* in, uint32_t rows, uint32_t cols, int dec,
+                        uint32_t* colours, double* weights) {
+  if (dec <= 0) return -1;
+  std::vector<uint32_t> seq;
+  for (uint64_t ir = 0; ir < rows; ir += (uint64_t)dec)
+    for (uint64_t ic = 0; ic < cols; ic += (uint64_t)dec) {
+      const uint64_t i = ic + ir * rows;
+      if (i >= n) return -1;
+      seq.push_back(in[i]);
+    }
+  const double norm = 1.0 / (std::ceil(rows / (double)dec) * std::ceil(cols / (double)dec));
+  return color_table_norm((uint32_t)seq.size(), seq.data(), colours, weights, norm);
+}
+
+// quant_varpart_fast restated (DivQuantCluster.cpp:1099-1179) for every
+// (num_bits, dec_factor, allPixelsUnique): the uniform-weight path when
+// allPixelsUnique && num_bits == 8 && dec == 1, else cut_bits (num_bits < 8,
+// or the uniform flag with decimation) + calc_color_table(dec) + the
+// weighted clustering with final centres shifted by 8 - num_bits.
+// Returns the number of empty clusters, or < 0.
+int dqo_quant_varpart(uint32_t n, const uint32_t* in, uint32_t rows, uint32_t cols, uint32_t* k_inout,
+                      uint32_t* ct, int num_bits, int dec, int max_iters, int uniq, double* means_out,
+                      int64_t* sizes_out, int64_t* trace_out) {
+  if (num_bits < 1 || num_bits > 8) return -2;
+  if (uniq && num_bits == 8 && dec == 1)
+    return dqo_cluster(n, in, k_inout, ct, max_iters, means_out, sizes_out, trace_out);
+  std::vector<uint32_t> cut(in, in + n);
+  if (!(!uniq && num_bits == 8)) dqo_cut_bits(in, n, cut.data(), num_bits, num_bits, num_bits);
+  std::vector<uint32_t> colours(n);
+  std::vector<double> w(n);
+  const int u = dqo_color_table_dec(n, cut.data(), rows, cols, dec, colours.data(), w.data());
+  if (u <= 0) return -3;
+  return cluster_weighted_bits((uint32_t)u, colours.data(), w.data(), k_inout, ct, max_iters, means_out,
+                               sizes_out, trace_out, num_bits);
 }
 
 // quant_recurse(..., allPixelsUnique = 0): table, weighted clustering, dedup, map.

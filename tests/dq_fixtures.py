@@ -240,3 +240,41 @@ def make_weighted_case(spec):
     if kind == "coarse":
         return (r[64:64 + n] & 0xC0C0C0).astype(np.uint32)
     raise ValueError(kind)
+
+
+# --------------------------------------------------------------------------
+# quant_varpart_fast's cut_bits / decimation paths (DivQuantCluster.cpp:1130-
+# 1146): num_bits < 8 and/or dec_factor > 1, either flag value.
+# Frame shapes keep the reference's numRows-stride index (calc_color_table
+# :124) inside the buffer: rows == 1, or rows <= cols.
+def varpart_case_specs():
+    specs = []
+    shapes = [(1, 4096), (64, 64), (48, 80), (1, 3001), (33, 57), (128, 128)]
+    kinds = ["uniform", "crop_batman", "crop_cookie", "fewcolours", "tight", "greyramp"]
+    ks = [1, 2, 4, 16, 64, 256]
+    i = 0
+    for nb in range(1, 9):
+        for dec in (1, 2, 3, 5):
+            for uniq in (0, 1):
+                if nb == 8 and dec == 1:
+                    continue   # the plain paths (cases / weighted fixtures)
+                rows, cols = shapes[i % len(shapes)]
+                specs.append({"rows": rows, "cols": cols, "num_bits": nb, "dec": dec, "uniq": uniq,
+                              "k": ks[(i * 7) % len(ks)], "kind": kinds[i % len(kinds)], "seed": 9000 + i,
+                              "max_iters": 10 if i % 5 else 3})
+                i += 1
+    return specs
+
+
+def make_varpart_case(spec):
+    n = spec["rows"] * spec["cols"]
+    kind = spec["kind"]
+    if kind == "uniform":
+        return xorshift(n, seed=spec["seed"])
+    if kind.startswith("crop_"):
+        px, w, h = load_png_u32(os.path.join(GOLDEN, "png", kind[5:] + ".png"))
+        r = xorshift(2, seed=spec["seed"])
+        x0, y0 = int(r[0]) % (w - 128), int(r[1]) % (h - 128)
+        crop = px.reshape(h, w)[y0:y0 + 128, x0:x0 + 128].reshape(-1)
+        return np.ascontiguousarray(crop[:n])
+    return make_weighted_case({"n": n, "kind": kind, "seed": spec["seed"]})

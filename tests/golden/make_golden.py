@@ -22,7 +22,7 @@ do not reproduce (its harness details are not recoverable); the fixtures below
 are regenerated from the reference itself by this script and are the pin.
 
 Fixture files (all data, no code): kats.json, cases.json/.npz, c1.npz,
-big.json/.npz, png.json/.npz, map.json, weighted.json, png/*.png (the two
+big.json/.npz, png.json/.npz, map.json, weighted.json, varpart.json/.npz, png/*.png (the two
 sample images the reference ships in tests/).
 """
 import argparse
@@ -64,6 +64,20 @@ class Ref:
             self.lib.quant_recurse(ctypes.c_uint32(len(px)), fx.vp(px), fx.vp(out),
                                    ctypes.byref(kk), fx.vp(ct), ctypes.c_int(uniq))
         return out, ct[:kk.value].copy(), cap.err
+
+    def varpart(self, px, spec):
+        """quant_varpart_fast (C++ linkage) with the spec's num_bits / dec_factor."""
+        px = np.ascontiguousarray(px, np.uint32)
+        tmp = np.zeros(len(px), np.uint32)
+        ct = np.zeros(spec["k"], np.uint32)
+        kk = ctypes.c_uint32(spec["k"])
+        fn = getattr(self.lib, "_Z18quant_varpart_fastjPKjPjjjS1_S1_iiii")
+        fn.restype = None
+        with Capture() as cap:
+            fn(ctypes.c_uint32(len(px)), fx.vp(px), fx.vp(tmp), ctypes.c_uint32(spec["rows"]),
+               ctypes.c_uint32(spec["cols"]), ctypes.byref(kk), fx.vp(ct), ctypes.c_int(spec["num_bits"]),
+               ctypes.c_int(spec["dec"]), ctypes.c_int(spec["max_iters"]), ctypes.c_int(spec["uniq"]))
+        return ct[:kk.value].copy(), cap.err
 
     def map_colors(self, px, pal):
         px = np.ascontiguousarray(px, np.uint32)
@@ -254,6 +268,24 @@ def main():
         fx.dump_json("weighted2.json", res)
         np.savez_compressed(os.path.join(HERE, "weighted2.npz"), **arrs)
         print("weighted2: %d cases, %d where UW differs" % (len(res), sum(r["uw_differs"] for r in res)))
+
+    # ---- 8c. quant_varpart_fast's cut_bits / decimation paths (num_bits < 8,
+    #        dec_factor > 1): colortable, trace and centroids of the mangled
+    #        C++ entry point (it does not map)
+    if want("varpart"):
+        res, arrs = [], {}
+        for i, spec in enumerate(fx.varpart_case_specs()):
+            px = fx.make_varpart_case(spec)
+            ct, _ = ref.varpart(px, spec)
+            ct2, err = instr.varpart(px, spec)
+            assert np.array_equal(ct, ct2), "instrumented build diverged"
+            trace, means = parse_instr(err, spec["k"])
+            res.append(dict(spec=spec, n_px=int(len(px)), ct=[int(v) for v in ct], k_out=int(len(ct))))
+            arrs["trace_%d" % i] = trace.astype(np.int32)
+            arrs["means_%d" % i] = means
+        fx.dump_json("varpart.json", res)
+        np.savez_compressed(os.path.join(HERE, "varpart.npz"), **arrs)
+        print("varpart: %d cases" % len(res))
 
     # ---- 9. C4 at size: the 64 distinct 4K frames of the batch (frame f uses
     #      seed SEED + f) -- hash, colortable, trace of every frame

@@ -423,6 +423,79 @@ def test_cpp_linkage_entry_points(gpu):
         assert dd == c["ct"], (i, spec)
 
 
+def test_varpart_cut_bits_decimation(gpu):
+    """quant_varpart_fast's cut_bits / decimation paths (SURVEY 8f.4,
+    DivQuantCluster.cpp:1130-1146) through the mangled C++ symbol, against
+    the reference's colortables for num_bits 1..8 x dec_factor {1,2,3,5} x
+    allPixelsUnique (62 cases, rows x cols frames with the numRows-stride
+    walk); the device entry dq_hip_varpart_dev also against the reference's
+    split traces and centroid doubles."""
+    import torch
+    L = gpu.lib()
+    qvf = getattr(L, "_Z18quant_varpart_fastjPKjPjjjS1_S1_iiii")
+    qvf.restype = None
+    qvf.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.dq_hip_varpart_dev.restype = ctypes.c_int
+    L.dq_hip_varpart_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    cases = fx.load_json("varpart.json")
+    arrs = fx.load_npz("varpart.npz")
+    for i, c in enumerate(cases):
+        s = c["spec"]
+        px = fx.make_varpart_case(s)
+        tmp = np.zeros_like(px)
+        k = ctypes.c_uint32(s["k"])
+        ct = np.zeros(s["k"], np.uint32)
+        qvf(len(px), fx.vp(px), fx.vp(tmp), s["rows"], s["cols"], ctypes.cast(ctypes.pointer(k), ctypes.c_void_p),
+            fx.vp(ct), s["num_bits"], s["dec"], s["max_iters"], s["uniq"])
+        assert [int(v) for v in ct[:k.value]] == c["ct"], (i, s)
+        d = torch.from_numpy(px.view(np.int32)).cuda()
+        k2 = ctypes.c_uint32(s["k"])
+        ct2 = np.zeros(s["k"], np.uint32)
+        rc = L.dq_hip_varpart_dev(0, d.data_ptr(), len(px), s["rows"], s["cols"],
+                                  ctypes.cast(ctypes.pointer(k2), ctypes.c_void_p), fx.vp(ct2), s["num_bits"],
+                                  s["dec"], s["max_iters"], s["uniq"], None)
+        assert rc >= 0 and [int(v) for v in ct2[:k2.value]] == c["ct"], (i, s)
+        if s["k"] > 1:
+            means, sizes = gpu.last_centroids(s["k"])
+            trace = gpu.last_trace(s["k"])
+            assert np.array_equal(trace, arrs["trace_%d" % i]), (i, s)
+            ref = arrs["means_%d" % i]
+            filled = ~np.isnan(ref[:, 0])
+            assert np.array_equal(filled, sizes > 0), (i, s)
+            assert np.array_equal(means[filled].view(np.uint64), ref[filled].view(np.uint64)), (i, s)
+    # a walk that would read past the input is refused (-2), not run
+    d = torch.zeros(48 * 80, dtype=torch.int32, device="cuda")
+    k3 = ctypes.c_uint32(4)
+    ct3 = np.zeros(4, np.uint32)
+    assert L.dq_hip_varpart_dev(0, d.data_ptr(), 48 * 80, 80, 48, ctypes.cast(ctypes.pointer(k3), ctypes.c_void_p),
+                                fx.vp(ct3), 8, 1, 10, 0, None) == -2
+
+
+def test_cut_bits_device(gpu):
+    """dq_hip_cut_bits_dev against the oracle's cut_bits restatement (equal and
+    per-channel bit counts, in place and out of place)."""
+    import torch
+    L = gpu.lib()
+    L.dq_hip_cut_bits_dev.restype = ctypes.c_int
+    px = fx.xorshift(1000003, seed=99) | np.uint32(0x5A000000)
+    for nbr, nbg, nbb in [(8, 8, 8), (5, 5, 5), (1, 1, 1), (3, 6, 7), (8, 2, 4)]:
+        want = np.zeros_like(px)
+        fx.oracle().dqo_cut_bits(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(want), nbr, nbg, nbb)
+        d = torch.from_numpy(px.view(np.int32)).cuda()
+        o = torch.empty_like(d)
+        assert L.dq_hip_cut_bits_dev(0, ctypes.c_void_p(d.data_ptr()), ctypes.c_uint32(len(px)),
+                                     ctypes.c_void_p(o.data_ptr()), nbr, nbg, nbb, None) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want), (nbr, nbg, nbb)
+        assert L.dq_hip_cut_bits_dev(0, ctypes.c_void_p(d.data_ptr()), ctypes.c_uint32(len(px)),
+                                     ctypes.c_void_p(d.data_ptr()), nbr, nbg, nbb, None) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(d.cpu().numpy().view(np.uint32), want), ("in place", nbr, nbg, nbb)
+
+
 def test_planned_rounds_equal_host_rounds(gpu):
     """Device-planned (speculative) rounds against host-planned rounds only:
     identical colortables, label maps, traces and centroid doubles, on

@@ -238,3 +238,59 @@ def test_color_table_matches_reference():
         assert u == c["num_colors"]
         assert [int(v) for v in col[:u]] == c["colors"]
         assert [float(x).hex() for x in w[:u]] == c["weights"]
+
+
+def oracle_varpart(px, spec):
+    """dqo_quant_varpart: quant_varpart_fast restated for any (num_bits, dec_factor)."""
+    k = spec["k"]
+    px = np.ascontiguousarray(px, np.uint32)
+    ct = np.zeros(k, np.uint32)
+    kk = ctypes.c_uint32(k)
+    means = np.zeros((k, 3), np.float64)
+    sizes = np.zeros(k, np.int64)
+    trace = np.zeros((max(k - 1, 1), 4), np.int64)
+    rc = fx.oracle().dqo_quant_varpart(
+        ctypes.c_uint32(len(px)), fx.vp(px), ctypes.c_uint32(spec["rows"]), ctypes.c_uint32(spec["cols"]),
+        ctypes.byref(kk), fx.vp(ct), ctypes.c_int(spec["num_bits"]), ctypes.c_int(spec["dec"]),
+        ctypes.c_int(spec["max_iters"]), ctypes.c_int(spec["uniq"]), fx.vp(means), fx.vp(sizes), fx.vp(trace))
+    assert rc >= 0, rc
+    return ct[:kk.value], means, sizes, trace[:k - 1]
+
+
+def test_varpart_fixtures():
+    """cut_bits / decimation: the oracle's quant_varpart_fast
+    restatement against the reference's colortables, split traces and double
+    centroids for num_bits 1..8 x dec_factor {1,2,3,5} x allPixelsUnique."""
+    cases = fx.load_json("varpart.json")
+    arrs = fx.load_npz("varpart.npz")
+    assert len(cases) == 62
+    for i, c in enumerate(cases):
+        s = c["spec"]
+        px = fx.make_varpart_case(s)
+        assert len(px) == c["n_px"]
+        ct, means, sizes, trace = oracle_varpart(px, s)
+        assert [int(v) for v in ct] == c["ct"], (i, s)
+        if s["k"] > 1:
+            assert np.array_equal(trace, arrs["trace_%d" % i]), (i, s)
+        ref = arrs["means_%d" % i]
+        filled = ~np.isnan(ref[:, 0])
+        if s["k"] > 1:
+            assert np.array_equal(filled, sizes > 0), (i, s)
+            assert np.array_equal(means[filled].view(np.uint64), ref[filled].view(np.uint64)), (i, s)
+
+
+def test_cut_bits_restatement():
+    """dqo_cut_bits against the reference's whole-word form (DivQuantUni.cpp:63-77)
+    and per-channel form (:78-93), restated in numpy."""
+    px = fx.xorshift(5000, seed=77) | np.uint32(0xAB000000)
+    for nb in range(1, 9):
+        sh = 8 - nb
+        bm = (0xFF >> sh) << sh
+        want = ((px & np.uint32((bm << 16) | (bm << 8) | bm)) >> np.uint32(sh)).astype(np.uint32)
+        got = np.zeros_like(px)
+        fx.oracle().dqo_cut_bits(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(got), nb, nb, nb)
+        assert np.array_equal(got, want), nb
+    got = np.zeros_like(px)
+    fx.oracle().dqo_cut_bits(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(got), 3, 5, 7)
+    want = (((px >> 16) & 0xFF) >> 5) << 16 | (((px >> 8) & 0xFF) >> 3) << 8 | ((px & 0xFF) >> 1)
+    assert np.array_equal(got, want.astype(np.uint32))
