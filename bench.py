@@ -86,6 +86,7 @@ def parse():
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline region")
     ap.add_argument("--no-c3", action="store_true", help="skip the single-frame C3 measurement")
     ap.add_argument("--no-rowtile", action="store_true", help="skip the C4 row-tile measurement")
+    ap.add_argument("--no-bgr", action="store_true", help="skip the BGR24-input measurements")
     ap.add_argument("--no-verify", action="store_true", help="skip the golden-fixture check")
     ap.add_argument("--lanes", type=int, default=0,
                     help="engine lanes per batch (0: library default); the roofline region always uses 1")
@@ -412,6 +413,50 @@ def main():
               "workload": "one %dx%d frame per call (C3), %d rank(s)" % (w, h, world),
               "verified": ok1}
 
+    # --- the same frames as OpenCV BGR24 Mats: read directly by
+    # the root's passes, partition and map (3 B per pixel, no packing pass);
+    # one frame per call (C3 shape) and the rank's batch in one call
+    bgr = None
+    if a.mode == "frames" and not a.no_bgr and nf > 1:
+        bf = []
+        for t in frames:
+            p = t.view(torch.int32)
+            bf.append(torch.stack([p & 0xFF, (p >> 8) & 0xFF, (p >> 16) & 0xFF], -1).to(torch.uint8).reshape(-1))
+        lastb = {}
+
+        def bone():
+            lastb["ct"], _ = pkg.quant_bgr24_device(bf[0], w, h, outs[0], k, device=local, stream=stream)
+
+        def bbatch():
+            lastb["cts"], _ = pkg.quant_bgr24_batch_device(bf, w, h, outs, k, device=local, stream=stream)
+        for _ in range(2):
+            bone()
+        dtb1 = max_over_ranks(timed_region(bone, a.steps, world, sync), world, dev)
+        okb1 = None
+        if not a.no_verify:
+            sync()
+            okb1 = all_ranks_ok(check_frame(pkg, outs[0], lastb["ct"], frame_fixture(w, h, k, ids[0])) is not False,
+                                world, dev)
+        for _ in range(2):
+            bbatch()
+        dtb = max_over_ranks(timed_region(bbatch, a.steps, world, sync), world, dev)
+        okb = None
+        if not a.no_verify:
+            sync()
+            okb = all_ranks_ok(all(check_frame(pkg, outs[i], lastb["cts"][i], frame_fixture(w, h, k, ids[i]))
+                                   is not False for i in range(nf)), world, dev)
+        if okb1 is False or okb is False:
+            print(json.dumps({"error": "BGR24-input outputs differ from the reference fixtures"}), flush=True)
+            sys.exit(3)
+        bgr = {"c3_ms_per_frame": round(dtb1 * 1e3 / a.steps, 3),
+               "c3_Mpix_per_s": round(n * world * a.steps / dtb1 / 1e6, 2),
+               "batch_ms_per_step": round(dtb * 1e3 / a.steps, 3),
+               "batch_Mpix_per_s": round(n * nf * world * a.steps / dtb / 1e6, 2),
+               "workload": "the same frames as BGR24 (CV_8UC3) device buffers: one frame per call, and %d frames "
+                           "per rank in one batched call (dq_hip_quant_bgr24[_batch]_dev)" % nf,
+               "verified": None if okb is None else bool(okb1 and okb)}
+        del bf
+
     # --- C4 row-tile variant: all 64 frames, each row-sharded over the ranks
     rowtile = None
     if a.mode == "frames" and not a.no_rowtile and (w, h, k) == (3840, 2160, 256):
@@ -484,6 +529,7 @@ def main():
                        "rounds_last_frame": rounds, "points_swept_last_call": swept,
                        "points_full_iterations_last_call": full,
                        "c3": c3,
+                       "bgr24_input": bgr,
                        "c4_rowtile": rowtile,
                        "kernels": {kname: {"launches": v[0], "ms": round(v[1], 3),
                                            "GBps": round(v[2] / (v[1] / 1e3) / 1e9, 1) if v[1] > 0 and v[2] > 0 else None}

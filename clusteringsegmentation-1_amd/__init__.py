@@ -102,6 +102,15 @@ def lib():
         "dq_hip_unpack_bgr24_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp, vp],
                                     c.c_int),
         "dq_hip_gather_bgr24_dev": ([c.c_int, vp, c.c_uint32, vp, c.c_uint32, vp, vp], c.c_int),
+        "dq_hip_varpart_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, u32p, vp, c.c_int, c.c_int,
+                                c.c_int, c.c_int, vp], c.c_int),
+        "dq_hip_cut_bits_dev": ([c.c_int, vp, c.c_uint32, vp, c.c_int, c.c_int, c.c_int, vp], c.c_int),
+        "dq_hip_quant_bgr24_batch_dev": ([c.c_int, c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp,
+                                          c.c_uint32, vp, vp, c.c_int, c.c_int, vp], c.c_int),
+        "dq_hip_quant_bgr24_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp, u32p, vp, c.c_int,
+                                    c.c_int, vp], c.c_int),
+        "dq_hip_map_bgr24_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp, vp, c.c_int, vp],
+                                 c.c_int),
         "quant_recurse": ([c.c_uint32, vp, vp, u32p, vp, c.c_int], None),
     }
     for name, (args, res) in sigs.items():
@@ -246,6 +255,42 @@ def quant_batch_device(t_ins, t_outs, num_clusters, max_iters=10, device=0, stre
     if r < 0:
         raise DivQuantError("dq_hip_quant_batch_dev: bad arguments")
     return [ct[i, :kout[i]].copy() for i in range(nf)], r
+
+
+def quant_bgr24_batch_device(t_bgrs, width, height, t_outs, num_clusters, stride=None, max_iters=10,
+                             device=0, stream=None, all_pixels_unique=1):
+    """quant_recurse of device BGR24 frames (OpenCV CV_8UC3 rows), read
+    directly by the root's passes, partition and map; outputs
+    packed colours.  Returns ([colortable per frame], total_empty)."""
+    nf = len(t_bgrs)
+    stride = 3 * width if stride is None else stride
+    ins = (ctypes.c_void_p * nf)(*[_dptr(t).value for t in t_bgrs])
+    outs = (ctypes.c_void_p * nf)(*[_dptr(t).value for t in t_outs])
+    ct = np.zeros((nf, num_clusters), np.uint32)
+    kout = np.zeros(nf, np.uint32)
+    r = lib().dq_hip_quant_bgr24_batch_dev(device, nf, ctypes.cast(ins, ctypes.c_void_p), width, height, stride,
+                                           ctypes.cast(outs, ctypes.c_void_p), num_clusters, _ptr(ct), _ptr(kout),
+                                           all_pixels_unique, max_iters, _stream_ptr(stream))
+    if r < 0:
+        raise DivQuantError("dq_hip_quant_bgr24_batch_dev: bad arguments")
+    return [ct[i, :kout[i]].copy() for i in range(nf)], r
+
+
+def quant_bgr24_device(t_bgr, width, height, t_out, num_clusters, stride=None, max_iters=10, device=0,
+                       stream=None, all_pixels_unique=1):
+    """quant_recurse of one device BGR24 frame; returns (colortable, empty)."""
+    cts, r = quant_bgr24_batch_device([t_bgr], width, height, [t_out], num_clusters, stride, max_iters, device,
+                                      stream, all_pixels_unique)
+    return cts[0], r
+
+
+def map_bgr24_device(t_bgr, width, height, t_out, colortable, stride=None, device=0, stream=None):
+    """map_colors_mps of a device BGR24 frame into packed colours."""
+    stride = 3 * width if stride is None else stride
+    ct = _u32(colortable)
+    if lib().dq_hip_map_bgr24_dev(device, _dptr(t_bgr), width, height, stride, _dptr(t_out), _ptr(ct), len(ct),
+                                  _stream_ptr(stream)) < 0:
+        raise DivQuantError("dq_hip_map_bgr24_dev: bad arguments")
 
 
 def quant_rows_device(t_ins, t_outs, num_clusters, widths=None, n_globals=None, nshard=1,

@@ -320,21 +320,10 @@ int dq_hip_gather_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t stride,
   return 0;
 }
 
-int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
-                           const uint32_t* n, uint32_t* const* d_out, uint32_t k,
-                           uint32_t* ct, uint32_t* k_out, int max_iters, void* stream) {
-  if (nframes <= 0 || !d_in || !n || !d_out || !ct || !k_out || k == 0 || max_iters < 1)
-    return -1;
-  for (int i = 0; i < nframes; ++i)
-    if (!d_in[i] || !d_out[i] || n[i] == 0) return -1;
-  std::vector<dq::FrameJob> jobs(nframes);
-  for (int i = 0; i < nframes; ++i) {
-    jobs[i].d_in = d_in[i];
-    jobs[i].n = n[i];
-    jobs[i].d_out = d_out[i];
-    jobs[i].k = (int)k;
-    jobs[i].ct = ct + (size_t)i * k;
-  }
+// The uniform-weight batch over the engine lanes (frames split over the
+// lanes' engines and streams).
+static int quant_batch(int device, std::vector<dq::FrameJob>& jobs, int max_iters, void* stream) {
+  const int nframes = (int)jobs.size();
   const int lanes = std::min(nframes, dq::batch_lanes());
   Engine& e0 = engine_for(device);
   if (lanes <= 1) {
@@ -381,11 +370,106 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
     e0.last_points_full = full;
   }
   int empty = 0;
-  for (int i = 0; i < nframes; ++i) {
-    k_out[i] = (uint32_t)jobs[i].k_out;
-    empty += jobs[i].num_empty;
-  }
+  for (int i = 0; i < nframes; ++i) empty += jobs[i].num_empty;
   return empty;
+}
+
+int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t* const* d_in,
+                           const uint32_t* n, uint32_t* const* d_out, uint32_t k,
+                           uint32_t* ct, uint32_t* k_out, int max_iters, void* stream) {
+  if (nframes <= 0 || !d_in || !n || !d_out || !ct || !k_out || k == 0 || max_iters < 1)
+    return -1;
+  for (int i = 0; i < nframes; ++i)
+    if (!d_in[i] || !d_out[i] || n[i] == 0) return -1;
+  std::vector<dq::FrameJob> jobs(nframes);
+  for (int i = 0; i < nframes; ++i) {
+    jobs[i].d_in = d_in[i];
+    jobs[i].n = n[i];
+    jobs[i].d_out = d_out[i];
+    jobs[i].k = (int)k;
+    jobs[i].ct = ct + (size_t)i * k;
+  }
+  const int empty = quant_batch(device, jobs, max_iters, stream);
+  for (int i = 0; i < nframes; ++i) k_out[i] = (uint32_t)jobs[i].k_out;
+  return empty;
+}
+
+int dq_hip_quant_bgr24_batch_dev(int device, int nframes, const uint8_t* const* d_bgr, uint32_t width,
+                                 uint32_t height, uint32_t stride, uint32_t* const* d_out, uint32_t k,
+                                 uint32_t* ct, uint32_t* k_out, int uniq, int max_iters, void* stream) {
+  if (nframes <= 0 || !d_bgr || !d_out || !ct || !k_out || k == 0 || max_iters < 1 ||
+      !bgr24_shape_ok(width, height, stride))
+    return -1;
+  for (int i = 0; i < nframes; ++i)
+    if (!d_bgr[i] || !d_out[i]) return -1;
+  const uint32_t n = width * height;
+  if (!uniq || stride != 3 * width) {
+    // the weighted path's colour table (and padded rows) take packed pixels:
+    // Vec3BToUID on the GPU into a scratch frame, then the packed entries
+    int empty = 0;
+    for (int i = 0; i < nframes; ++i) {
+      uint32_t* px = nullptr;
+      hipStream_t st = engine_stream(device, stream);
+      DQ_HIP(hipMallocAsync((void**)&px, (size_t)n * 4 + 16, st));
+      dq::launch_bgr24_pack(d_bgr[i], width, height, stride, px, st);
+      uint32_t kk = k;
+      int r;
+      if (uniq) {
+        const uint32_t* pin = px;
+        r = dq_hip_quant_batch_dev(device, 1, &pin, &n, &d_out[i], k, ct + (size_t)i * k, &kk, max_iters, stream);
+      } else {
+        r = dq_hip_quant_weighted_dev(device, px, n, d_out[i], &kk, ct + (size_t)i * k, max_iters, stream);
+      }
+      DQ_HIP(hipFreeAsync(px, st));
+      if (r < 0) return r;
+      k_out[i] = kk;
+      empty += r;
+    }
+    return empty;
+  }
+  std::vector<dq::FrameJob> jobs(nframes);
+  for (int i = 0; i < nframes; ++i) {
+    jobs[i].d_in = reinterpret_cast<const uint32_t*>(d_bgr[i]);
+    jobs[i].bgr = true;
+    jobs[i].n = n;
+    jobs[i].d_out = d_out[i];
+    jobs[i].k = (int)k;
+    jobs[i].ct = ct + (size_t)i * k;
+  }
+  const int empty = quant_batch(device, jobs, max_iters, stream);
+  for (int i = 0; i < nframes; ++i) k_out[i] = (uint32_t)jobs[i].k_out;
+  return empty;
+}
+
+int dq_hip_quant_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t width, uint32_t height,
+                           uint32_t stride, uint32_t* d_out, uint32_t* k, uint32_t* ct, int uniq,
+                           int max_iters, void* stream) {
+  if (!k || *k == 0) return -1;
+  uint32_t kk = 0;
+  const int r = dq_hip_quant_bgr24_batch_dev(device, 1, &d_bgr, width, height, stride, &d_out, *k, ct, &kk,
+                                             uniq, max_iters, stream);
+  if (r >= 0) *k = kk;
+  return r;
+}
+
+int dq_hip_map_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t width, uint32_t height,
+                         uint32_t stride, uint32_t* d_out, const uint32_t* ct, int k, void* stream) {
+  if (!d_bgr || !d_out || !ct || k <= 0 || !bgr24_shape_ok(width, height, stride)) return -1;
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  hipStream_t st = dev_stream(e, stream);
+  if (stride != 3 * width) {   // padded rows: packed first
+    uint32_t* px = nullptr;
+    const uint32_t n = width * height;
+    DQ_HIP(hipMallocAsync((void**)&px, (size_t)n * 4 + 16, st));
+    dq::launch_bgr24_pack(d_bgr, width, height, stride, px, st);
+    e.map(px, n, d_out, ct, k, st);
+    DQ_HIP(hipFreeAsync(px, st));
+    return 0;
+  }
+  Engine::MapJob j{reinterpret_cast<const uint32_t*>(d_bgr), width * height, d_out, ct, k, true};
+  e.map_many(&j, 1, st);
+  return 0;
 }
 
 int dq_hip_quant_rows_dev(int device, int nframes, const uint32_t* const* d_in,

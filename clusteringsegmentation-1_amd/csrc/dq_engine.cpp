@@ -36,6 +36,9 @@ constexpr int BUF_IN = 0, BUF_P0 = 1, BUF_P1 = 2;
 inline int child_buf(int b) { return b == BUF_P0 ? BUF_P1 : BUF_P0; }
 inline size_t align4(size_t x) { return (x + 3) & ~(size_t)3; }
 inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+// words of an aligned BGR24 copy of n points: whole 16-point vectors + slack,
+// a multiple of 4 words (the next copy starts 16-B aligned)
+inline size_t bgr_words(size_t n) { return ((3 * align16(n) + 64) / 4 + 3) & ~(size_t)3; }
 
 // Split-pass threshold (:473): cut_pos < v <=> v >= thr for integer v.
 int32_t split_threshold(double cut) {
@@ -469,7 +472,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
       DevNode& d = hn[a * S + sh];
       d.src = buf_ptr(n.buf, fs, sh);
       d.dst = const_cast<uint8_t*>(buf_ptr(child_buf(n.buf), fs, sh));
-      d.planar = n.buf != BUF_IN;
+      d.planar = n.buf != BUF_IN ? SRC_PLANAR : (fs.job->bgr ? SRC_BGR24 : SRC_PACKED);
       const Seg& sg = seg(order[a], sh);
       d.off = sg.off;
       d.len = sg.len;
@@ -1082,6 +1085,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     DQ_CHECK(j.n_global == 0 || j.n_global >= j.n, "n_global < n");
     DQ_CHECK(j.n_global == 0 || j.n_global == j.n || comm_ != nullptr,
              "n_global > n needs a communicator (dq_hip_comm_init)");
+    DQ_CHECK(!j.bgr || (S == 1 && (j.n_global == 0 || j.n_global == j.n)), "BGR24 frames are one shard");
     FrameState& f = frames_[i];
     f.job = &j;
     // shard boundaries: whole rows when the width is known, else 4-point multiples
@@ -1103,7 +1107,11 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
       f.base[sh] = (uint32_t)total;
       total += align16(f.n[sh]) + 16;
       const uint32_t* p = j.d_in + f.first[sh];
-      if (((uintptr_t)p & 15) != 0 || (f.n[sh] & 3) != 0) align_need += align4(f.n[sh]) + 4;
+      if (j.bgr) {   // 48-B sweep vectors: 16-B aligned, no vector past the frame's end
+        if (((uintptr_t)j.d_in & 15) != 0 || (j.n & 15) != 0) align_need += bgr_words(j.n);
+      } else if (((uintptr_t)p & 15) != 0 || (f.n[sh] & 3) != 0) {
+        align_need += align4(f.n[sh]) + 4;
+      }
     }
   }
   DQ_CHECK(total < (1ull << 32), "batch larger than 2^32 points");
@@ -1130,7 +1138,20 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     root.w = 1.0;          // :329
     root.glen = ng;
     root.buf = BUF_IN;
-    for (int sh = 0; sh < S; ++sh) {
+    if (j.bgr) {
+      f.in[0] = j.d_in;
+      if (((uintptr_t)j.d_in & 15) != 0 || (j.n & 15) != 0) {   // aligned copy, zero tail to 16 points
+        const size_t w = bgr_words(j.n);
+        uint8_t* dst = reinterpret_cast<uint8_t*>(d_align_ + aoff);
+        DQ_HIP(hipMemcpyAsync(dst, j.d_in, (size_t)j.n * 3, hipMemcpyDeviceToDevice, stream));
+        DQ_HIP(hipMemsetAsync(dst + (size_t)j.n * 3, 0, w * 4 - (size_t)j.n * 3, stream));
+        f.in[0] = d_align_ + aoff;
+        aoff += w;
+      }
+      root_seg[0].off = 0;
+      root_seg[0].len = f.n[0];
+    }
+    for (int sh = 0; sh < S && !j.bgr; ++sh) {
       const uint32_t* p = j.d_in + f.first[sh];
       f.in[sh] = p;
       if (((uintptr_t)p & 15) != 0 || (f.n[sh] & 3) != 0) {   // 16-B loads may read up to align4(n)
@@ -1231,7 +1252,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
       j.k_out = m;
       if (j.d_out)   // every shard's rows with the frame's palette
         for (int sh = 0; sh < S; ++sh)
-          if (f.n[sh] > 0) mj.push_back(MapJob{f.in[sh], f.n[sh], j.d_out + f.first[sh], j.ct, m});
+          if (f.n[sh] > 0) mj.push_back(MapJob{f.in[sh], f.n[sh], j.d_out + f.first[sh], j.ct, m, j.bgr});
     }
     if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream);
   }
@@ -1548,6 +1569,47 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     DQ_CHECK(jobs[i].k > 0, "colormapSize must be > 0 (DivQuantMapColors.cpp:264)");
     DQ_CHECK(jobs[i].k <= (int)kMapPal, "colormapSize > 16384 is not supported by the LDS palette");
   }
+  // BGR24 frames: map_lds_kernel reads them directly (K <= 1024, 8-B aligned
+  // in, 16-B aligned out); otherwise they are packed first (bgr24_pack)
+  std::vector<MapJob> packed;
+  {
+    int kmax_all = 0;
+    bool any_bgr = false, any_staged = false;   // (a staged chunk runs map_kernel task by task)
+    bool all_bgr = true;                        // (one launch maps one pixel format)
+    for (int i = 0; i < njobs; ++i) {
+      kmax_all = std::max(kmax_all, jobs[i].k);
+      any_bgr |= jobs[i].bgr;
+      all_bgr &= jobs[i].bgr;
+      any_staged |= !jobs[i].bgr && (((uintptr_t)jobs[i].d_in & 15) != 0 || ((uintptr_t)jobs[i].d_out & 15) != 0);
+    }
+    if (any_bgr) {
+      size_t need = 0;
+      bool direct_all = kmax_all <= 1024 && use_lds_map_ && !any_staged && all_bgr;
+      for (int i = 0; i < njobs; ++i)
+        direct_all &= ((uintptr_t)jobs[i].d_in & 7) == 0 && ((uintptr_t)jobs[i].d_out & 15) == 0;
+      auto direct = [&](const MapJob&) { return direct_all; };
+      for (int i = 0; i < njobs; ++i)
+        if (jobs[i].bgr && !direct(jobs[i])) need += align4(jobs[i].n) + 4;
+      if (need > 0) {
+        if (need > cap_bgr_pack_) {
+          DQ_HIP(hipStreamSynchronize(stream));
+          if (d_bgr_pack_) DQ_HIP(hipFree(d_bgr_pack_));
+          DQ_HIP(hipMalloc((void**)&d_bgr_pack_, need * sizeof(uint32_t)));
+          cap_bgr_pack_ = need;
+        }
+        packed.assign(jobs, jobs + njobs);
+        size_t off = 0;
+        for (MapJob& j : packed)
+          if (j.bgr && !direct(j)) {
+            launch_bgr24_pack(reinterpret_cast<const uint8_t*>(j.d_in), j.n, 1, 3 * j.n, d_bgr_pack_ + off, stream);
+            j.d_in = d_bgr_pack_ + off;
+            j.bgr = false;
+            off += align4(j.n) + 4;
+          }
+        jobs = packed.data();
+      }
+    }
+  }
   // the staging is reused: the previous map's upload must have run
   const double tm0 = trace_ ? host_us() : 0.0;
   if (map_pending_) {
@@ -1602,7 +1664,8 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       MapTask& m = ht[t];
       m.in = j.d_in;
       m.out = j.d_out;
-      if (((uintptr_t)j.d_in & 15) != 0 || ((uintptr_t)j.d_out & 15) != 0) staged.push_back(t);
+      m.bgr = j.bgr ? 1 : 0;   // (aligned and K <= 1024: never staged)
+      if (!j.bgr && (((uintptr_t)j.d_in & 15) != 0 || ((uintptr_t)j.d_out & 15) != 0)) staged.push_back(t);
       m.pal = db + 768 / 2;
       m.lut = reinterpret_cast<const uint16_t*>(db);
       m.cell_rec = d_cell_rec_ + (size_t)t * kCells * kCellRecWords;
@@ -1640,12 +1703,15 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       timed_begin(stream);
       launch_build_cells(dt, nt, kmax, stream);
       timed_end(ST_CELLS, 0.0, stream);
-      double px = 0;
-      for (int t = 0; t < nt; ++t) px += ht[t].n;
+      double px = 0, mb = 0;   // pixels; bytes: 4 (BGR24: 3) read + 4 written per pixel
+      for (int t = 0; t < nt; ++t) {
+        px += ht[t].n;
+        mb += (ht[t].bgr ? 7.0 : 8.0) * ht[t].n;
+      }
       timed_begin(stream);
-      if (lds_map) launch_map_lds(dt, nt, kmax, nblocks, stream);
+      if (lds_map) launch_map_lds(dt, nt, kmax, nblocks, ht[0].bgr != 0, stream);
       else launch_map(dt, nt, kmax, nblocks, stream);
-      timed_end(ST_MAP, 8.0 * px, stream, px);
+      timed_end(ST_MAP, mb, stream, px);
     } else {
       // rare path: run the chunk task by task, staging misaligned buffers
       for (int t = 0; t < nt; ++t) {

@@ -87,6 +87,10 @@ struct FrameJob {
   // DivQuantCluster.cpp:1139-1146): channels cut to num_bits, every dec-th
   // row and column of a rows x cols frame read with the reference's numRows
   // stride (calc_color_table :124); cols 0: n; centres << (8 - num_bits).
+  // d_in is a BGR24 frame (OpenCV CV_8UC3, continuous rows: 3 B per point,
+  // B G R) read directly by the root's passes, its partition and the map
+  // (uniform-weight path, one shard)
+  bool bgr = false;
   int num_bits = 8;
   int dec = 1;
   uint32_t rows = 1, cols = 0;
@@ -132,6 +136,7 @@ class Engine {
     uint32_t* d_out;
     const uint32_t* ct;   // host colortable
     int k;
+    bool bgr = false;     // d_in is a BGR24 frame (3 B per pixel)
   };
   void map_many(const MapJob* jobs, int njobs, hipStream_t stream);
 
@@ -273,12 +278,16 @@ class Engine {
   const uint8_t* buf_ptr(int buf, const FrameState& f, int shard) const;
   // bytes a pass reads per point of a node: the caller's packed frame (a
   // root) or the planar working buffers
-  double point_bytes(int node) const { return nodes_[node].buf == 0 ? 4.0 : 3.0; }
+  double point_bytes(int node) const {
+    return nodes_[node].buf == 0 && !frames_[nodes_[node].frame].job->bgr ? 4.0 : 3.0;
+  }
   void timed_begin(hipStream_t stream);
   void timed_end(int kind, double bytes, hipStream_t stream, double units = 0.0);
   void collect_timing();
 
   int device_ = 0;
+  uint32_t* d_bgr_pack_ = nullptr;   // BGR24 frames the map cannot read directly, packed
+  size_t cap_bgr_pack_ = 0;
   bool fixed_point_ = true;
   hipStream_t stream_ = nullptr;
   std::mutex mu_;

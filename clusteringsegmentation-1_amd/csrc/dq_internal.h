@@ -48,6 +48,13 @@ struct alignas(16) Params {
 // Per-node state.  One record per node per round it is split in; the records
 // of earlier rounds stay valid for the whole run (a later round partitions a
 // node through its record and tiles, see PartTile).
+// DevNode::planar: how a node's points are stored at src.
+enum SrcFormat : int32_t {
+  SRC_PACKED = 0,   // the caller's u32 0x00RRGGBB frame (4 B per point)
+  SRC_PLANAR = 1,   // byte planes R, G, B of P0 / P1 (3 B per point)
+  SRC_BGR24 = 2,    // the caller's BGR24 frame (OpenCV CV_8UC3 rows, 3 B per point)
+};
+
 struct alignas(16) DevNode {
   // --- set by the host when the round starts
   const uint8_t* src;       // the frame (shard) in the buffer holding the node: element 0 of
@@ -60,7 +67,8 @@ struct alignas(16) DevNode {
   int32_t split_pb, split_pe;   // fused split: the parent's PartTiles [pb, pe) of the round
   int32_t split_side;           //   0: this node is the parent's old half, 1: the new half
                                 //   (split_pb < 0: the node has its own split pass)
-  int32_t planar;               // src holds byte planes (0: the caller's packed frame)
+  int32_t planar;               // source format of src (SrcFormat): the caller's packed
+                                //   frame, the byte planes of P0 / P1, or a BGR24 frame
   double s;                 // data_weight of the frame (get_double_scale)
   double tw;                // total_weight = weight[old_index]  (:353)
   double tm[3], tv[3];      // total_mean / total_var (root: written by PASS_INIT)

@@ -116,6 +116,7 @@ struct alignas(16) MapTask {
   int32_t k;
   uint32_t block_begin;     // first map workgroup of this task
   uint32_t grp_per_block;   // groups of kMapPx pixels per workgroup
+  int32_t bgr;              // in is a BGR24 frame (3 B per pixel, 8-B aligned; map_lds_kernel only)
 };
 
 // Map: candidate records per colour cell for every task (one launch), then
@@ -129,7 +130,9 @@ void launch_map(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hi
 // 1024-thread workgroup per CU); map_lds_blocks gives each task's share of
 // the grid (block_begin / grp_per_block set by the caller from it).
 constexpr int kMapLdsBlock = 1024;
-void launch_map_lds(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream);
+// bgr: every task's input is a BGR24 frame (MapTask::bgr), else every task's is packed.
+void launch_map_lds(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, bool bgr,
+                    hipStream_t stream);
 
 // Block histograms of a mapped frame (genHistogramsForBlocks' block loop,
 // ClusteringSegmentation.cpp:420-563).  Blocks of dim x dim pixels, dim 1..4 (the app: 4);

@@ -175,10 +175,21 @@ __device__ __forceinline__ uint32_t valid_mask(uint32_t vs, uint32_t start, uint
 // vector straddling `end` is loaded whole (every buffer keeps >= 16 readable
 // bytes of slack past each frame shard).  `src`: the shard's element 0 (a
 // packed frame) or its R plane (planar; G, B at + plane, + 2 plane).
-template <bool PLANAR, bool FULL, bool NT = false>
+//   BGR24 source (PLANAR's slot layout; a lane's 16 points are 48 contiguous
+//   bytes B G R B G R .. at 3 (vs + 16 l): three 16-B loads, 16-B aligned
+//   because vs is a multiple of 16 and the frame is 16-B aligned)
+template <bool PLANAR, bool FULL, bool NT = false, bool BGR = false>
 __device__ __forceinline__ void fetch_sweep(const uint8_t* src, uint64_t plane, uint32_t vs, uint32_t end,
                                             RawSweep& x) {
-  if (PLANAR) {
+  if (BGR) {
+    const uint32_t i = vs + 16u * lane_id();
+    g_cu4* p = (g_cu4*)(src + 3ull * i);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      if (FULL || i < end) x.v[c] = NT ? __builtin_nontemporal_load(p + c) : p[c];
+      else x.v[c] = (u32x4){0u, 0u, 0u, 0u};
+    }
+  } else if (PLANAR) {
     const uint32_t i = vs + 16u * lane_id();
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -197,12 +208,21 @@ __device__ __forceinline__ void fetch_sweep(const uint8_t* src, uint64_t plane, 
   }
 }
 
-// Raw loads -> channel words (packed: 5 v_perm_b32 per 4 points).
-template <bool PLANAR>
+// Raw loads -> channel words (packed: 5 v_perm_b32 per 4 points; BGR24: 6,
+// from the three words w0 = B0 G0 R0 B1, w1 = G1 R1 B2 G2, w2 = R2 B3 G3 R3
+// holding slots 4j .. 4j+3).
+template <bool PLANAR, bool BGR = false>
 __device__ __forceinline__ void unpack_sweep(const RawSweep& x, Sweep& w) {
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
-    if (PLANAR) {
+    if (BGR) {
+      const uint32_t w0 = x.v[(3 * j) >> 2][(3 * j) & 3];
+      const uint32_t w1 = x.v[(3 * j + 1) >> 2][(3 * j + 1) & 3];
+      const uint32_t w2 = x.v[(3 * j + 2) >> 2][(3 * j + 2) & 3];
+      w.b[j] = __builtin_amdgcn_perm(w2, __builtin_amdgcn_perm(w1, w0, 0x0C060300u), 0x05020100u);
+      w.g[j] = __builtin_amdgcn_perm(w2, __builtin_amdgcn_perm(w1, w0, 0x0C070401u), 0x06020100u);
+      w.r[j] = __builtin_amdgcn_perm(w2, __builtin_amdgcn_perm(w1, w0, 0x0C0C0502u), 0x07040100u);
+    } else if (PLANAR) {
       w.r[j] = x.v[0][j];
       w.g[j] = x.v[1][j];
       w.b[j] = x.v[2][j];
@@ -332,7 +352,7 @@ __device__ __forceinline__ void sweep_sums(const Sweep& w, uint32_t vs, uint32_t
 
 // A wave's sweeps over [ws, we) of a pass (pass_kernel, kpass_kernel), the
 // next sweep's loads issued before this sweep's arithmetic.
-template <int KIND, bool PLANAR>
+template <int KIND, bool PLANAR, bool BGR = false>
 __device__ __forceinline__ void wave_pass(const uint8_t* src, uint64_t plane, uint32_t ws, uint32_t we,
                                           const Params& q, LaneSums& s) {
   const bool exact_all = !(q.eps < __builtin_inff());   // FP32 filter off for this node
@@ -340,17 +360,17 @@ __device__ __forceinline__ void wave_pass(const uint8_t* src, uint64_t plane, ui
   bool full = vs >= ws && vs + kWaveSweep <= we;
   RawSweep x;
   if (vs < we) {
-    if (full) fetch_sweep<PLANAR, true>(src, plane, vs, we, x);
-    else fetch_sweep<PLANAR, false>(src, plane, vs, we, x);
+    if (full) fetch_sweep<PLANAR, true, false, BGR>(src, plane, vs, we, x);
+    else fetch_sweep<PLANAR, false, false, BGR>(src, plane, vs, we, x);
   }
   while (vs < we) {
     Sweep w;
-    unpack_sweep<PLANAR>(x, w);
+    unpack_sweep<PLANAR, BGR>(x, w);
     const uint32_t nvs = vs + kWaveSweep;
     const bool nfull = nvs + kWaveSweep <= we;
     if (nvs < we) {
-      if (nfull) fetch_sweep<PLANAR, true>(src, plane, nvs, we, x);
-      else fetch_sweep<PLANAR, false>(src, plane, nvs, we, x);
+      if (nfull) fetch_sweep<PLANAR, true, false, BGR>(src, plane, nvs, we, x);
+      else fetch_sweep<PLANAR, false, false, BGR>(src, plane, nvs, we, x);
     }
     if (full) sweep_sums<KIND, PLANAR, true>(w, vs, ws, we, q, exact_all, s);
     else sweep_sums<KIND, PLANAR, false>(w, vs, ws, we, q, exact_all, s);
@@ -505,7 +525,8 @@ __global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void pass_kernel(RoundArgs a
   LaneSums s;
   uint32_t ws, we;
   wave_range(t.start, t.end, wave_id(), ws, we);
-  if (nd.planar) wave_pass<KIND, true>(nd.src, a.plane, ws, we, q, s);
+  if (nd.planar == SRC_PLANAR) wave_pass<KIND, true>(nd.src, a.plane, ws, we, q, s);
+  else if (nd.planar == SRC_BGR24) wave_pass<KIND, true, true>(nd.src, a.plane, ws, we, q, s);
   else wave_pass<KIND, false>(nd.src, a.plane, ws, we, q, s);
 
   uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
@@ -904,7 +925,8 @@ __global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void kpass_kernel(RoundArgs 
   LaneSums s;
   uint32_t ws, we;
   wave_range(t.start, t.end, wave_id(), ws, we);
-  if (nd.planar) wave_pass<KIND, true>(nd.src, a.plane, ws, we, q, s);
+  if (nd.planar == SRC_PLANAR) wave_pass<KIND, true>(nd.src, a.plane, ws, we, q, s);
+  else if (nd.planar == SRC_BGR24) wave_pass<KIND, true, true>(nd.src, a.plane, ws, we, q, s);
   else wave_pass<KIND, false>(nd.src, a.plane, ws, we, q, s);
   uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
 #pragma unroll
@@ -1187,9 +1209,15 @@ constexpr uint32_t kOOB = 0xF0000000u;
 // parent's segment (planar: the R, G, B planes; packed: the frame words in
 // r), branch-free: vectors starting at or past `end` read kOOB (zeros).  A
 // planar vector straddling `end` is loaded whole (16 B of slack per shard).
-template <bool PLANAR>
+template <bool PLANAR, bool BGR = false>
 __device__ __forceinline__ void fetch_sweep_rs(const PlaneRsrc& s, uint32_t vs, uint32_t end, RawSweep& x) {
-  if (PLANAR) {
+  if (BGR) {   // 48 bytes at 3 i through the frame's resource (s.r)
+    const uint32_t i = vs + 16u * lane_id();
+    const int o = (int)(i < end ? 3u * i : kOOB);
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      x.v[c] = __builtin_amdgcn_raw_buffer_load_b128(s.r, o + 16 * c, 0, DQ_PS_NTLOAD ? 2 : 0);
+  } else if (PLANAR) {
     const uint32_t i = vs + 16u * lane_id();
     const int o = (int)(i < end ? i : kOOB);
     x.v[0] = __builtin_amdgcn_raw_buffer_load_b128(s.r, o, 0, DQ_PS_NTLOAD ? 2 : 0);
@@ -1484,7 +1512,7 @@ typedef uint8_t StageMem;
 // read from a PartTile made these flat loads)
 typedef const __attribute__((address_space(1))) DevNode g_cnode;
 typedef const __attribute__((address_space(1))) Tile g_ctile;
-template <bool PLANAR>
+template <bool PLANAR, bool BGR = false>
 __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g_ctile* tp,
                                               const DevNode* nodes, uint32_t* wparts, uint64_t plane,
                                               StageMem* st, SplitSums& so, SplitSums& sn) {
@@ -1540,7 +1568,14 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   {
     const uint8_t* src = nd.src;
     const uint32_t ext = nd.off + nd.len;
-    if (PLANAR) {
+    if (BGR) {
+      // a 16-B load is dropped whole when any byte of it is out of range: the
+      // range covers a straddling vector's 48 bytes (a frame whose size is not
+      // a multiple of 16 points is an aligned copy with >= 48 B of slack; a
+      // caller's frame that is one has no vector past its end)
+      s.r = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(3u * ext + 48u), 0x00020000);
+      s.g = s.b = s.r;
+    } else if (PLANAR) {
       const int nb = (int)(ext + 16u);   // (16 B of slack after every shard)
       s.r = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, nb, 0x00020000);
       s.g = __builtin_amdgcn_make_buffer_rsrc((void*)(src + plane), (short)0, nb, 0x00020000);
@@ -1553,23 +1588,23 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   RawSweep x, xn;
   uint32_t vs = start & ~15u;
   bool full = vs >= start && vs + kWaveSweep <= end;
-  fetch_sweep_rs<PLANAR>(s, vs, end, x);
+  fetch_sweep_rs<PLANAR, BGR>(s, vs, end, x);
 #if DQ_PS_PREFETCH == 2
   RawSweep xnn;
-  fetch_sweep_rs<PLANAR>(s, vs + kWaveSweep, end, xn);
+  fetch_sweep_rs<PLANAR, BGR>(s, vs + kWaveSweep, end, xn);
 #endif
   while (vs < end) {
     const uint32_t nvs = vs + kWaveSweep;
     const bool nfull = nvs + kWaveSweep <= end;
 #if DQ_PS_PREFETCH == 2
-    fetch_sweep_rs<PLANAR>(s, nvs + kWaveSweep, end, xnn);
+    fetch_sweep_rs<PLANAR, BGR>(s, nvs + kWaveSweep, end, xnn);
 #elif DQ_PS_PREFETCH
     // the next sweep's loads in flight during this one (past the end: kOOB,
     // no memory access -- a fixed load count per sweep)
-    fetch_sweep_rs<PLANAR>(s, nvs, end, xn);
+    fetch_sweep_rs<PLANAR, BGR>(s, nvs, end, xn);
 #endif
     Sweep sw;
-    unpack_sweep<PLANAR>(x, sw);
+    unpack_sweep<PLANAR, BGR>(x, sw);
     // the parent's final decision: its cut when proven, else its last 2-means plane
     SweepMask om, nm;
     if (full) {
@@ -1636,7 +1671,7 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
 #elif DQ_PS_PREFETCH
     x = xn;
 #else
-    if (nvs < end) fetch_sweep_rs<PLANAR>(s, nvs, end, x);
+    if (nvs < end) fetch_sweep_rs<PLANAR, BGR>(s, nvs, end, x);
 #endif
     vs = nvs;
     full = nfull;
@@ -1663,7 +1698,8 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
   __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
   StageMem* st = stage + wave_id() * kStageWave;
 #endif
-  if (nd.planar) partsplit_run<true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
+  if (nd.planar == SRC_PLANAR) partsplit_run<true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
+  else if (nd.planar == SRC_BGR24) partsplit_run<true, true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
   else partsplit_run<false>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
 
   __shared__ uint32_t red[kTileWaves][16];
@@ -1750,7 +1786,7 @@ __device__ void plan_child(const PlanArgs& a, const DevNode& P, const NodeResult
   d->split_pb = pb;
   d->split_pe = pe;
   d->split_side = side;
-  d->planar = 1;
+  d->planar = SRC_PLANAR;
   d->s = ps;
   d->tw = tw;
   d->tm[0] = m0;
@@ -2274,6 +2310,17 @@ constexpr int kMapQ = 64;
 #ifndef DQ_MAP_NT
 #define DQ_MAP_NT 1
 #endif
+// 12 BGR24 bytes (3 words, little-endian) -> 4 packed 0x00RRGGBB words.
+__device__ __forceinline__ u32x4 bgr12_to_px4(uint32_t w0, uint32_t w1, uint32_t w2) {
+  u32x4 o;
+  o.x = w0 & 0x00FFFFFFu;
+  o.y = __builtin_amdgcn_perm(w1, w0, 0x0C050403u);   // b3 b4 b5 0
+  o.z = __builtin_amdgcn_perm(w2, w1, 0x0C040302u);   // b6 b7 b8 0
+  o.w = w2 >> 8;                                       // b9 b10 b11 0
+  return o;
+}
+
+template <bool BGR>
 __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __restrict__ tasks,
                                                               int ntasks) {
   int ti = 0;
@@ -2307,6 +2354,21 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   g_cu4* gidx4 = (g_cu4*)tk.cell_idx;
   g_cu16* gidx = (g_cu16*)tk.cell_idx;
   g_cu4* in4 = (g_cu4*)tk.in;
+  // a BGR24 frame (tk.bgr): group g is the 24 bytes at 24 g, three 8-B loads
+  typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+  typedef const __attribute__((address_space(1))) u32x2v g_cu2;
+  g_cu2* in2 = (g_cu2*)tk.in;
+  constexpr bool bgr = BGR;   // (every task of a launch has the same pixel format)
+  auto load_group = [&](uint32_t gi, u32x4& a, u32x4& b) {
+    if (bgr) {
+      const u32x2v x0 = in2[3 * gi], x1 = in2[3 * gi + 1], x2 = in2[3 * gi + 2];
+      a = (u32x4){x0.x, x0.y, x1.x, x1.y};
+      b = (u32x4){x2.x, x2.y, 0u, 0u};
+    } else {
+      a = in4[2 * gi];
+      b = in4[2 * gi + 1];
+    }
+  };
   typedef __attribute__((address_space(1))) u32x4 g_u4;
   g_u4* out4 = (g_u4*)as_gw(tk.out);
 
@@ -2372,10 +2434,7 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   const uint32_t g1 = min(ngrp, g0 + tk.grp_per_block);
   // the next iteration's pixels are loaded before this one's are mapped
   u32x4 na = (u32x4){0u, 0u, 0u, 0u}, nb = na;
-  if (g0 + threadIdx.x < g1) {
-    na = in4[2 * (g0 + threadIdx.x)];
-    nb = in4[2 * (g0 + threadIdx.x) + 1];
-  }
+  if (g0 + threadIdx.x < g1) load_group(g0 + threadIdx.x, na, nb);
   for (uint32_t gb = g0; gb < g1; gb += kMapLdsBlock) {
     const uint32_t g = gb + threadIdx.x;
     const bool have = g < g1;
@@ -2383,12 +2442,15 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
     {
       const u32x4 a = na, b = nb;
       const uint32_t gn = g + kMapLdsBlock;
-      if (gn < g1) {
-        na = in4[2 * gn];
-        nb = in4[2 * gn + 1];
-      }
+      if (gn < g1) load_group(gn, na, nb);
+      if (bgr) {
+        const u32x4 lo = bgr12_to_px4(a[0], a[1], a[2]), hi = bgr12_to_px4(a[3], b[0], b[1]);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { px[e] = a[e]; px[4 + e] = b[e]; }
+        for (int e = 0; e < 4; ++e) { px[e] = lo[e]; px[4 + e] = hi[e]; }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { px[e] = a[e]; px[4 + e] = b[e]; }
+      }
     }
     uint32_t res[kMapPx], rec[kMapPx];
 #pragma unroll
@@ -2464,7 +2526,10 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   // tail (n % kMapPx points): the task's first workgroup, whole palette
   const uint32_t t = ngrp * kMapPx + threadIdx.x;
   if (lb == 0 && t < n) {
-    const uint32_t p = as_g(tk.in)[t] & 0xFFFFFFu;
+    typedef const __attribute__((address_space(1))) uint8_t g_cu8;
+    g_cu8* b8 = (g_cu8*)tk.in;
+    const uint32_t p = bgr ? ((uint32_t)b8[3 * t + 2] << 16) | ((uint32_t)b8[3 * t + 1] << 8) | b8[3 * t]
+                           : as_g(tk.in)[t] & 0xFFFFFFu;
     const uint32_t S = start_of(p);
     uint32_t best = 0xFFFFFFFFu;
     for (int j = 0; j < k; ++j) best = min(best, key(p, S, (uint32_t)j));
@@ -2561,17 +2626,21 @@ uint32_t map_groups_per_block(uint32_t n) {
   return 8u * kBlock;
 }
 
-void launch_map_lds(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream) {
+void launch_map_lds(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, bool bgr,
+                    hipStream_t stream) {
   if (ntasks <= 0 || nblocks == 0) return;
   const size_t lds = (size_t)kCells * 4 + (size_t)(kMapLdsBlock / 64) * kMapQ * 4 +
                      (size_t)(kmax + 1) * 8 + 768 * 2;
   static bool attr = false;
   if (!attr) {   // more than 64 KB of dynamic LDS
-    (void)hipFuncSetAttribute((const void*)map_lds_kernel,
+    (void)hipFuncSetAttribute((const void*)map_lds_kernel<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)map_lds_kernel<true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  map_lds_kernel<<<dim3(nblocks), dim3(kMapLdsBlock), lds, stream>>>(tasks, ntasks);
+  if (bgr) map_lds_kernel<true><<<dim3(nblocks), dim3(kMapLdsBlock), lds, stream>>>(tasks, ntasks);
+  else map_lds_kernel<false><<<dim3(nblocks), dim3(kMapLdsBlock), lds, stream>>>(tasks, ntasks);
 }
 
 void launch_map(const MapTask* tasks, int ntasks, int kmax, uint32_t nblocks, hipStream_t stream) {
@@ -2800,14 +2869,6 @@ typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
                                // of 270 or 540 rows measured slower)
 #endif
 
-__device__ __forceinline__ u32x4 bgr12_to_px4(uint32_t w0, uint32_t w1, uint32_t w2) {
-  u32x4 o;
-  o.x = w0 & 0x00FFFFFFu;
-  o.y = __builtin_amdgcn_perm(w1, w0, 0x0C050403u);   // b3 b4 b5 0
-  o.z = __builtin_amdgcn_perm(w2, w1, 0x0C040302u);   // b6 b7 b8 0
-  o.w = w2 >> 8;                                       // b9 b10 b11 0
-  return o;
-}
 
 __device__ __forceinline__ void px4_to_bgr12(u32x4 p, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
   w0 = __builtin_amdgcn_perm(p.y, p.x, 0x04020100u);   // B0 G0 R0 B1

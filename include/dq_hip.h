@@ -169,6 +169,30 @@ int dq_hip_cut_bits_dev(int device, const uint32_t *d_in, uint32_t n, uint32_t *
 int dq_hip_map_dev(int device, const uint32_t *d_in, uint32_t n,
                    uint32_t *d_out, const uint32_t *ct, int k, void *stream);
 
+/* ---- BGR24 frames (OpenCV CV_8UC3: B, G, R bytes, `stride` bytes per row)
+ * quant_recurse of device BGR24 frames without the packed conversion
+ * (SURVEY 8f.3): with uniq = 1 and continuous rows (stride == 3*width) the
+ * root's passes, its partition and the map read the 3-B pixels directly
+ * (a frame whose pointer is not 16-B aligned or whose pixel count is not a
+ * multiple of 16 is first copied to aligned scratch); padded rows or uniq = 0
+ * (the weighted path's colour table) pack the frame on the GPU first.  d_out
+ * gets packed 0x00RRGGBB colours (the reference's output format).  The batch
+ * form runs every frame of a call over the engine lanes like
+ * dq_hip_quant_batch_dev (ct: nframes * k, k_out: nframes).  Returns the
+ * number of empty clusters or < 0. */
+int dq_hip_quant_bgr24_batch_dev(int device, int nframes, const uint8_t *const *d_bgr,
+                                 uint32_t width, uint32_t height, uint32_t stride,
+                                 uint32_t *const *d_out, uint32_t k, uint32_t *ct,
+                                 uint32_t *k_out, int uniq, int max_iters, void *stream);
+int dq_hip_quant_bgr24_dev(int device, const uint8_t *d_bgr, uint32_t width, uint32_t height,
+                           uint32_t stride, uint32_t *d_out, uint32_t *k, uint32_t *ct,
+                           int uniq, int max_iters, void *stream);
+/* map_colors_mps of a device BGR24 frame (read directly when K <= 1024 and
+ * the rows are continuous) into packed colours. */
+int dq_hip_map_bgr24_dev(int device, const uint8_t *d_bgr, uint32_t width, uint32_t height,
+                         uint32_t stride, uint32_t *d_out, const uint32_t *ct, int k,
+                         void *stream);
+
 /* ---- diagnostics of the last clustering on `device` ----------------------
  * means: k*3 doubles (the reference's mean[ic] per cluster index, the north
  * star's "float centroids"); sizes: k cluster sizes; trace: (k-1)*4 of

@@ -169,3 +169,95 @@ def test_png_bgr_end_to_end(gpu, name):
                         ctypes.c_int(len(ct)))
     assert "%016x" % fx.fnv(mapped) == fix["k16"]["out_fnv"]
     assert np.array_equal(d_out.cpu().numpy(), _orc_unpack(mapped, w, h, 3 * w))
+
+
+# ------------------------------------------- fused BGR24 reads (GPU) -------
+def _bgr_of(px):
+    """Packed 0x00RRGGBB -> BGR24 bytes (PixelToVec3b order)."""
+    px = np.asarray(px, np.uint32)
+    return np.stack([px & 0xFF, (px >> 8) & 0xFF, (px >> 16) & 0xFF], -1).astype(np.uint8).reshape(-1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["batman", "cookie"])
+def test_fused_bgr24_png(gpu, name):
+    """quant_recurse straight from the Mat's BGR24 bytes (the root's passes,
+    its partition and the map read 3-B pixels): the reference's
+    colortables and output hashes for the sample images, uniform-weight K in
+    {4, 16, 125, 256} and weighted K in {4, 16}."""
+    import torch
+    fix = fx.load_json("png.json")[name]
+    bgr, w, h = _png_bgr(name)
+    d_bgr = torch.from_numpy(bgr.reshape(-1)).to("cuda:0")
+    d_out = torch.empty(w * h, dtype=torch.int32, device="cuda:0")
+    for k in (4, 16, 125, 256):
+        ct, _ = gpu.quant_bgr24_device(d_bgr, w, h, d_out, k)
+        torch.cuda.synchronize()
+        assert [int(v) for v in ct] == fix["k%d" % k]["ct"], (name, k)
+        assert "%016x" % fx.fnv(d_out.cpu().numpy().view(np.uint32)) == fix["k%d" % k]["out_fnv"], (name, k)
+    for k in (4, 16):
+        ct, _ = gpu.quant_bgr24_device(d_bgr, w, h, d_out, k, all_pixels_unique=0)
+        torch.cuda.synchronize()
+        assert [int(v) for v in ct] == fix["k%d_weighted" % k]["ct"], (name, k)
+        assert "%016x" % fx.fnv(d_out.cpu().numpy().view(np.uint32)) == fix["k%d_weighted" % k]["out_fnv"]
+
+
+@pytest.mark.gpu
+def test_fused_bgr24_c4_frames(gpu):
+    """Two of C4's 4K frames (seed + f) as BGR24, one batched call
+    over the engine lanes: every frame's colortable and output hash equal the
+    reference's (tests/golden/c4.json)."""
+    import torch
+    fix = fx.load_json("c4.json")
+    w, h = 3840, 2160
+    frames = [torch.from_numpy(_bgr_of(fx.xorshift(w * h, seed=fx.SEED + f))).to("cuda:0") for f in range(2)]
+    outs = [torch.empty(w * h, dtype=torch.int32, device="cuda:0") for _ in range(2)]
+    cts, _ = gpu.quant_bgr24_batch_device(frames, w, h, outs, 256)
+    torch.cuda.synchronize()
+    for f in range(2):
+        r = fix["f%02d" % f]
+        assert [int(v) for v in cts[f]] == r["ct"], f
+        assert "%016x" % fx.fnv(outs[f].cpu().numpy().view(np.uint32)) == r["out_fnv"], f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h,pad,off", [(333, 77, 0, 0), (256, 64, 0, 1), (320, 50, 0, 0), (100, 40, 5, 0),
+                                         (1, 1, 0, 0), (17, 3, 0, 3)])
+def test_fused_bgr24_layouts(gpu, w, h, pad, off):
+    """Ragged pixel counts (not a multiple of 16), misaligned frames and padded
+    rows take the staged / packed forms: results equal the packed path's on
+    the same pixels (colortable, output), uniform and weighted."""
+    import torch
+    stride = 3 * w + pad
+    buf = _frame(w, h, stride, seed=1000 + w + h)
+    px = _orc_pack(buf, w, h, stride)
+    raw = torch.zeros(len(buf) + 64, dtype=torch.uint8, device="cuda:0")
+    raw[off:off + len(buf)] = torch.from_numpy(buf).to("cuda:0")
+    d_bgr = raw[off:off + len(buf)]
+    d_px = torch.from_numpy(px.view(np.int32)).to("cuda:0")
+    d_a = torch.empty(w * h, dtype=torch.int32, device="cuda:0")
+    d_b = torch.empty(w * h, dtype=torch.int32, device="cuda:0")
+    for k, uniq in ((16, 1), (5, 1), (8, 0)):
+        ct_a, _ = gpu.quant_bgr24_device(d_bgr, w, h, d_a, k, stride=stride, all_pixels_unique=uniq)
+        ct_b, _ = gpu.quant_device(d_px, d_b, k, all_pixels_unique=uniq)
+        torch.cuda.synchronize()
+        assert list(ct_a) == list(ct_b), (k, uniq)
+        assert torch.equal(d_a, d_b), (k, uniq)
+
+
+@pytest.mark.gpu
+def test_map_bgr24(gpu):
+    """map_colors_mps from BGR24 bytes (direct for K <= 1024, packed first
+    above) equals the oracle's map of the packed pixels."""
+    import torch
+    w, h = 640, 360
+    px = fx.xorshift(w * h, seed=4242) & np.uint32(0xFFFFFF)
+    d_bgr = torch.from_numpy(_bgr_of(px)).to("cuda:0")
+    d_out = torch.empty(w * h, dtype=torch.int32, device="cuda:0")
+    for k in (1, 16, 300, 1024, 2000):
+        pal = fx.xorshift(k, seed=77 + k) & np.uint32(0xFFFFFF)
+        gpu.map_bgr24_device(d_bgr, w, h, d_out, pal)
+        torch.cuda.synchronize()
+        want = np.zeros(w * h, np.uint32)
+        fx.oracle().dqo_map(fx.vp(px), ctypes.c_uint32(len(px)), fx.vp(want), fx.vp(pal), ctypes.c_int(k))
+        assert np.array_equal(d_out.cpu().numpy().view(np.uint32), want), k

@@ -436,10 +436,6 @@ def test_varpart_cut_bits_decimation(gpu):
     qvf.restype = None
     qvf.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
-    L.dq_hip_varpart_dev.restype = ctypes.c_int
-    L.dq_hip_varpart_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
-                                     ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     cases = fx.load_json("varpart.json")
     arrs = fx.load_npz("varpart.npz")
     for i, c in enumerate(cases):
@@ -455,7 +451,7 @@ def test_varpart_cut_bits_decimation(gpu):
         k2 = ctypes.c_uint32(s["k"])
         ct2 = np.zeros(s["k"], np.uint32)
         rc = L.dq_hip_varpart_dev(0, d.data_ptr(), len(px), s["rows"], s["cols"],
-                                  ctypes.cast(ctypes.pointer(k2), ctypes.c_void_p), fx.vp(ct2), s["num_bits"],
+                                  ctypes.byref(k2), fx.vp(ct2), s["num_bits"],
                                   s["dec"], s["max_iters"], s["uniq"], None)
         assert rc >= 0 and [int(v) for v in ct2[:k2.value]] == c["ct"], (i, s)
         if s["k"] > 1:
@@ -470,7 +466,7 @@ def test_varpart_cut_bits_decimation(gpu):
     d = torch.zeros(48 * 80, dtype=torch.int32, device="cuda")
     k3 = ctypes.c_uint32(4)
     ct3 = np.zeros(4, np.uint32)
-    assert L.dq_hip_varpart_dev(0, d.data_ptr(), 48 * 80, 80, 48, ctypes.cast(ctypes.pointer(k3), ctypes.c_void_p),
+    assert L.dq_hip_varpart_dev(0, d.data_ptr(), 48 * 80, 80, 48, ctypes.byref(k3),
                                 fx.vp(ct3), 8, 1, 10, 0, None) == -2
 
 
@@ -479,7 +475,6 @@ def test_cut_bits_device(gpu):
     per-channel bit counts, in place and out of place)."""
     import torch
     L = gpu.lib()
-    L.dq_hip_cut_bits_dev.restype = ctypes.c_int
     px = fx.xorshift(1000003, seed=99) | np.uint32(0x5A000000)
     for nbr, nbg, nbb in [(8, 8, 8), (5, 5, 5), (1, 1, 1), (3, 6, 7), (8, 2, 4)]:
         want = np.zeros_like(px)

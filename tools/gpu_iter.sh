@@ -20,9 +20,10 @@ print('value %.0f ms/step %.3f c3 %.3f ms rowtile %.0f frac %.3f (%s %.1f us) ve
     d['value'], d['ms_per_step'], d['detail']['c3']['ms_per_frame'], d['detail']['c4_rowtile']['Mpix_per_s'],
     d['roofline']['frac'], d['roofline']['kernel'], d['roofline']['avg_launch_us'], d['verified']['ok']))
 print(' '.join('%s %.1fus' % (n, v['ms'] * 1e3 / v['launches']) for n, v in k.items() if v['launches']))
+print('bgr24', d['detail'].get('bgr24_input'))
 PY
 cd /tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o lanes1 --output-format csv -- python3 $R/bench.py --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-c3 --no-rowtile > $O/prof.log 2>&1
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o lanes1 --output-format csv -- python3 $R/bench.py --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-c3 --no-rowtile --no-bgr > $O/prof.log 2>&1
 python3 - $O/prof <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True)[0]

@@ -17,6 +17,6 @@ timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -
 cat $O/bench.json
 if [ "${PROF:-0}" = 1 ]; then
   cd /tmp
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o c4share_lanes1 --output-format csv -- python3 $R/bench.py --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-c3 --no-rowtile > $O/prof_c4share_lanes1.log 2>&1
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o c4share_lanes1 --output-format csv -- python3 $R/bench.py --lanes 1 --steps 5 --warmup 2 --no-cpu-baseline --no-c3 --no-rowtile --no-bgr > $O/prof_c4share_lanes1.log 2>&1
   find $O/prof -name "*stats*"
 fi
