@@ -216,16 +216,25 @@ def frame_fixture(w, h, k, f):
     return None
 
 
+MISMATCH = []   # details of failed frame checks (reported with the error line)
+
+
 def check_frame(pkg, out_t, ct, fix, rows=None, h=None, world=1, rank=0):
     """Compare one frame's output (whole frame, or this rank's row band) and
     colortable with the fixture.  Returns True / False / None (no fixture)."""
     if fix is None:
         return None
     if [int(v) for v in ct] != fix["ct"]:
+        got = [int(v) for v in ct]
+        MISMATCH.append({"what": "ct", "k_out": len(got), "k_ref": len(fix["ct"]),
+                         "first_diff": next((i for i, (x, y) in enumerate(zip(got, fix["ct"])) if x != y), None)})
         return False
     out = out_t.cpu().numpy().view(np.uint32)
     if rows is None:
-        return "%016x" % pkg.fnv1a64(out) == fix["out_fnv"]
+        ok = "%016x" % pkg.fnv1a64(out) == fix["out_fnv"]
+        if not ok:
+            MISMATCH.append({"what": "out"})
+        return ok
     bands = fix.get("band_fnv")
     if world == 1:
         return "%016x" % pkg.fnv1a64(out) == fix["out_fnv"]
@@ -366,7 +375,8 @@ def main():
                                   " of this rank's row bands" if a.mode == "rows" and world > 1 else "")}
         if not ok:
             print(json.dumps({"error": "bench outputs differ from the reference fixtures",
-                              "verified": verified, "per_frame_rank%d" % rank: res}), flush=True)
+                              "verified": verified, "per_frame_rank%d" % rank: res, "mismatch": MISMATCH}),
+                  flush=True)
             sys.exit(3)
     # --- roofline region: the same steps again with HIP events around every
     # launch (on the library's launch stream) for per-kernel durations
