@@ -559,7 +559,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   ra.nn = nr;
   ra.tot = d_tot_;
   ra.nshard = S;
-  ra.fuse_split = 0;
+  ra.pad = 0;
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = nullptr;
@@ -662,10 +662,8 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   const size_t o_cnt = o_pt + al(R.ptiles_cap * sizeof(PartTile));
   const size_t o_ctr = o_cnt + 64;
   const size_t o_wp = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
-  // arrival words per (2-means iteration, record), then the fused split
-  // epilogue's per parent (row max_iters)
   const size_t o_rd = o_wp + al(R.tiles_cap * kTileWaves * sizeof(uint32_t));
-  const size_t bytes = o_rd + al((size_t)(max_iters + 1) * nr * sizeof(uint32_t));
+  const size_t bytes = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
   R.bytes = bytes;
   char* dblk = arena_alloc(bytes);
   R.dn = reinterpret_cast<DevNode*>(dblk);
@@ -715,15 +713,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   ra.nn = R.nr;
   ra.tot = d_tot_;
   ra.nshard = 1;
-  // the split epilogue fused into partsplit (its parents' last workgroups)
-  // measured slower: partsplit 104.5 -> 119 us per 8 x 4K launch against the
-  // 11 us epilogue launch it removes (the finalising workgroup's serial sums
-  // and cursor scan lengthen the kernel's tail); off unless DQ_HIP_FUSE_SPLIT=1
-  static const bool fuse = [] {
-    const char* v = getenv("DQ_HIP_FUSE_SPLIT");
-    return v && v[0] == '1';
-  }();
-  ra.fuse_split = fuse ? 1 : 0;
+  ra.pad = 0;
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = R.dcounts;
@@ -732,13 +722,11 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   launch_plan(pa, stream);
   timed_end(ST_PLAN, 0.0, stream);
   timed_begin(stream);
-  launch_partsplit(ra, (int)R.ptiles_cap, stream);   // (+ the split epilogue: fuse_split)
+  launch_partsplit(ra, (int)R.ptiles_cap, stream);
   timed_end(ST_PARTITION, part_bytes, stream, (double)total);
-  if (!ra.fuse_split) {
-    timed_begin(stream);
-    launch_epilogue(PASS_SPLIT, ra, R.nr, false, stream);
-    timed_end(ST_EPILOGUE, 0.0, stream);
-  }
+  timed_begin(stream);
+  launch_epilogue(PASS_SPLIT, ra, R.nr, false, stream);
+  timed_end(ST_EPILOGUE, 0.0, stream);
   if (trace_) tr_build_us_ += host_us() - tb0;
   R.t_enq = trace_ ? host_us() : 0.0;
   return ri;

@@ -44,11 +44,8 @@ struct RoundArgs {
   // sharded rounds (a frame split into row ranges, one record per shard):
   uint64_t* tot;            // per logical node: 8 u64 totals (nodesum, then allreduce)
   int32_t nshard;           // records per logical node (record r = node * nshard + shard)
-  int32_t fuse_split;       // partsplit finalises the records (the split epilogue fused:
-                            //   planned rounds, every record a child of a part-tiled parent)
-  uint32_t* rdone;          // per (2-means iteration, record): kpass workgroups finished;
-                            //   row max_iters (fuse_split): a parent's partsplit workgroups
-                            //   finished, counted on its old child's record
+  int32_t pad;
+  uint32_t* rdone;          // per (2-means iteration, record): kpass workgroups finished
   NodeResult* dres;         // device copy of the final results (read by the next round's plan)
   const uint32_t* counts;   // planned rounds: [tiles, part tiles, aborted] written by
                             //   plan_kernel (grids are upper bounds); nullptr: host-built

@@ -959,46 +959,6 @@ __global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void kpass_kernel(RoundArgs 
   if (slast && wave_id() == 0) kmeans_epilogue_wave<KIND>(a, rec, &sres);
 }
 
-// The split epilogue of one record, one wave, run by the last partsplit
-// workgroup of the record's parent (fuse_split): exactly
-// epilogue_kernel<PASS_SPLIT, false> for the record -- its side of the
-// parent's part-tile partials (agent-scope loads: other workgroups of the
-// running kernel stored them), the FP64 update, the partition cursors of a
-// final split, the results, the arrival on the split counter.
-__device__ __forceinline__ void split_epilogue_wave(const RoundArgs& a, int rec, NodeResult* sres) {
-  DevNode* w = a.nodes + rec;
-  const uint32_t lane = lane_id();
-  const int side = w->split_side;
-  uint64_t acc[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
-  const uint32_t* sp = reinterpret_cast<const uint32_t*>(a.sparts);
-  for (int i = w->split_pb + (int)lane; i < w->split_pe; i += 64)
-#pragma unroll
-    for (int k = 0; k < F_NUM; ++k)
-      acc[k] += __hip_atomic_load(sp + (size_t)(2 * i + side) * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t tot[F_NUM];
-#pragma unroll
-  for (int k = 0; k < F_NUM; ++k) tot[k] = wave_sum_u64(acc[k]);
-  int fin = 0;
-  if (lane == 0) {
-    fin = node_update<PASS_SPLIT>(w, sres, tot, a.fixed_point != 0) ? 1 : 0;
-    if (fin) {
-      for (int c = 0; c < 3; ++c) { sres->tm[c] = w->tm[c]; sres->tv[c] = w->tv[c]; }
-      w->n_new_local = (uint32_t)tot[F_CNT];
-      sres->n_new_local = (uint32_t)tot[F_CNT];
-      sres->done_it = w->done_it;
-    }
-  }
-  const bool final_results = __shfl(fin, 0, 64) != 0;
-  if (final_results) record_cursors<true>(a.tiles, a.wparts, w->tile_begin, w->tile_end, lane);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (final_results) store_result(a.hres + rec, a.dres ? a.dres + rec : nullptr, *sres, lane, w->len, a.seq);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0)
-    arrive(a.ctr + a.it, (uint32_t)rec, (uint32_t)a.nn, !final_results, a.hstat + a.it, a.seq);
-}
-
 // ---------------------------------------------------------------------------
 // Fused partition + split pass over the tiles of parents split in an earlier
 // round (replaces the reference's per-split O(N) member[] gather, :894-1026,
@@ -1757,26 +1717,9 @@ __global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArg
     uint32_t x = 0;
 #pragma unroll
     for (int ww = 0; ww < kTileWaves; ++ww) x += red[ww][threadIdx.x];
-    // (2 TilePartials: 16 words; agent scope: a fused epilogue on another XCD reads them)
+    // (2 TilePartials: 16 words)
     __hip_atomic_store(a.sparts[2 * blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (!a.fuse_split) return;
-  // the parent's last workgroup to finish finalises both children (waves 0
-  // and 1); every store of this workgroup -- partials, the children's chunk
-  // counts -- completes before it counts itself in
-  __shared__ int slast;
-  __shared__ NodeResult sres[2];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const DevNode* c0 = a.nodes + pt.child[0];
-    const uint32_t nparts = (uint32_t)(c0->split_pe - c0->split_pb);
-    slast = __hip_atomic_fetch_add(a.rdone + (size_t)a.it * a.nn + pt.child[0], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT) == nparts - 1;
-  }
-  __syncthreads();
-  // (the child by a select: pt.child[w] would index the PartTile through scratch)
-  if (slast && w < 2u) split_epilogue_wave(a, w == 0u ? pt.child[0] : pt.child[1], &sres[w]);
 }
 
 // ---------------------------------------------------------------------------
