@@ -63,6 +63,7 @@ Engine::Engine(int device) : device_(device) {
   if (const char* v = getenv("DQ_HIP_LDS_MAP")) use_lds_map_ = v[0] != '0';
   const char* la = getenv("DQ_HIP_LOOKAHEAD");
   if (la && la[0]) lookahead_ = std::max(0, std::min(8, atoi(la)));
+  if (const char* v = getenv("DQ_HIP_SPEC_KMEANS")) speculate_kmeans_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_PLAN")) plan_ = v[0] != '0';
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -799,7 +800,7 @@ void Engine::kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream) {
 // Wait for a round's split epilogue, run its 2-means iterations if any record
 // is still active (host-polled, `lookahead_` launched past the one awaited),
 // then take its results: children nodes, segments, the parents' tiles.
-void Engine::finish_round(int ri, int max_iters, hipStream_t stream) {
+void Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool speculate) {
   Round& R = rounds_[ri];
   const int S = nshard_;
   const double tw0 = tr_wait_us_;
@@ -808,6 +809,12 @@ void Engine::finish_round(int ri, int max_iters, hipStream_t stream) {
   const NodeResult* res = h_res_ + (size_t)R.par * cap_res_;
   int launched = 0, known = 0;
   bool all_proven = false;
+  // Nothing else queued behind this round (a frame's last rounds): its first
+  // 2-means iterations go in before its split status is known -- a record
+  // final at the split makes them exit at once (~4 us each); C3's last round
+  // needs them and otherwise waited ~15 us for the host to see the status.
+  if (speculate && fixed_point_ && S == 1 && comm_ == nullptr)
+    for (; launched < max_iters && launched <= lookahead_; ++launched) kmeans_iter(R, launched, max_iters, stream);
   if (fixed_point_) all_proven = wait_status(stat + max_iters, R.seq, stream) == 0;
   if (R.planned) {   // the plan's counts equal the host's mirror of its layout
     const uint32_t* hc = h_counts_ + 4 * R.par;
@@ -1193,7 +1200,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   while (!q.empty()) {
     const int ri = q.front();
     if (q.size() == 1 && plan_list(ri, &plist)) q.push_back(enqueue_planned_round(ri, plist, max_iters, stream));
-    finish_round(ri, max_iters, stream);
+    finish_round(ri, max_iters, stream, q.size() == 1 && speculate_kmeans_);
     q.pop_front();
     last_rounds++;
     if (rounds_[ri].planned) last_planned++;

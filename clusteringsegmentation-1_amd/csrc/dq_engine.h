@@ -268,7 +268,7 @@ class Engine {
   int enqueue_planned_round(int prev, const std::vector<int32_t>& plist, int max_iters,
                             hipStream_t stream);
   void assign_planned(int ri);
-  void finish_round(int ri, int max_iters, hipStream_t stream);
+  void finish_round(int ri, int max_iters, hipStream_t stream, bool speculate = false);
   void kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream);
   uint64_t tile_len_of(uint64_t len, uint64_t tl) const;
   uint64_t round_tile_len(uint64_t total) const;
@@ -338,7 +338,10 @@ class Engine {
   bool stage_pending_ = false;
   bool plan_ = true;                  // device-planned rounds (DQ_HIP_PLAN=0: host only)
   uint64_t seq_ = 0;                  // round sequence number
-  int lookahead_ = 1;                 // 2-means iterations queued past the one awaited
+  int lookahead_ = 2;                 // 2-means iterations queued past the one awaited
+                                      //   (1: C3 0.543-0.554 ms, 2: 0.518-0.525, 4: 0.520-0.532)
+  bool speculate_kmeans_ = true;      // a round with nothing queued behind it starts its
+                                      //   2-means iterations before its split status (DQ_HIP_SPEC_KMEANS)
   int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TILES)
   int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_NODE_TILES)
   uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TILE_MAX)
