@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-pmc}; shift || true
 O=$R/gpurun_out/$TAG
 mkdir -p $O
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-timing --no-c3 --no-rowtile --no-verify $*"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-timing --no-c3 --no-rowtile --no-bgr --no-verify $*"
 K="--kernel-include-regex (partsplit|pass_kernel|map_|epilogue|build_cells)"
 cd /tmp
 run() {   # name counters...
