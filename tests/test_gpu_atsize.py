@@ -48,6 +48,35 @@ def test_c4_share_batch_default_lanes(gpu):
     _check_centroids(gpu, 256, arrs["means_f07"])
 
 
+def test_c4_share_repeatable(gpu):
+    """The bench workload called 60 times over 1, 2 and 3 engine lanes: every
+    call's colortables equal the reference's and every output equals the
+    first (reference-checked) call's, bit for bit -- the device-planned
+    rounds, lane overlap and fused 2-means epilogues leave no run-to-run
+    differences."""
+    import torch
+    fix = fx.load_json("c4.json")
+    t_in = _frames(range(8))
+    t_out = [torch.empty_like(t) for t in t_in]
+    ref = None
+    try:
+        for c in range(60):
+            gpu.set_lanes(1 + c % 3)
+            cts, _ = gpu.quant_batch_device(t_in, t_out, 256)
+            torch.cuda.synchronize()
+            for f in range(8):
+                assert [int(v) for v in cts[f]] == fix["f%02d" % f]["ct"], (c, f)
+            if ref is None:
+                for f in range(8):
+                    assert "%016x" % fx.fnv(t_out[f].cpu().numpy().view(np.uint32)) == fix["f%02d" % f]["out_fnv"]
+                ref = [t.clone() for t in t_out]
+            else:
+                for f in range(8):
+                    assert torch.equal(t_out[f], ref[f]), (c, f)
+    finally:
+        gpu.set_lanes(0)
+
+
 def test_c4_frames_8_to_63_one_call(gpu):
     """The remaining 56 frames of C4 (the other ranks' shares) in one call."""
     import torch
