@@ -729,6 +729,9 @@ __device__ __forceinline__ void block_cursors(Tile* tiles, const uint32_t* wp, i
   }
 }
 
+#ifndef DQ_RESULT_ORDERED
+#define DQ_RESULT_ORDERED 0
+#endif
 // Final results go straight to host-coherent memory: relaxed system-scope
 // 8-B stores, one per lane (no L2 write-back); the device copy (ddst, may be
 // null) is what the next round's plan reads.  The last word (len_local,
@@ -747,6 +750,7 @@ __device__ __forceinline__ void store_result(NodeResult* dst, NodeResult* ddst, 
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint64_t v = lane < (uint32_t)kWords ? reinterpret_cast<const uint64_t*>(&r)[lane] : 0ull;
+#if DQ_RESULT_ORDERED
   if (lane < (uint32_t)kWords - 1) {
     __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + lane, v, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -758,6 +762,17 @@ __device__ __forceinline__ void store_result(NodeResult* dst, NodeResult* ddst, 
                        __HIP_MEMORY_SCOPE_SYSTEM);
     if (ddst) reinterpret_cast<uint64_t*>(ddst)[lane] = v;
   }
+#else
+  // (all words in one store instruction: the host reads a round's results
+  // only after its status word, which the last arriver publishes after every
+  // record's vmcnt(0) -- the tag check stays as a consistency check; the
+  // ordered form waited one extra host-memory round trip per record)
+  if (lane < (uint32_t)kWords) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + lane, v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    if (ddst) reinterpret_cast<uint64_t*>(ddst)[lane] = v;
+  }
+#endif
 }
 
 // One record's arrival on a launch's counters (lane 0): 64-bit words (low =
