@@ -690,7 +690,7 @@ __device__ __forceinline__ void record_cursors(Tile* tiles, const uint32_t* wp, 
 // workgroup must call it; s_tot: W / 64 words of LDS.
 template <int W>
 __device__ __forceinline__ void block_cursors(Tile* tiles, const uint32_t* wp, int tb, int te,
-                                              uint64_t* s_tot) {
+                                              uint64_t* s_tot, int wbase = 0) {
   const int T = te - tb;
   const int chunk = (T + W - 1) / W;
   const int c0 = tb + (int)threadIdx.x * chunk;
@@ -698,7 +698,7 @@ __device__ __forceinline__ void block_cursors(Tile* tiles, const uint32_t* wp, i
   const uint32_t lane = lane_id(), wv = wave_id();
   uint64_t local = 0;   // old | new << 32
   for (int i = c0; i < c1; ++i) {
-    const u32x4 x = *(const u32x4*)(wp + (size_t)i * kTileWaves);
+    const u32x4 x = *(const u32x4*)(wp + (size_t)(i - wbase) * kTileWaves);
 #pragma unroll
     for (int ww = 0; ww < kTileWaves; ++ww) local += (uint64_t)(x[ww] & 0xFFFFu) | ((uint64_t)(x[ww] >> 16) << 32);
   }
@@ -715,7 +715,7 @@ __device__ __forceinline__ void block_cursors(Tile* tiles, const uint32_t* wp, i
   const uint64_t run0 = base + inc - local;
   uint32_t ro = (uint32_t)run0, rn = (uint32_t)(run0 >> 32);
   for (int i = c0; i < c1; ++i) {
-    const u32x4 x = *(const u32x4*)(wp + (size_t)i * kTileWaves);
+    const u32x4 x = *(const u32x4*)(wp + (size_t)(i - wbase) * kTileWaves);
     u32x4 ob, nb;
 #pragma unroll
     for (int ww = 0; ww < kTileWaves; ++ww) {
@@ -817,13 +817,32 @@ __device__ __forceinline__ void arrive(LaunchCtr* c, uint32_t rec, uint32_t nn, 
 //     node is active (after the split: nodes proven final by
 //     cut_is_fixed_point need no 2-means pass at all).
 constexpr int kEpiBlock = 256;
+// The record and (up to kEpiStageTiles tiles) its per-(tile, wave) counts
+// are staged in LDS at the start, beside the partial sums: the FP64 update
+// and the cursor scan then read LDS, not one dependent global round trip
+// after another; the updated record is written back once.
+constexpr int kEpiStageTiles = 1024;
 template <int KIND, bool FROM_TOT>
 __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
   constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
   if (a.counts && a.counts[2] != 0) return;   // planned round aborted by its plan
-  DevNode* w = a.nodes + blockIdx.x;
+  DevNode* gw = a.nodes + blockIdx.x;
   const uint32_t lane = lane_id();
+  __shared__ __attribute__((aligned(16))) DevNode sw;
+  __shared__ __attribute__((aligned(16))) uint32_t s_wp[kEpiStageTiles * kTileWaves];
+  static_assert(sizeof(DevNode) % 16 == 0, "the record is staged in 16-B words");
+  constexpr int kW16 = (int)(sizeof(DevNode) / 16);
+  typedef __attribute__((address_space(1))) u32x4 g_u4;
+  if (threadIdx.x < (uint32_t)kW16) reinterpret_cast<u32x4*>(&sw)[threadIdx.x] = ((const g_cu4*)gw)[threadIdx.x];
+  __syncthreads();
+  DevNode* w = &sw;
   const bool skip = kMeans && w->done_it != 0;   // final in an earlier launch
+  const int tb = w->tile_begin, te = w->tile_end;
+  const bool stage_wp = (kMeans || KIND == PASS_SPLIT) && !skip && te - tb <= kEpiStageTiles;
+  if (stage_wp) {
+    const g_cu4* wp4 = (const g_cu4*)(a.wparts + (size_t)tb * kTileWaves);
+    for (int i = (int)threadIdx.x; i < te - tb; i += kEpiBlock) reinterpret_cast<u32x4*>(s_wp)[i] = wp4[i];
+  }
   __shared__ NodeResult sres;
   __shared__ uint64_t red[kEpiBlock / 64][8];
   uint64_t tot[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -864,9 +883,13 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
     s_fin = fin;
   }
   __syncthreads();
+  if (!skip && threadIdx.x < (uint32_t)kW16)   // the updated record back (read by later launches)
+    ((g_u4*)gw)[threadIdx.x] = reinterpret_cast<const u32x4*>(&sw)[threadIdx.x];
   const bool final_results = s_fin != 0;
-  if ((kMeans || KIND == PASS_SPLIT) && final_results)
-    block_cursors<kEpiBlock>(a.tiles, a.wparts, w->tile_begin, w->tile_end, s_tot);
+  if ((kMeans || KIND == PASS_SPLIT) && final_results) {
+    if (stage_wp) block_cursors<kEpiBlock>(a.tiles, s_wp, tb, te, s_tot, tb);
+    else block_cursors<kEpiBlock>(a.tiles, a.wparts, tb, te, s_tot);
+  }
   if (wave_id() != 0) return;
   if (kMeans || KIND == PASS_SPLIT) {   // (split: proven fixed points, status slot max_iters)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
