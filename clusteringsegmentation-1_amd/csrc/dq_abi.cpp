@@ -846,8 +846,13 @@ void quant_varpart_fast(const uint32_t numPixels, const uint32_t* inPixels, uint
   j.cols = numCols;
   // uniform weights only for unique 8-bit undecimated input (:1130-1132);
   // else calc_color_table (after cut_bits unless !unique && 8 bits, :1133-1146)
-  if (allPixelsUnique && num_bits == 8 && dec_factor == 1) e.run(&j, 1, max_iters, false, st);
-  else e.run_weighted(j, max_iters, false, st);
+  if (allPixelsUnique && num_bits == 8 && dec_factor == 1) {
+    e.run(&j, 1, max_iters, false, st);
+  } else {
+    if (numRows == 0 || numCols == 0)   // calc_color_table visits no pixel; DivQuantCluster asserts (:211)
+      dq::die("quant_varpart_fast", __FILE__, __LINE__, "numRows and numCols must be > 0 for calc_color_table");
+    e.run_weighted(j, max_iters, false, st);
+  }
   report_empty(j.num_empty);
   const int k = j.k_out;
   *numClustersPtr = (uint32_t)k;
