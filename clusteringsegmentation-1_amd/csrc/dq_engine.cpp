@@ -64,6 +64,7 @@ Engine::Engine(int device) : device_(device) {
   const char* la = getenv("DQ_HIP_LOOKAHEAD");
   if (la && la[0]) lookahead_ = std::max(0, std::min(8, atoi(la)));
   if (const char* v = getenv("DQ_HIP_SPEC_KMEANS")) speculate_kmeans_ = v[0] != '0';
+  if (const char* v = getenv("DQ_HIP_SPIN_SYNC")) spin_sync_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_PLAN")) plan_ = v[0] != '0';
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -259,6 +260,25 @@ void Engine::ensure_round(size_t rec_cap, size_t tiles_cap, size_t, size_t stagi
 
 // Wait for a status word of round `seq`; returns the number of records still
 // active.  Bounded: once the stream has drained the word must be there.
+// The end of a call: an event on the stream, polled with pause (the host's
+// status-word waits spin the same way); hipStreamSynchronize's blocking wait
+// woke the host tens of microseconds after the last kernel (DQ_HIP_SPIN_SYNC=0:
+// hipStreamSynchronize).
+void Engine::sync_stream(hipStream_t stream) {
+  if (!spin_sync_) {
+    DQ_HIP(hipStreamSynchronize(stream));
+    return;
+  }
+  if (!sync_ev_) DQ_HIP(hipEventCreateWithFlags(&sync_ev_, hipEventDisableTiming));
+  DQ_HIP(hipEventRecord(sync_ev_, stream));
+  for (;;) {
+    const hipError_t e = hipEventQuery(sync_ev_);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) die("hipEventQuery", __FILE__, __LINE__, hipGetErrorString(e));
+    for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+  }
+}
+
 uint32_t Engine::wait_status(const uint64_t* slot, uint64_t seq, hipStream_t stream) {
   const double t0 = trace_ ? host_us() : 0.0;
   struct Acc {
@@ -1265,7 +1285,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   }
   // Synchronous on return: lookahead launches of the last round may still be
   // queued, and they read the caller's input.
-  DQ_HIP(hipStreamSynchronize(stream));
+  sync_stream(stream);
   if (trace_) {
     const double t_end = host_us();
     std::fprintf(stderr, "divquant-hip trace: map prep %.1fus, map launch+sync %.1fus\n",
@@ -1758,7 +1778,7 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     }
   }
   const double tm2 = trace_ ? host_us() : 0.0;
-  DQ_HIP(hipStreamSynchronize(stream));
+  sync_stream(stream);
   if (trace_) {
     tr_mapsync_us_ = host_us() - tm2;
     std::fprintf(stderr, "divquant-hip map: first sync %.1fus\n", tm1 - tm0);

@@ -340,6 +340,9 @@ class Engine {
   uint64_t seq_ = 0;                  // round sequence number
   int lookahead_ = 2;                 // 2-means iterations queued past the one awaited
                                       //   (1: C3 0.543-0.554 ms, 2: 0.518-0.525, 4: 0.520-0.532)
+  bool spin_sync_ = true;             // sync_stream polls an event (DQ_HIP_SPIN_SYNC)
+  hipEvent_t sync_ev_ = nullptr;
+  void sync_stream(hipStream_t stream);
   bool speculate_kmeans_ = true;      // a round with nothing queued behind it starts its
                                       //   2-means iterations before its split status (DQ_HIP_SPEC_KMEANS)
   int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TILES)
