@@ -11,34 +11,44 @@ Workload (BASELINE.json metric "Mpixels/sec DivQuant K=256 on 4K RGB"):
   frames this rank owns, already resident in HBM, in ONE batched call.
   Default F = 8: C4's per-GPU share (C4 = 64 4K frames over 8 GPUs, so
   --gpus 8 is exactly C4).  Frames are independent objects: no data-path
-  collective, "scaling": "weak".  The same run also measures C3 (one 4K
-  frame per call: detail.c3) and C4's row-tile variant (all 64 frames, each
-  row-sharded over the N ranks, one RCCL allreduce of every frame's node
-  totals per pass: detail.c4_rowtile).
+  collective, "scaling": "weak".  The same run also measures, each verified
+  against the reference build's outputs:
+    detail.c3         C3: one 4K frame per call;
+    detail.c2         C2: one 1920x1080 frame per call, K=256;
+    detail.c5         C5: the 16384x16384 K=1024 tile, its rows split over the
+                      N ranks, one RCCL allreduce of the node totals per pass
+                      (N=1: the whole tile on one GPU);
+    detail.c4_rowtile C4's row-tile variant: all 64 frames, each row-sharded
+                      over the N ranks, one allreduce of every frame's node
+                      totals per pass;
+    detail.bgr24_input the C3 frame and the rank's batch as BGR24 Mats.
 * --mode rows: F frames of the config (default 1; --config c5: the
-  16384x16384 K=1024 gigapixel tile) row-tile sharded over the N ranks; every
-  pass's integer node totals of all frames are allreduced in one RCCL call
+  16384x16384 K=1024 gigapixel tile) row-tile sharded over the N ranks
   ("scaling": "strong": the total work is fixed).
+
+--gpus N > 1 without a torchrun environment launches N ranks itself
+(torch.distributed.run, one process per GPU, RCCL over xGMI) before any GPU
+call in this process; every rank asserts the world size is N.
 
 Frames are the SURVEY 8c/8d generator (xorshift64, frame f = seed + f); the
 outputs of the timed work are checked against the reference build's golden
 fixtures (tests/golden/c4.json, big.json) after the timed region and the run
-FAILS on a mismatch ("verified" field).
-
-N>1 is launched by torch.distributed.run, one rank per GPU.  Prints ONE JSON
-line on rank 0.  `roofline` is the kernel with the largest measured time in
-the step, timed live on the library's stream with HIP events around every
-launch, against the 8 TB/s HBM peak, with its bytes from the engine work
-model; `traffic` comes from the committed rocprofv3 PMC
-counters of the same command (profiles/pmc_traffic.json).  `cpu_baseline`
-times the reference DivQuant (oracle/_ref, built from the unmodified
-reference sources) -- or, if that build is absent, the oracle's restatement --
-on one 4K frame, one host core, rank 0 at N=1 only.
+FAILS on a mismatch ("verified" fields).  Prints ONE JSON line on rank 0.
+`roofline` is the kernel with the largest measured time in the step, timed
+live on the library's stream with HIP events around every launch, against
+the 8 TB/s HBM peak, with its bytes from the engine work model
+and SURVEY 8(d)'s model beside it; `traffic` comes from the committed
+rocprofv3 PMC counters (profiles/pmc_traffic.json).  `cpu_baseline` times the
+reference DivQuant (oracle/_ref, built from the unmodified reference sources)
+-- or, if that build is absent, the oracle's restatement -- on one 4K frame,
+one host core, rank 0 at N=1 only.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -72,7 +82,7 @@ ROOF_KERNELS = {"pass_kmeans": ("kpass_kernel<PASS_KMEANS>", "3 B read per swept
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -85,17 +95,40 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline region")
     ap.add_argument("--no-c3", action="store_true", help="skip the single-frame C3 measurement")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 (1080p K=256) measurement")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (16384^2 K=1024) measurement")
     ap.add_argument("--no-rowtile", action="store_true", help="skip the C4 row-tile measurement")
     ap.add_argument("--no-bgr", action="store_true", help="skip the BGR24-input measurements")
     ap.add_argument("--no-verify", action="store_true", help="skip the golden-fixture check")
     ap.add_argument("--lanes", type=int, default=0,
                     help="engine lanes per batch (0: library default); the roofline region always uses 1")
-    a = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher and timing harness only (no GPU work; the CPU tests use it)")
+    a = ap.parse_args(argv)
     if a.config is None:
         a.config = "c5" if a.mode == "rows" else "c3"
     if a.frames is None:
         a.frames = 8 if a.mode == "frames" else 1
     return a
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(a):
+    """--gpus N > 1 without a torchrun environment: run this script as N
+    ranks under torch.distributed.run (one process per GPU) and return their
+    exit code.  Nothing here touches the GPU (the ranks do)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    return subprocess.call(cmd, env=env)
 
 
 def cpu_baseline(w, h, k):
@@ -230,14 +263,12 @@ def check_frame(pkg, out_t, ct, fix, rows=None, h=None, world=1, rank=0):
                          "first_diff": next((i for i, (x, y) in enumerate(zip(got, fix["ct"])) if x != y), None)})
         return False
     out = out_t.cpu().numpy().view(np.uint32)
-    if rows is None:
+    if rows is None or world == 1:
         ok = "%016x" % pkg.fnv1a64(out) == fix["out_fnv"]
         if not ok:
             MISMATCH.append({"what": "out"})
         return ok
     bands = fix.get("band_fnv")
-    if world == 1:
-        return "%016x" % pkg.fnv1a64(out) == fix["out_fnv"]
     if not bands or 8 % world != 0:
         return None
     per = 8 // world   # this rank's rows = bands [rank*per, (rank+1)*per)
@@ -247,8 +278,14 @@ def check_frame(pkg, out_t, ct, fix, rows=None, h=None, world=1, rank=0):
         b = rank * per + j
         lo = (b * bh - rows[0]) * w
         if "%016x" % pkg.fnv1a64(out[lo:lo + bh * w]) != bands[b]:
+            MISMATCH.append({"what": "band", "band": b})
             return False
     return True
+
+
+def fail(msg, rank, **kw):
+    print(json.dumps(dict({"error": msg, "rank": rank, "mismatch": MISMATCH}, **kw)), flush=True)
+    sys.exit(3)
 
 
 def pick_roofline(stats, pmc_key):
@@ -295,22 +332,114 @@ def upload_frames(torch, pkg, dev, w, h, ids, rows=None):
     return ts
 
 
+def rows_leg(ctx, cfg, nf, steps, warmup, verify):
+    """nf frames of config `cfg`, each row-sharded over the ranks (one RCCL
+    allreduce of all frames' node totals per pass); returns (dt, verified,
+    comm ranks).  The communicator exists only inside the leg."""
+    torch, pkg, dev, local, rank, world, stream = (ctx[k] for k in
+                                                   ("torch", "pkg", "dev", "local", "rank", "world", "stream"))
+    w, h, k = CONFIGS[cfg]
+    n = w * h
+    if world > 1:
+        pkg.comm_init_torch(device=local)
+    comm = pkg.comm_size(device=local)
+    r0, r1 = row_range(h, rank, world)
+    fr = upload_frames(torch, pkg, dev, w, h, range(nf), rows=(r0, r1))
+    out = [torch.empty_like(f) for f in fr]
+    last = {}
+
+    def step():
+        last["cts"], _ = pkg.quant_rows_device(fr, out, k, widths=[w] * nf, n_globals=[n] * nf, nshard=1,
+                                               max_iters=10, device=local, stream=stream)
+    for _ in range(warmup):
+        step()
+    dt = max_over_ranks(timed_region(step, steps, world, ctx["sync"]), world, dev)
+    ok = None
+    if verify:
+        ctx["sync"]()
+        rr = [check_frame(pkg, out[i], last["cts"][i], frame_fixture(w, h, k, i), rows=(r0, r1), h=h,
+                          world=world, rank=rank) for i in range(nf)]
+        checked = [r for r in rr if r is not None]
+        ok = all_ranks_ok(all(checked), world, dev) if checked else None
+        if ok is False:
+            fail("%s row-tile outputs differ from the reference fixtures" % cfg.upper(), rank,
+                 per_frame=rr)
+    if world > 1:
+        pkg.comm_destroy(device=local)
+    del fr, out
+    torch.cuda.empty_cache()
+    return dt, ok, comm
+
+
+def frame_leg(ctx, cfg, steps, verify):
+    """One frame of config `cfg` per call (this rank's frame 0 of the config:
+    the fixture's frame at N=1); returns (dt, verified)."""
+    torch, pkg, dev, local, rank, world, stream = (ctx[k] for k in
+                                                   ("torch", "pkg", "dev", "local", "rank", "world", "stream"))
+    w, h, k = CONFIGS[cfg]
+    # C3: this rank's first frame (C4's fixtures hold all 64); C2: frame 0 on
+    # every rank (replicas: the one frame with a fixture)
+    fid = frame_id(rank, 0, ctx["nf"]) if cfg == "c3" else 0
+    t_in = upload_frames(torch, pkg, dev, w, h, [fid])[0]
+    t_out = torch.empty_like(t_in)
+    last = {}
+
+    def one():
+        last["ct"], _ = pkg.quant_device(t_in, t_out, k, max_iters=10, device=local, stream=stream)
+    for _ in range(3):
+        one()
+    dt = max_over_ranks(timed_region(one, steps, world, ctx["sync"]), world, dev)
+    ok = None
+    if verify:
+        ctx["sync"]()
+        r = check_frame(pkg, t_out, last["ct"], frame_fixture(w, h, k, fid))
+        ok = all_ranks_ok(r is not False, world, dev)
+        if r is None and world == 1:
+            ok = None
+        if ok is False:
+            fail("%s output differs from the reference fixture" % cfg.upper(), rank)
+    return dt, ok
+
+
+def dry_run(a, rank, world):
+    """--dry-run: the launcher and the timing harness without GPU work."""
+    if world != a.gpus:
+        raise SystemExit("bench: --gpus %d but the launcher started %d rank(s)" % (a.gpus, world))
+    dt = max_over_ranks(timed_region(lambda: time.sleep(0.01 * (rank + 1)), a.steps, world, lambda: None), world)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run", "value": 0.0, "n_gpus": world, "steps": a.steps,
+                          "ms_per_step": round(dt * 1e3 / a.steps, 3), "dry_run": True}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    rank, world, local = init_dist()
+    if world != a.gpus:
+        raise SystemExit("bench: --gpus %d but %d rank(s) in the torchrun environment" % (a.gpus, world))
+    if a.dry_run:
+        dry_run(a, rank, world)
+        return
     import torch
     from __graft_entry__ import load_package
 
-    rank, world, local = init_dist()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pkg = load_package()
     stream = torch.cuda.current_stream(dev)
     sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+    ctx = {"torch": torch, "pkg": pkg, "dev": dev, "local": local, "rank": rank, "world": world,
+           "stream": stream, "sync": sync, "nf": a.frames}
+    verify = not a.no_verify
 
     w, h, k = CONFIGS[a.config]
     n = w * h
     nf = a.frames
-    verify = []   # (name, out tensor, colortable getter, fixture, rows)
+    comm_ranks = None
     if a.mode == "frames":
         ids = [frame_id(rank, i, nf) for i in range(nf)]
         frames = upload_frames(torch, pkg, dev, w, h, ids)
@@ -327,12 +456,13 @@ def main():
         px_per_step = n * nf * world
         workload = ("C4 per-GPU share: %d x %dx%d frames per rank per step, K=%d, quant_recurse "
                     "max_iters=10 (cluster + dedup + map), one batched call" % (nf, w, h, k)
-                    if nf > 1 else "C3: one %dx%d frame per step, K=%d, quant_recurse" % (w, h, k))
+                    if nf > 1 else "one %dx%d frame per step, K=%d, quant_recurse" % (w, h, k))
         parallelism = "frames-per-rank x%d" % world
         scaling = "weak"
     else:
         if world > 1:
             pkg.comm_init_torch(device=local)
+        comm_ranks = pkg.comm_size(device=local)
         r0, r1 = row_range(h, rank, world)
         frames = upload_frames(torch, pkg, dev, w, h, range(nf), rows=(r0, r1))
         outs = [torch.empty_like(f) for f in frames]
@@ -356,17 +486,15 @@ def main():
     dt = timed_region(step, a.steps, world, sync)
     # --- correctness of the timed work: the last step's outputs vs the reference
     verified = None
-    if not a.no_verify:
+    if verify:
         sync()
         res = []
         for i in range(nf):
             if a.mode == "frames":
-                fix = frame_fixture(w, h, k, ids[i])
-                res.append(check_frame(pkg, outs[i], last["cts"][i], fix))
+                res.append(check_frame(pkg, outs[i], last["cts"][i], frame_fixture(w, h, k, ids[i])))
             else:
-                fix = frame_fixture(w, h, k, i)
-                res.append(check_frame(pkg, outs[i], last["cts"][i], fix, rows=(r0, r1), h=h,
-                                       world=world, rank=rank))
+                res.append(check_frame(pkg, outs[i], last["cts"][i], frame_fixture(w, h, k, i), rows=(r0, r1),
+                                       h=h, world=world, rank=rank))
         checked = [r for r in res if r is not None]
         ok = all_ranks_ok(all(checked), world, dev)
         verified = {"ok": ok, "frames_checked_rank0": len(checked), "frames_rank0": nf,
@@ -374,10 +502,7 @@ def main():
                                % ("c4.json" if (w, h, k) == (3840, 2160, 256) else "big.json",
                                   " of this rank's row bands" if a.mode == "rows" and world > 1 else "")}
         if not ok:
-            print(json.dumps({"error": "bench outputs differ from the reference fixtures",
-                              "verified": verified, "per_frame_rank%d" % rank: res, "mismatch": MISMATCH}),
-                  flush=True)
-            sys.exit(3)
+            fail("bench outputs differ from the reference fixtures", rank, verified=verified, per_frame=res)
     # --- roofline region: the same steps again with HIP events around every
     # launch (on the library's launch stream) for per-kernel durations
     stats = {}
@@ -397,37 +522,31 @@ def main():
     rounds = pkg.last_rounds(device=local)
     swept = pkg.last_points_swept(device=local)
     full = pkg.last_points_full(device=local)
+    dt = max_over_ranks(dt, world, dev)
+    value = px_per_step * a.steps / dt / 1e6
 
-    # --- C3 single-frame latency (same frame shape, one frame per call)
-    c3 = None
-    if a.mode == "frames" and not a.no_c3 and nf > 1:
-        last3 = {}
-
-        def one():
-            last3["ct"], _ = pkg.quant_device(frames[0], outs[0], k, max_iters=10, device=local,
-                                              stream=stream)
-        for _ in range(2):
-            one()
-        dt1 = timed_region(one, a.steps, world, sync)
-        dt1 = max_over_ranks(dt1, world, dev)
-        ok1 = None
-        if not a.no_verify:
-            sync()
-            ok1 = all_ranks_ok(check_frame(pkg, outs[0], last3["ct"], frame_fixture(w, h, k, ids[0])) is not False,
-                               world, dev)
-            if not ok1:
-                print(json.dumps({"error": "C3 output differs from the reference fixture"}), flush=True)
-                sys.exit(3)
-        c3 = {"ms_per_frame": round(dt1 * 1e3 / a.steps, 3),
-              "Mpix_per_s": round(n * world * a.steps / dt1 / 1e6, 2),
-              "workload": "one %dx%d frame per call (C3), %d rank(s)" % (w, h, world),
-              "verified": ok1}
+    detail = {}
+    big4k = a.mode == "frames" and (w, h, k) == (3840, 2160, 256)
+    # --- C3: one 4K frame per call (this rank's first frame)
+    if big4k and not a.no_c3 and nf > 1:
+        dt1, ok1 = frame_leg(ctx, "c3", a.steps, verify)
+        detail["c3"] = {"ms_per_frame": round(dt1 * 1e3 / a.steps, 3),
+                        "Mpix_per_s": round(n * world * a.steps / dt1 / 1e6, 2),
+                        "workload": "one 3840x2160 frame per call (C3), K=256, %d rank(s)" % world,
+                        "verified": ok1}
+    # --- C2: one 1920x1080 frame per call, K=256
+    if a.mode == "frames" and not a.no_c2:
+        w2, h2, _ = CONFIGS["c2"]
+        dt2, ok2 = frame_leg(ctx, "c2", a.steps, verify)
+        detail["c2"] = {"ms_per_frame": round(dt2 * 1e3 / a.steps, 3),
+                        "Mpix_per_s": round(w2 * h2 * world * a.steps / dt2 / 1e6, 2),
+                        "workload": "one 1920x1080 frame per call (C2), K=256, %d rank(s) (replicas)" % world,
+                        "verified": ok2}
 
     # --- the same frames as OpenCV BGR24 Mats: read directly by
     # the root's passes, partition and map (3 B per pixel, no packing pass);
     # one frame per call (C3 shape) and the rank's batch in one call
-    bgr = None
-    if a.mode == "frames" and not a.no_bgr and nf > 1:
+    if big4k and not a.no_bgr and nf > 1:
         bf = []
         for t in frames:
             p = t.view(torch.int32)
@@ -443,7 +562,7 @@ def main():
             bone()
         dtb1 = max_over_ranks(timed_region(bone, a.steps, world, sync), world, dev)
         okb1 = None
-        if not a.no_verify:
+        if verify:
             sync()
             okb1 = all_ranks_ok(check_frame(pkg, outs[0], lastb["ct"], frame_fixture(w, h, k, ids[0])) is not False,
                                 world, dev)
@@ -451,61 +570,47 @@ def main():
             bbatch()
         dtb = max_over_ranks(timed_region(bbatch, a.steps, world, sync), world, dev)
         okb = None
-        if not a.no_verify:
+        if verify:
             sync()
             okb = all_ranks_ok(all(check_frame(pkg, outs[i], lastb["cts"][i], frame_fixture(w, h, k, ids[i]))
                                    is not False for i in range(nf)), world, dev)
         if okb1 is False or okb is False:
-            print(json.dumps({"error": "BGR24-input outputs differ from the reference fixtures"}), flush=True)
-            sys.exit(3)
-        bgr = {"c3_ms_per_frame": round(dtb1 * 1e3 / a.steps, 3),
-               "c3_Mpix_per_s": round(n * world * a.steps / dtb1 / 1e6, 2),
-               "batch_ms_per_step": round(dtb * 1e3 / a.steps, 3),
-               "batch_Mpix_per_s": round(n * nf * world * a.steps / dtb / 1e6, 2),
-               "workload": "the same frames as BGR24 (CV_8UC3) device buffers: one frame per call, and %d frames "
-                           "per rank in one batched call (dq_hip_quant_bgr24[_batch]_dev)" % nf,
-               "verified": None if okb is None else bool(okb1 and okb)}
+            fail("BGR24-input outputs differ from the reference fixtures", rank)
+        detail["bgr24_input"] = {
+            "c3_ms_per_frame": round(dtb1 * 1e3 / a.steps, 3),
+            "c3_Mpix_per_s": round(n * world * a.steps / dtb1 / 1e6, 2),
+            "batch_ms_per_step": round(dtb * 1e3 / a.steps, 3),
+            "batch_Mpix_per_s": round(n * nf * world * a.steps / dtb / 1e6, 2),
+            "workload": "the same frames as BGR24 (CV_8UC3) device buffers: one frame per call, and %d frames "
+                        "per rank in one batched call (dq_hip_quant_bgr24[_batch]_dev)" % nf,
+            "verified": None if okb is None else bool(okb1 and okb)}
         del bf
 
-    # --- C4 row-tile variant: all 64 frames, each row-sharded over the ranks
-    rowtile = None
-    if a.mode == "frames" and not a.no_rowtile and (w, h, k) == (3840, 2160, 256):
+    if a.mode == "frames":
         del frames, outs
         torch.cuda.empty_cache()
-        if world > 1:
-            pkg.comm_init_torch(device=local)
-        r0, r1 = row_range(h, rank, world)
-        nrt = 64
-        rf = upload_frames(torch, pkg, dev, w, h, range(nrt), rows=(r0, r1))
-        ro = [torch.empty_like(f) for f in rf]
-        lastr = {}
-
-        def rstep():
-            lastr["cts"], _ = pkg.quant_rows_device(rf, ro, k, widths=[w] * nrt, n_globals=[n] * nrt,
-                                                    nshard=1, max_iters=10, device=local, stream=stream)
-        rstep()
+    # --- C5: the gigapixel tile, rows over the ranks (N=1: whole on one GPU)
+    if a.mode == "frames" and not a.no_c5:
+        w5, h5, k5 = CONFIGS["c5"]
+        s5 = max(1, min(5, a.steps))
+        dt5, ok5, comm5 = rows_leg(ctx, "c5", 1, s5, 2, verify)
+        comm_ranks = comm5
+        detail["c5"] = {"ms_per_tile": round(dt5 * 1e3 / s5, 3),
+                        "Mpix_per_s": round(w5 * h5 * s5 / dt5 / 1e6, 2), "steps": s5,
+                        "workload": "C5: one 16384x16384 tile, K=1024, rows split over %d rank(s), one RCCL "
+                                    "allreduce of the node totals per pass" % world,
+                        "scaling": "strong", "verified": ok5}
+    # --- C4 row-tile variant: all 64 frames, each row-sharded over the ranks
+    if big4k and not a.no_rowtile:
         rsteps = max(1, min(3, a.steps))
-        dtr = max_over_ranks(timed_region(rstep, rsteps, world, sync), world, dev)
-        okr = None
-        if not a.no_verify:
-            sync()
-            rr = [check_frame(pkg, ro[i], lastr["cts"][i], frame_fixture(w, h, k, i), rows=(r0, r1), h=h,
-                              world=world, rank=rank) for i in range(nrt)]
-            okr = all_ranks_ok(all(r is not False for r in rr), world, dev)
-            if not okr:
-                print(json.dumps({"error": "C4 row-tile outputs differ from the reference fixtures"}), flush=True)
-                sys.exit(3)
-        rowtile = {"ms_per_step": round(dtr * 1e3 / rsteps, 3),
-                   "Mpix_per_s": round(n * nrt * rsteps / dtr / 1e6, 2), "steps": rsteps,
-                   "workload": "C4 row-tile variant: 64 x %dx%d frames, K=%d, each frame's rows split over "
-                               "%d rank(s), one RCCL allreduce of all frames' node totals per pass"
-                               % (w, h, k, world),
-                   "scaling": "strong", "verified": okr}
-        if world > 1:
-            pkg.comm_destroy(device=local)
-
-    dt = max_over_ranks(dt, world, dev)
-    value = px_per_step * a.steps / dt / 1e6
+        dtr, okr, commr = rows_leg(ctx, "c3", 64, rsteps, 1, verify)
+        comm_ranks = commr
+        detail["c4_rowtile"] = {
+            "ms_per_step": round(dtr * 1e3 / rsteps, 3),
+            "Mpix_per_s": round(n * 64 * rsteps / dtr / 1e6, 2), "steps": rsteps,
+            "workload": "C4 row-tile variant: 64 x %dx%d frames, K=%d, each frame's rows split over "
+                        "%d rank(s), one RCCL allreduce of all frames' node totals per pass" % (w, h, k, world),
+            "scaling": "strong", "verified": okr}
 
     if rank == 0:
         pmc_key = "%s_%s_f%d_n%d" % (a.mode, a.config, nf, world)
@@ -513,6 +618,17 @@ def main():
         # engine-model bytes of all kernels of the roofline region, per step,
         # over the timed step's wall time (<= 1: they are bytes the kernels move)
         eng_bytes = sum(v[2] for v in stats.values()) / max(1, a.steps)
+        detail.update({
+            "ms_per_frame": round(dt * 1e3 / a.steps / (nf * world if a.mode == "frames" else nf), 3),
+            "pipeline_engine_GBps_per_gpu": round(eng_bytes / (dt / a.steps) / 1e9, 1) if stats else None,
+            "pipeline_engine_frac_per_gpu": round(eng_bytes / (dt / a.steps) / 1e9 / HBM_PEAK_GBS, 4)
+            if stats else None,
+            "rounds_last_frame": rounds, "points_swept_last_call": swept,
+            "points_full_iterations_last_call": full,
+            "rccl_comm_ranks": comm_ranks,
+            "kernels": {kname: {"launches": v[0], "ms": round(v[1], 3),
+                                "GBps": round(v[2] / (v[1] / 1e3) / 1e9, 1) if v[1] > 0 and v[2] > 0 else None}
+                        for kname, v in stats.items() if v[0]}})
         res = {
             "metric": "Mpixels/sec DivQuant K=%d on %dx%d RGB" % (k, w, h),
             "value": round(value, 2),
@@ -532,18 +648,7 @@ def main():
                        "width": w, "height": h, "k": k, "max_iters": 10, "parallelism": parallelism},
             "verified": verified,
             "roofline": roof,
-            "detail": {"ms_per_frame": round(dt * 1e3 / a.steps / (nf * world if a.mode == "frames" else nf), 3),
-                       "pipeline_engine_GBps_per_gpu": round(eng_bytes / (dt / a.steps) / 1e9, 1) if stats else None,
-                       "pipeline_engine_frac_per_gpu": round(eng_bytes / (dt / a.steps) / 1e9 / HBM_PEAK_GBS, 4)
-                       if stats else None,
-                       "rounds_last_frame": rounds, "points_swept_last_call": swept,
-                       "points_full_iterations_last_call": full,
-                       "c3": c3,
-                       "bgr24_input": bgr,
-                       "c4_rowtile": rowtile,
-                       "kernels": {kname: {"launches": v[0], "ms": round(v[1], 3),
-                                           "GBps": round(v[2] / (v[1] / 1e3) / 1e9, 1) if v[1] > 0 and v[2] > 0 else None}
-                                   for kname, v in stats.items() if v[0]}},
+            "detail": detail,
         }
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(3840, 2160, 256)

@@ -73,6 +73,7 @@ def lib():
         "dq_hip_comm_unique_id": ([vp], c.c_int),
         "dq_hip_comm_init": ([c.c_int, c.c_int, c.c_int, vp], c.c_int),
         "dq_hip_comm_destroy": ([c.c_int], c.c_int),
+        "dq_hip_comm_size": ([c.c_int], c.c_int),
         "dq_hip_cluster_dev": ([c.c_int, vp, c.c_uint32, u32p, vp, c.c_int, vp], c.c_int),
         "dq_hip_map_dev": ([c.c_int, vp, c.c_uint32, vp, vp, c.c_int, vp], c.c_int),
         "dq_hip_quant_weighted_dev": ([c.c_int, vp, c.c_uint32, vp, u32p, vp, c.c_int, vp], c.c_int),
@@ -112,6 +113,8 @@ def lib():
         "dq_hip_map_bgr24_dev": ([c.c_int, vp, c.c_uint32, c.c_uint32, c.c_uint32, vp, vp, c.c_int, vp],
                                  c.c_int),
         "quant_recurse": ([c.c_uint32, vp, vp, u32p, vp, c.c_int], None),
+        "dq_hip_build_id": ([], c.c_uint64),
+        "dq_hip_set_debug": ([c.c_int, c.c_int], None),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -342,6 +345,11 @@ def comm_destroy(device=0):
     lib().dq_hip_comm_destroy(device)
 
 
+def comm_size(device=0):
+    """Ranks of the engine's RCCL communicator on `device` (1: none)."""
+    return lib().dq_hip_comm_size(device)
+
+
 def comm_init_torch(device=0, group=None):
     """comm_init over an initialised torch.distributed process group: rank 0's
     id is broadcast with the group (any backend), then every rank joins."""
@@ -532,6 +540,18 @@ def set_lanes(lanes):
 
 def get_lanes():
     return lib().dq_hip_get_lanes()
+
+
+def build_id():
+    """FNV-1a-64 of the sources the loaded library was built from (tools/source_id.py)."""
+    return int(lib().dq_hip_build_id())
+
+
+def set_debug(flags, device=0):
+    """Test-only interleaving knobs (dq_hip.h dq_hip_set_debug; 0 in production):
+    1 prewarm the 2-means hand-off lines, 2 uneven workgroup stalls, 4 host
+    delays between a round's status and its results, 8 plan-kernel stall."""
+    lib().dq_hip_set_debug(device, int(flags))
 
 
 def set_timing(on, device=0):

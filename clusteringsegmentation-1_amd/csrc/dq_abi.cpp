@@ -72,14 +72,19 @@ void report_empty(int num_empty) {
 // Persistent host threads for the batch lanes 1..L-1 (a std::thread per lane
 // per call cost tens of microseconds of every call's host time).  run()
 // hands job(i) to worker i, runs job(0) on the caller and returns when all
-// are done; workers spin briefly on the generation word before sleeping.
+// are done.  A worker reads the generation, the job and the lane count
+// together under mu_ (run() publishes them together under mu_), so it runs
+// each generation's job at most once; a thread starts with `seen` = the
+// generation current when it was created.  Workers spin briefly on the
+// generation word before sleeping on the condition variable.
 class LaneWorkers {
  public:
   void run(int n, const std::function<void(int)>& job) {
     std::lock_guard<std::mutex> call(call_mu_);
     while ((int)threads_.size() < n - 1) {
       const int id = (int)threads_.size() + 1;
-      threads_.emplace_back([this, id] { loop(id); });
+      const uint64_t g0 = gen_.load(std::memory_order_acquire);   // (no publish in flight: call_mu_)
+      threads_.emplace_back([this, id, g0] { loop(id, g0); });
       threads_.back().detach();
     }
     {
@@ -102,24 +107,16 @@ class LaneWorkers {
   }
 
  private:
-  void loop(int id) {
-    uint64_t seen = 0;
+  void loop(int id, uint64_t seen) {
     for (;;) {
-      uint64_t g = gen_.load(std::memory_order_acquire);
-      for (uint32_t spin = 0; g == seen && spin < (1u << 14); ++spin) {
+      for (uint32_t spin = 0; gen_.load(std::memory_order_acquire) == seen && spin < (1u << 14); ++spin)
         __builtin_ia32_pause();
-        g = gen_.load(std::memory_order_acquire);
-      }
-      if (g == seen) {
-        std::unique_lock<std::mutex> l(mu_);
-        cv_.wait(l, [&] { return gen_.load(std::memory_order_acquire) != seen; });
-        g = gen_.load(std::memory_order_acquire);
-      }
-      seen = g;
       const std::function<void(int)>* job;
       int n;
       {
-        std::lock_guard<std::mutex> l(mu_);
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
+        seen = gen_.load(std::memory_order_relaxed);   // the generation job_ / nact_ belong to
         job = job_;
         n = nact_;
       }
@@ -141,16 +138,64 @@ class LaneWorkers {
   std::vector<std::thread> threads_;
 };
 
+// Events for one-shot cross-stream joins (a call's "inputs ready" mark, a
+// NULL-stream call's completion), one per use: concurrent calls never share
+// one (an event re-recorded by another call before a stream waited on it
+// would order the wait after the wrong work).  A stream wait captures the
+// event's state when it is enqueued, so the event returns to the pool as
+// soon as every wait on it has been enqueued.
+class EventPool {
+ public:
+  hipEvent_t get() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!free_.empty()) {
+        hipEvent_t e = free_.back();
+        free_.pop_back();
+        return e;
+      }
+    }
+    hipEvent_t e = nullptr;
+    DQ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+  }
+  void put(hipEvent_t e) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(e);
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<hipEvent_t> free_;
+};
+
+EventPool& events() {
+  static EventPool* p = new EventPool();   // (never destroyed, like the engines)
+  return *p;
+}
+
 // The stream a device-pointer entry runs on: the caller's, or (NULL) the
 // engine's non-blocking stream made to wait for the legacy default stream
 // first -- the caller's inputs may still be in flight there (a torch
 // host-to-device copy on the default stream, say).
 hipStream_t dev_stream(Engine& e, void* stream) {
   if (stream) return (hipStream_t)stream;
-  hipEvent_t ev = e.ready_event();
+  hipEvent_t ev = events().get();
   DQ_HIP(hipEventRecord(ev, nullptr));
   DQ_HIP(hipStreamWaitEvent(e.stream(), ev, 0));
+  events().put(ev);
   return e.stream();
+}
+
+// An asynchronous entry called with stream NULL ran on the engine's stream:
+// order the legacy default stream after it, so work the caller queues there
+// next (a framework's copy of the outputs) sees the results.
+void join_default_stream(void* stream, hipStream_t used) {
+  if (stream) return;
+  hipEvent_t ev = events().get();
+  DQ_HIP(hipEventRecord(ev, used));
+  DQ_HIP(hipStreamWaitEvent(nullptr, ev, 0));
+  events().put(ev);
 }
 
 LaneWorkers& lane_workers() {
@@ -240,6 +285,7 @@ int dq_hip_cut_bits_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t* 
   hipStream_t st = engine_stream(device, stream);
   dq::launch_cut_gather(d_in, d_out, 1, n, 1, 1, (uint32_t)(8 - nbr), (uint32_t)(8 - nbg),
                         (uint32_t)(8 - nbb), st);
+  join_default_stream(stream, st);
   return 0;
 }
 
@@ -281,6 +327,7 @@ int dq_hip_block_hist_dev(int device, const uint32_t* d_in, uint32_t width, uint
                       work, nullptr, 0};
   const int rc = dq::launch_block_hist(a, (int)dim, st);
   DQ_HIP(hipFreeAsync(work, st));
+  join_default_stream(stream, st);
   return rc;
 }
 
@@ -298,7 +345,9 @@ static hipStream_t engine_stream(int device, void* stream) {
 int dq_hip_pack_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t width, uint32_t height,
                           uint32_t stride, uint32_t* d_out, void* stream) {
   if (!d_bgr || !d_out || !bgr24_shape_ok(width, height, stride)) return -1;
-  dq::launch_bgr24_pack(d_bgr, width, height, stride, d_out, engine_stream(device, stream));
+  hipStream_t st = engine_stream(device, stream);
+  dq::launch_bgr24_pack(d_bgr, width, height, stride, d_out, st);
+  join_default_stream(stream, st);
   DQ_HIP(hipGetLastError());
   return 0;
 }
@@ -306,7 +355,9 @@ int dq_hip_pack_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t width, uint
 int dq_hip_unpack_bgr24_dev(int device, const uint32_t* d_in, uint32_t width, uint32_t height,
                             uint32_t stride, uint8_t* d_bgr, void* stream) {
   if (!d_in || !d_bgr || !bgr24_shape_ok(width, height, stride)) return -1;
-  dq::launch_bgr24_unpack(d_in, width, height, stride, d_bgr, engine_stream(device, stream));
+  hipStream_t st = engine_stream(device, stream);
+  dq::launch_bgr24_unpack(d_in, width, height, stride, d_bgr, st);
+  join_default_stream(stream, st);
   DQ_HIP(hipGetLastError());
   return 0;
 }
@@ -315,7 +366,9 @@ int dq_hip_gather_bgr24_dev(int device, const uint8_t* d_bgr, uint32_t stride,
                             const uint32_t* d_coords, uint32_t n, uint32_t* d_out, void* stream) {
   if (!d_bgr || !d_coords || !d_out || stride < 3u) return -1;
   if (n == 0) return 0;
-  dq::launch_bgr24_gather(d_bgr, stride, d_coords, n, d_out, engine_stream(device, stream));
+  hipStream_t st = engine_stream(device, stream);
+  dq::launch_bgr24_gather(d_bgr, stride, d_coords, n, d_out, st);
+  join_default_stream(stream, st);
   DQ_HIP(hipGetLastError());
   return 0;
 }
@@ -333,7 +386,7 @@ static int quant_batch(int device, std::vector<dq::FrameJob>& jobs, int max_iter
     // frames [f0(l), f0(l+1)) on lane l; every lane first waits for the
     // caller's stream (the frames may have been produced there)
     DQ_HIP(hipSetDevice(device));
-    hipEvent_t ready = e0.ready_event();
+    hipEvent_t ready = events().get();   // this call's own (concurrent calls: one each)
     DQ_HIP(hipEventRecord(ready, (hipStream_t)stream));
     for (int l = 1; l < lanes; ++l) {   // lanes inherit lane 0's switches
       Engine& e = engine_for(device, l);
@@ -350,6 +403,7 @@ static int quant_batch(int device, std::vector<dq::FrameJob>& jobs, int max_iter
       e.run(jobs.data() + f0, f1 - f0, max_iters, true, e.stream());
     };
     lane_workers().run(lanes, work);
+    events().put(ready);   // (every lane's wait on it is enqueued)
     // lane 0 reports for the batch: the last frame's diagnostics, summed counters
     Engine& el = engine_for(device, lanes - 1);
     std::lock_guard<std::mutex> g(e0.mutex());
@@ -519,6 +573,8 @@ int dq_hip_comm_init(int device, int nranks, int rank, const void* id128) {
   e.comm_init(nranks, rank, static_cast<const char*>(id128));
   return 0;
 }
+
+int dq_hip_comm_size(int device) { return engine_for(device).comm_ranks(); }
 
 int dq_hip_comm_destroy(int device) {
   Engine& e = engine_for(device);
@@ -740,6 +796,11 @@ void dq_hip_set_planned_rounds(int device, int on) {
 int dq_hip_last_planned_rounds(int device) { return engine_for(device).last_planned; }
 
 void dq_hip_set_timing(int device, int on) { engine_for(device).set_timing(on != 0); }
+
+void dq_hip_set_debug(int device, int flags) {
+  (void)device;   // (process-wide: every engine reads it when a run starts)
+  dq::set_debug_flags(flags);
+}
 
 void dq_hip_set_lanes(int lanes) { dq::set_batch_lanes(lanes); }
 int dq_hip_get_lanes(void) { return dq::batch_lanes(); }

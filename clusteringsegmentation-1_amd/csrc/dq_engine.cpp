@@ -121,6 +121,12 @@ void Engine::collect_timing() {
   pending_.clear();
 }
 
+void Engine::debug_host_delay() const {
+  if (!(debug_ & kDebugHostDelay)) return;
+  const double t0 = host_us();
+  while (host_us() - t0 < 200.0) __builtin_ia32_pause();
+}
+
 void Engine::reset_stats() {
   for (auto& s : stats) s = KernelStat();
 }
@@ -348,6 +354,7 @@ uint64_t Engine::tile_len_of(uint64_t len, uint64_t tl) const {
 // split, so the leaves of the last round never are.
 int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_round, int max_iters,
                                hipStream_t stream) {
+  debug_host_delay();
   const double tb0 = trace_ ? host_us() : 0.0;
   const int S = nshard_;
   const bool sharded = S > 1 || comm_ != nullptr;
@@ -580,7 +587,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   ra.nn = nr;
   ra.tot = d_tot_;
   ra.nshard = S;
-  ra.pad = 0;
+  ra.debug = debug_;
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = nullptr;
@@ -718,6 +725,8 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   pa.p0 = reinterpret_cast<const uint8_t*>(d_p0_);
   pa.p1 = reinterpret_cast<const uint8_t*>(d_p1_);
   pa.cap_bytes = 4 * cap_px_;
+  pa.debug = debug_;
+  pa.pad = 0;
   RoundArgs& ra = R.ra;
   ra.tiles = R.dt;
   ra.nodes = R.dn;
@@ -734,7 +743,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   ra.nn = R.nr;
   ra.tot = d_tot_;
   ra.nshard = 1;
-  ra.pad = 0;
+  ra.debug = debug_;
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = R.dcounts;
@@ -844,6 +853,7 @@ void Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specul
                  __atomic_load_n(hc + 1, __ATOMIC_ACQUIRE) == (uint32_t)R.nptiles,
              "plan_kernel's tile counts differ from the host's mirror");
   }
+  debug_host_delay();
   R.kmeans = !all_proven;
   while (!all_proven) {
     while (launched < max_iters && launched <= known + lookahead_) {
@@ -855,6 +865,7 @@ void Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specul
     if (act == 0) break;
     DQ_CHECK(known < max_iters, "nodes still active after the last 2-means iteration");
   }
+  debug_host_delay();
   const double tp0 = trace_ ? host_us() : 0.0;
   const int nl = R.nl;
   // Every record's result carries the round's tag, stored after its other
@@ -1090,6 +1101,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   DQ_CHECK(max_iters >= 1, "max_iters < 1 is not supported (the reference never writes member[] then)");
   DQ_HIP(hipSetDevice(device_));
   if (!stream) stream = stream_;
+  debug_ = debug_flags();
 
   frames_.assign(nframes, FrameState());
   nodes_.clear();
@@ -1818,5 +1830,9 @@ int batch_lanes() {
 }
 
 void set_batch_lanes(int lanes) { g_lanes_override.store(std::max(0, lanes)); }
+
+static std::atomic<int> g_debug_flags{0};
+void set_debug_flags(int flags) { g_debug_flags.store(flags); }
+int debug_flags() { return g_debug_flags.load(); }
 
 }  // namespace dq

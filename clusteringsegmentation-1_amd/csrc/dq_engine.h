@@ -149,11 +149,6 @@ class Engine {
   uint32_t* scratch_words(size_t n);
 
   hipStream_t stream() const { return stream_; }
-  // An event the batch call records on the caller's stream for its lanes.
-  hipEvent_t ready_event() {
-    if (!ready_ev_) DQ_HIP(hipEventCreateWithFlags(&ready_ev_, hipEventDisableTiming));
-    return ready_ev_;
-  }
 
   // Row-tile sharding across processes (one GPU each): an RCCL communicator
   // over which every pass's node totals are allreduced.
@@ -286,6 +281,8 @@ class Engine {
   void collect_timing();
 
   int device_ = 0;
+  int debug_ = 0;                     // debug_flags() of the current run
+  void debug_host_delay() const;
   uint32_t* d_bgr_pack_ = nullptr;   // BGR24 frames the map cannot read directly, packed
   size_t cap_bgr_pack_ = 0;
   bool fixed_point_ = true;
@@ -364,7 +361,6 @@ class Engine {
   uint32_t* d_mapstage_ = nullptr;
   uint32_t* d_mapstage_view_ = nullptr;   // device view of h_mapstage_ (host-coherent)
   hipEvent_t map_ev_ = nullptr;           // the last upload of h_mapstage_
-  hipEvent_t ready_ev_ = nullptr;         // ready_event()
   bool map_pending_ = false;
   size_t cap_mapstage_ = 0;
   void ensure_map_stage(size_t nmaps);
@@ -397,10 +393,14 @@ class Engine {
 // every call and holds the diagnostics; a batch of frames is split over
 // batch_lanes() lanes, each an engine with its own stream driven by its own
 // host thread, so one group's kernels fill the GPU while another group's host
-// replays its round (DQ_HIP_LANES, default 2: measured best for 8 4K frames, interleaved A/B).
+// replays its round (DQ_HIP_LANES, default 3: measured best for 8 4K frames, interleaved A/B).
 constexpr int kMaxLanes = 8;
 Engine& engine_for(int device, int lane = 0);
 int batch_lanes();
 void set_batch_lanes(int lanes);   // 0: the default
+// Test-only interleaving knobs (kDebug* in dq_kernels.h; 0 in production),
+// read by every engine when a run starts.
+void set_debug_flags(int flags);
+int debug_flags();
 
 }  // namespace dq

@@ -44,7 +44,7 @@ struct RoundArgs {
   // sharded rounds (a frame split into row ranges, one record per shard):
   uint64_t* tot;            // per logical node: 8 u64 totals (nodesum, then allreduce)
   int32_t nshard;           // records per logical node (record r = node * nshard + shard)
-  int32_t pad;
+  int32_t debug;            // kDebug* flags (tests only: forced interleavings, 0 in production)
   uint32_t* rdone;          // per (2-means iteration, record): kpass workgroups finished
   NodeResult* dres;         // device copy of the final results (read by the next round's plan)
   const uint32_t* counts;   // planned rounds: [tiles, part tiles, aborted] written by
@@ -77,8 +77,25 @@ struct PlanArgs {
   const uint8_t* p0;        // the two working buffers (a child's dst is the
   const uint8_t* p1;        //   other one of its src)
   uint64_t cap_bytes;       // bytes per working buffer
+  int32_t debug;            // kDebug* flags
+  int32_t pad;
 };
-constexpr int kPlanMaxParents = 6144;   // parents per planned round (LDS scans)
+constexpr int kPlanMaxParents = 6144;
+
+// Test-only interleaving knobs (dq_hip_set_debug): each forces a timing or
+// cache state the production path must tolerate, with identical outputs.
+//   kDebugPrewarm:   every 2-means workgroup loads its record's tile partials
+//                    and per-wave counts (into its L1 and its XCD's L2)
+//                    before storing its own, so a last arriver that skipped
+//                    the agent-scope acquire would read stale lines;
+//   kDebugUneven:    1 in 8 workgroups of every 2-means pass and partition
+//                    stalls ~10 us before publishing (uneven arrival order);
+//   kDebugHostDelay: the host sleeps 200 us between a round's status word and
+//                    reading its results, and before enqueueing a round (the
+//                    GPU runs ahead into the other parity slot);
+//   kDebugPlanStall: the plan kernel's first workgroup stalls ~20 us before
+//                    publishing the plan's counts.
+constexpr int32_t kDebugPrewarm = 1, kDebugUneven = 2, kDebugHostDelay = 4, kDebugPlanStall = 8;   // parents per planned round (LDS scans)
 void launch_plan(const PlanArgs& a, hipStream_t stream);
 // Host-built round tables: copy `bytes` from host-coherent pinned staging
 // (device view) into the round's device block on the round's stream (no
@@ -154,10 +171,7 @@ struct BlockHistArgs {
 // per 4K frame (light + rank kernel, us): 1 queue 61+21 (same-address
 // atomics), 8: 15+21, 16: 10+22, 32: 9+93, 64: 10+157 (the ranking kernel
 // degrades with many sparse queues; not understood yet).
-#ifndef DQ_BH_QUEUES
-#define DQ_BH_QUEUES 16
-#endif
-constexpr uint32_t kBhQueues = DQ_BH_QUEUES, kBhQueueStride = 32;
+constexpr uint32_t kBhQueues = 16, kBhQueueStride = 32;
 size_t block_hist_scratch_words(uint32_t block_w, uint32_t block_h);
 int launch_block_hist(const BlockHistArgs& a, int dim, hipStream_t stream);
 

@@ -75,6 +75,14 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
+// Test-only stalls (RoundArgs::debug, kDebugUneven / kDebugPlanStall): about
+// `us` microseconds of s_sleep by the calling wave.
+__device__ __forceinline__ void debug_sleep_us(int us) {
+  for (int i = 0; i < us; ++i) __builtin_amdgcn_s_sleep(40);   // (64 x 40 cycles ~ 1 us)
+}
+// 1 in 8 workgroups, by a hash of the workgroup index
+__device__ __forceinline__ bool debug_unlucky(uint32_t b) { return ((b * 2654435761u) >> 29) == 0u; }
+
 // (:561-598 / :787-810) means and weights of both halves from the new side's
 // exact integer sums.  cnt/sums are exact in double (all < 2^53).
 __device__ __forceinline__ void means_from_sums(const uint64_t t[F_NUM], double s, double tw,
@@ -510,11 +518,9 @@ __device__ bool node_update(DevNode* w, NodeResult* r, const uint64_t t[F_NUM], 
 // the sums need no per-point binning: packed lane partials -> wave sums ->
 // LDS -> one 32-B partial per tile.
 // Waves per SIMD the pass kernels are compiled for (VGPR budget 512 / n).
-#ifndef DQ_PASS_WAVES
-#define DQ_PASS_WAVES 4
-#endif
+constexpr int kPassWaves = 4;
 template <int KIND>
-__global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void pass_kernel(RoundArgs a) {
+__global__ __launch_bounds__(kBlock, kPassWaves) void pass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const DevNode& nd = a.nodes[t.node];
   if ((KIND == PASS_KMEANS || KIND == PASS_KLAST) && nd.done_it != 0) return;   // final
@@ -729,9 +735,6 @@ __device__ __forceinline__ void block_cursors(Tile* tiles, const uint32_t* wp, i
   }
 }
 
-#ifndef DQ_RESULT_ORDERED
-#define DQ_RESULT_ORDERED 0
-#endif
 // Final results go straight to host-coherent memory: relaxed system-scope
 // 8-B stores, one per lane (no L2 write-back); the device copy (ddst, may be
 // null) is what the next round's plan reads.  The last word (len_local,
@@ -750,19 +753,6 @@ __device__ __forceinline__ void store_result(NodeResult* dst, NodeResult* ddst, 
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint64_t v = lane < (uint32_t)kWords ? reinterpret_cast<const uint64_t*>(&r)[lane] : 0ull;
-#if DQ_RESULT_ORDERED
-  if (lane < (uint32_t)kWords - 1) {
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + lane, v, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    if (ddst) reinterpret_cast<uint64_t*>(ddst)[lane] = v;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == (uint32_t)kWords - 1) {
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(dst) + lane, v, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    if (ddst) reinterpret_cast<uint64_t*>(ddst)[lane] = v;
-  }
-#else
   // (all words in one store instruction: the host reads a round's results
   // only after its status word, which the last arriver publishes after every
   // record's vmcnt(0) -- the tag check stays as a consistency check; the
@@ -772,7 +762,6 @@ __device__ __forceinline__ void store_result(NodeResult* dst, NodeResult* ddst, 
                        __HIP_MEMORY_SCOPE_SYSTEM);
     if (ddst) reinterpret_cast<uint64_t*>(ddst)[lane] = v;
   }
-#endif
 }
 
 // One record's arrival on a launch's counters (lane 0): 64-bit words (low =
@@ -892,6 +881,7 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
   }
   if (wave_id() != 0) return;
   if (kMeans || KIND == PASS_SPLIT) {   // (split: proven fixed points, status slot max_iters)
+    if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x)) debug_sleep_us(10);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -947,7 +937,7 @@ __device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int rec
 }
 
 template <int KIND>
-__global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void kpass_kernel(RoundArgs a) {
+__global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const int rec = t.node;
   const DevNode& nd = a.nodes[rec];
@@ -970,6 +960,17 @@ __global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void kpass_kernel(RoundArgs 
 #pragma unroll
   for (int k = 0; k < F_NUM; ++k) f[k] = wave_sum_u32(f[k]);
   const uint32_t vsum = wave_sum_u32(s.vcnt);
+  if (a.debug & kDebugPrewarm) {   // (tests) the record's hand-off lines into this CU's caches
+    const uint32_t* pp = reinterpret_cast<const uint32_t*>(a.parts);
+    uint32_t x = 0;
+    for (int i = nd.tile_begin + (int)lane_id(); i < nd.tile_end; i += 64) {
+      for (int k = 0; k < 8; ++k) x += pp[(size_t)i * 8 + k];
+      for (int k = 0; k < 8; ++k) x += __hip_atomic_load(pp + (size_t)i * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int ww = 0; ww < kTileWaves; ++ww) x += a.wparts[(size_t)i * kTileWaves + ww];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::"v"(x) : "memory");
+  }
+  if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x)) debug_sleep_us(10);
   if (lane_id() == 0) {
     __hip_atomic_store(a.wparts + blockIdx.x * kTileWaves + wave_id(),
                        (vsum - f[F_CNT]) | (f[F_CNT] << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -983,16 +984,29 @@ __global__ __launch_bounds__(kBlock, DQ_PASS_WAVES) void kpass_kernel(RoundArgs 
     for (int w = 0; w < kBlock / 64; ++w) x += red[w][threadIdx.x];
     __hip_atomic_store(a.parts[blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // every wave's partial / count stores complete before the workgroup counts
-  // itself in: __syncthreads() alone emits no vmcnt(0) here, and a store
-  // still in flight when the last arriver reads the partials gave it the
-  // previous iteration's value (run-to-run differences with many 2-means
-  // iterations)
+  // Hand-off to the record's last arriver (the gfx950 agent-
+  // scope protocol of MI355X_MICROARCH.md "inter-workgroup visibility"):
+  //   producer (every workgroup): the partial and the per-wave counts are
+  //     write-through (sc1) stores; EVERY wave drains them (asm vmcnt(0):
+  //     __syncthreads() alone emits no wait) before the workgroup's one
+  //     arrival (lane 0, agent-scope atomic, behind the barrier);
+  //   consumer (the workgroup whose add returns count - 1): an agent-scope
+  //     ACQUIRE (buffer_inv sc1) before any load of the handed-off lines, so
+  //     no copy this CU's L1 or its XCD's L2 holds from before the stores
+  //     is read (kDebugPrewarm plants exactly such copies; tests/
+  //     test_gpu_handoff.py).  Only the acquiring wave reads.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    slast = __hip_atomic_fetch_add(a.rdone + (size_t)a.it * a.nn + rec, 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(nd.tile_end - nd.tile_begin) - 1;
+  if (threadIdx.x == 0) {
+    const bool last = __hip_atomic_fetch_add(a.rdone + (size_t)a.it * a.nn + rec, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) ==
+                      (uint32_t)(nd.tile_end - nd.tile_begin) - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    slast = last;
+  }
   __syncthreads();
   if (slast && wave_id() == 0) kmeans_epilogue_wave<KIND>(a, rec, &sres);
 }
@@ -1110,36 +1124,6 @@ __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
 
 // Occupancy of partsplit: 4 waves per SIMD (LDS staging 25 KB per
 // workgroup, <= 128 VGPRs).
-#ifndef DQ_PS_WAVES
-#define DQ_PS_WAVES 4
-#endif
-// the next sweep's loads issued before this sweep's work (1) or after it (0;
-// measured 104 vs 108 us per 8 x 4K launch)
-#ifndef DQ_PS_PREFETCH
-#define DQ_PS_PREFETCH 1
-#endif
-// Cache policy of partsplit's streams (a parent's points are read once, its
-// children's written once): nontemporal loads, store cache-policy bits
-#ifndef DQ_PS_NTLOAD
-#define DQ_PS_NTLOAD 0
-#endif
-// timing experiments only (wrong results): partsplit stores dropped
-#ifndef DQ_PS_ABLATE_STORE
-#define DQ_PS_ABLATE_STORE 0
-#endif
-#ifndef DQ_PS_ABLATE_STAGE   // staged bytes all to 16 LDS bytes (no bank spread)
-#define DQ_PS_ABLATE_STAGE 0
-#endif
-#ifndef DQ_PS_ABLATE_PART   // no staging / flush / stores at all
-#define DQ_PS_ABLATE_PART 0
-#endif
-#ifndef DQ_PS_ABLATE_SUMS
-#define DQ_PS_ABLATE_SUMS 0
-#endif
-#ifndef DQ_PS_STORE_AUX
-#define DQ_PS_STORE_AUX 0
-#endif
-
 // partsplit works on byte masks: word j of a SweepMask holds 0x01 in byte e
 // iff slot 4j + e is in the set -- the 0/1 byte weights v_dot4 sums with,
 // and what the SWAR cut comparison produces (partsplit was VALU-bound with
@@ -1254,19 +1238,19 @@ __device__ __forceinline__ void fetch_sweep_rs(const PlaneRsrc& s, uint32_t vs, 
     const int o = (int)(i < end ? 3u * i : kOOB);
 #pragma unroll
     for (int c = 0; c < 3; ++c)
-      x.v[c] = __builtin_amdgcn_raw_buffer_load_b128(s.r, o + 16 * c, 0, DQ_PS_NTLOAD ? 2 : 0);
+      x.v[c] = __builtin_amdgcn_raw_buffer_load_b128(s.r, o + 16 * c, 0, 0);
   } else if (PLANAR) {
     const uint32_t i = vs + 16u * lane_id();
     const int o = (int)(i < end ? i : kOOB);
-    x.v[0] = __builtin_amdgcn_raw_buffer_load_b128(s.r, o, 0, DQ_PS_NTLOAD ? 2 : 0);
-    x.v[1] = __builtin_amdgcn_raw_buffer_load_b128(s.g, o, 0, DQ_PS_NTLOAD ? 2 : 0);
-    x.v[2] = __builtin_amdgcn_raw_buffer_load_b128(s.b, o, 0, DQ_PS_NTLOAD ? 2 : 0);
+    x.v[0] = __builtin_amdgcn_raw_buffer_load_b128(s.r, o, 0, 0);
+    x.v[1] = __builtin_amdgcn_raw_buffer_load_b128(s.g, o, 0, 0);
+    x.v[2] = __builtin_amdgcn_raw_buffer_load_b128(s.b, o, 0, 0);
   } else {
 #pragma unroll
     for (int j = 0; j < kVecPerThread; ++j) {
       const uint32_t i = vs + 4u * (j * 64 + lane_id());
       x.v[j] = __builtin_amdgcn_raw_buffer_load_b128(s.r, (int)(i < end ? 4u * i : kOOB), 0,
-                                                     DQ_PS_NTLOAD ? 2 : 0);
+                                                     0);
     }
   }
 }
@@ -1293,7 +1277,6 @@ __device__ __forceinline__ void stage_sweep(const Sweep& w, const SweepMask& om,
   const uint32_t exs = ex - g.cbo, eys = ey - g.cbn;
   auto put = [&](int s, uint32_t lp) {
     const int j = s >> 2, sh = 8 * (s & 3);
-    if (DQ_PS_ABLATE_STAGE) lp &= 15u;
     st[lp] = (uint8_t)(w.r[j] >> sh);
     st[kStagePlane + lp] = (uint8_t)(w.g[j] >> sh);
     st[2 * kStagePlane + lp] = (uint8_t)(w.b[j] >> sh);
@@ -1336,10 +1319,10 @@ __device__ __forceinline__ void stage_bytes(const uint8_t* st, const PlaneRsrc& 
   const uint32_t pos = (run ? g.cbn : g.cbo) + i;
   const uint32_t lo = run ? g.lon : g.loo, hi = run ? hi_n : hi_o;
   const uint32_t lp = run * kStageRun + i;   // (lanes 32-63 read a staged byte, store nothing)
-  const uint32_t o = (l < 32u && pos >= lo && pos < hi && !DQ_PS_ABLATE_STORE) ? pos : kOOB;
-  __builtin_amdgcn_raw_buffer_store_b8(st[lp], d.r, (int)o, 0, DQ_PS_STORE_AUX);
-  __builtin_amdgcn_raw_buffer_store_b8(st[kStagePlane + lp], d.g, (int)o, 0, DQ_PS_STORE_AUX);
-  __builtin_amdgcn_raw_buffer_store_b8(st[2 * kStagePlane + lp], d.b, (int)o, 0, DQ_PS_STORE_AUX);
+  const uint32_t o = (l < 32u && pos >= lo && pos < hi) ? pos : kOOB;
+  __builtin_amdgcn_raw_buffer_store_b8(st[lp], d.r, (int)o, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(st[kStagePlane + lp], d.g, (int)o, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(st[2 * kStagePlane + lp], d.b, (int)o, 0, 0);
 }
 
 // Chunk q of a flush (q < nfo: the old run's, else the new run's), stored by
@@ -1356,13 +1339,13 @@ __device__ __forceinline__ void flush_chunk(const uint8_t* st, const PlaneRsrc& 
   const uint32_t pos = (run ? g.cbn : g.cbo) + k16;
   const bool ok = q < nf && pos >= (run ? g.lon : g.loo);
   const uint32_t lp = ok ? (run ? kStageRun : 0u) + k16 : 0u;
-  const uint32_t o = (ok && !DQ_PS_ABLATE_STORE) ? pos : kOOB;
+  const uint32_t o = (ok) ? pos : kOOB;
   const u32x4 vr = *reinterpret_cast<const u32x4*>(st + lp);
   const u32x4 vg = *reinterpret_cast<const u32x4*>(st + kStagePlane + lp);
   const u32x4 vb = *reinterpret_cast<const u32x4*>(st + 2 * kStagePlane + lp);
-  __builtin_amdgcn_raw_buffer_store_b128(vr, d.r, (int)o, 0, DQ_PS_STORE_AUX);
-  __builtin_amdgcn_raw_buffer_store_b128(vg, d.g, (int)o, 0, DQ_PS_STORE_AUX);
-  __builtin_amdgcn_raw_buffer_store_b128(vb, d.b, (int)o, 0, DQ_PS_STORE_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(vr, d.r, (int)o, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(vg, d.g, (int)o, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(vb, d.b, (int)o, 0, 0);
 }
 
 // After a sweep: the completed chunks of both runs (at most 65: <= 15 + 15
@@ -1405,145 +1388,7 @@ __device__ __forceinline__ void stage_flush(uint8_t* st, const PlaneRsrc& d, Sta
   wave_lds_sync();
 }
 
-// ---------------------------------------------------------------------------
-// Word staging (DQ_PS_STAGE4, default): one 32-bit word per point in the
-// caller's packed 0x00RRGGBB form instead of one byte per point and plane --
-// one ds_write_b32 per point where the byte form needs three ds_write_b8
-// (LDS instruction issue bounded the byte form: its staging and flush cost
-// as much time as the loads); the flush reads a 16-point chunk with four
-// ds_read_b128 and splits it into the three 16-B plane vectors with
-// unpack_sweep's v_perm form.  Region-relative index i lives at word
-// s4_word(i) = i ^ ((i >> 4) & 12): the 16-B blocks of chunk k are rotated by
-// XOR with (k >> 2) & 3, which makes the flush's ds_read_b128 (one chunk per
-// lane, 64-B stride) conflict-free while a slot's ranked writes (consecutive
-// indices) stay conflict-free inside each chunk.  Index semantics as in the
-// byte form, but both runs' indices are region-relative.
-#ifndef DQ_PS_STAGE4
-#define DQ_PS_STAGE4 0
-#endif
-constexpr uint32_t kS4Run = 1056;                // words per (wave, run) region: 15 + 1024 + slack
-constexpr uint32_t kS4Wave = 2 * kS4Run * 4;     // bytes per wave (old region, new region)
-
-__device__ __forceinline__ uint32_t s4_word(uint32_t i) { return i ^ ((i >> 4) & 12u); }
-
-// slot s of the sweep as a packed word (B in byte 0, G in 1, R in 2)
-__device__ __forceinline__ uint32_t slot_word(const Sweep& w, int s) {
-  const int j = s >> 2, e = s & 3;
-  const uint32_t gb = __builtin_amdgcn_perm(w.g[j], w.b[j], e < 2 ? 0x05010400u : 0x07030602u);   // B G B G
-  return __builtin_amdgcn_perm(w.r[j], gb, (e & 1) ? ((e < 2) ? 0x0C050302u : 0x0C070302u)
-                                                   : ((e < 2) ? 0x0C040100u : 0x0C060100u));
-}
-
-struct Stage4 {
-  uint32_t cbo, cbn, po, pn, loo, lon;   // pn: new-region-relative (the byte form adds kStageRun)
-};
-
-template <bool PRE>
-__device__ __forceinline__ void stage4_sweep(const Sweep& w, const SweepMask& om, const SweepMask& nm, bool full,
-                                             uint32_t* st, Stage4& g, uint32_t l, const SweepMask& xm,
-                                             const SweepMask& ym, uint32_t ex, uint32_t ey, uint32_t& ax,
-                                             uint32_t& ay) {
-  constexpr int kSlots = kVecPerThread * 4;
-  const uint32_t exs = ex - g.cbo, eys = ey - g.cbn;
-  auto put = [&](int s, bool o, uint32_t i) {
-    st[(o ? 0u : kS4Run) + s4_word(i)] = slot_word(w, s);
-    if (PRE) {
-      ax += (uint32_t)(slot_in(xm, s) && i < exs);
-      ay += (uint32_t)(slot_in(ym, s) && i < eys);
-    }
-  };
-  if (full) {   // (wave-uniform)
-    const uint32_t po0 = g.po;
-    uint32_t t = g.pn + l;
-#pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
-      const bool o = slot_in(om, s);
-      const uint64_t bo = __ballot(o);
-      const uint32_t ro = mbcnt64(bo);
-      put(s, o, o ? g.po + ro : t - ro);
-      const uint32_t co = (uint32_t)__popcll(bo);
-      g.po += co;
-      t += 64u - co;
-    }
-    g.pn += (uint32_t)kWaveSweep - (g.po - po0);
-  } else {
-#pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
-      const bool o = slot_in(om, s), n = slot_in(nm, s);
-      const uint64_t bo = __ballot(o), bn = __ballot(n);
-      if (o || n) put(s, o, o ? g.po + mbcnt64(bo) : g.pn + mbcnt64(bn));
-      g.po += (uint32_t)__popcll(bo);
-      g.pn += (uint32_t)__popcll(bn);
-    }
-  }
-}
-
-// Lanes 0-15 / 16-31 write the staged points i of the old / new run's first
-// chunk whose child positions lie in [max(cb, lo), hi), byte by byte.
-__device__ __forceinline__ void stage4_bytes(const uint32_t* st, const PlaneRsrc& d, const Stage4& g,
-                                             uint32_t hi_o, uint32_t hi_n, uint32_t l) {
-  const uint32_t run = (l >> 4) & 1u, i = l & 15u;
-  const uint32_t pos = (run ? g.cbn : g.cbo) + i;
-  const uint32_t lo = run ? g.lon : g.loo, hi = run ? hi_n : hi_o;
-  const uint32_t v = st[run * kS4Run + s4_word(i)];   // (lanes 32-63 read one, store nothing)
-  const uint32_t o = (l < 32u && pos >= lo && pos < hi && !DQ_PS_ABLATE_STORE) ? pos : kOOB;
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> 16), d.r, (int)o, 0, DQ_PS_STORE_AUX);
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> 8), d.g, (int)o, 0, DQ_PS_STORE_AUX);
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, d.b, (int)o, 0, DQ_PS_STORE_AUX);
-}
-
-// Chunk q of a flush, every lane storing (kOOB: no chunk / a first chunk
-// that stage4_bytes writes), as flush_chunk.
-__device__ __forceinline__ void flush4_chunk(const uint32_t* st, const PlaneRsrc& d, const Stage4& g,
-                                             uint32_t q, uint32_t nfo, uint32_t nf) {
-  const bool run = q >= nfo;
-  const uint32_t k = run ? q - nfo : q;
-  const uint32_t pos = (run ? g.cbn : g.cbo) + 16u * k;
-  const bool ok = q < nf && pos >= (run ? g.lon : g.loo);
-  const uint32_t kk = ok ? k : 0u, key = (kk >> 2) & 3u;
-  const uint32_t* c = st + (run ? kS4Run : 0u) + 16u * kk;
-  RawSweep x;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) x.v[b] = *reinterpret_cast<const u32x4*>(c + 4u * ((uint32_t)b ^ key));
-  Sweep w;
-  unpack_sweep<false>(x, w);
-  const uint32_t o = (ok && !DQ_PS_ABLATE_STORE) ? pos : kOOB;
-  __builtin_amdgcn_raw_buffer_store_b128((u32x4){w.r[0], w.r[1], w.r[2], w.r[3]}, d.r, (int)o, 0, DQ_PS_STORE_AUX);
-  __builtin_amdgcn_raw_buffer_store_b128((u32x4){w.g[0], w.g[1], w.g[2], w.g[3]}, d.g, (int)o, 0, DQ_PS_STORE_AUX);
-  __builtin_amdgcn_raw_buffer_store_b128((u32x4){w.b[0], w.b[1], w.b[2], w.b[3]}, d.b, (int)o, 0, DQ_PS_STORE_AUX);
-}
-
-__device__ __forceinline__ void stage4_flush(uint32_t* st, const PlaneRsrc& d, Stage4& g, uint32_t l) {
-  wave_lds_sync();
-  const uint32_t nfo = g.po >> 4, nfn = g.pn >> 4;
-  const uint32_t nf = nfo + nfn;
-  flush4_chunk(st, d, g, l, nfo, nf);
-  if (nf > 64u) flush4_chunk(st, d, g, 64u + l, nfo, nf);   // (wave-uniform, rare)
-  const uint32_t ho = (nfo > 0u && g.cbo < g.loo) ? g.cbo + 16u : 0u;
-  const uint32_t hn = (nfn > 0u && g.cbn < g.lon) ? g.cbn + 16u : 0u;
-  if (ho | hn) stage4_bytes(st, d, g, ho, hn, l);
-  if (nfo | nfn) {   // the partial chunks to the front
-    const uint32_t run = (l >> 4) & 1u, i = l & 15u;
-    const uint32_t nfr = run ? nfn : nfo;
-    const bool mv = l < 32u && nfr > 0u;
-    uint32_t v = 0;
-    wave_lds_sync();
-    if (mv) v = st[run * kS4Run + s4_word(16u * nfr + i)];
-    wave_lds_sync();
-    if (mv) st[run * kS4Run + s4_word(i)] = v;
-    g.cbo += 16u * nfo;
-    g.po -= 16u * nfo;
-    g.cbn += 16u * nfn;
-    g.pn -= 16u * nfn;
-  }
-  wave_lds_sync();
-}
-
-#if DQ_PS_STAGE4
-typedef uint32_t StageMem;
-#else
 typedef uint8_t StageMem;
-#endif
 
 // The kernel's loop for one source format of the parent.
 // (records and tiles through global-address-space views: generic pointers
@@ -1586,13 +1431,8 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   ChunkAcc cx, cy;
   chunk_init(cx, nodes, wparts, pt.child[0], oc0);
   chunk_init(cy, nodes, wparts, pt.child[1], nc0);
-#if DQ_PS_STAGE4
-  Stage4 g;
-  constexpr uint32_t kPnOff = 0;   // (new-region-relative indices)
-#else
   Stage g;
   constexpr uint32_t kPnOff = kStageRun;
-#endif
   g.cbo = oc0 & ~15u;
   g.po = oc0 & 15u;
   g.loo = oc0;
@@ -1627,20 +1467,12 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   uint32_t vs = start & ~15u;
   bool full = vs >= start && vs + kWaveSweep <= end;
   fetch_sweep_rs<PLANAR, BGR>(s, vs, end, x);
-#if DQ_PS_PREFETCH == 2
-  RawSweep xnn;
-  fetch_sweep_rs<PLANAR, BGR>(s, vs + kWaveSweep, end, xn);
-#endif
   while (vs < end) {
     const uint32_t nvs = vs + kWaveSweep;
     const bool nfull = nvs + kWaveSweep <= end;
-#if DQ_PS_PREFETCH == 2
-    fetch_sweep_rs<PLANAR, BGR>(s, nvs + kWaveSweep, end, xnn);
-#elif DQ_PS_PREFETCH
     // the next sweep's loads in flight during this one (past the end: kOOB,
     // no memory access -- a fixed load count per sweep)
     fetch_sweep_rs<PLANAR, BGR>(s, nvs, end, xn);
-#endif
     Sweep sw;
     unpack_sweep<PLANAR, BGR>(x, sw);
     // the parent's final decision: its cut when proven, else its last 2-means plane
@@ -1670,10 +1502,8 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
       xm.m[j] &= om.m[j];   // new for the old child
       ym.m[j] &= nm.m[j];   // new for the new child
     }
-    if (!DQ_PS_ABLATE_SUMS) {
-      add_sums_bytes(sw, xm, so);
-      add_sums_bytes(sw, ym, sn);
-    }
+    add_sums_bytes(sw, xm, so);
+    add_sums_bytes(sw, ym, sn);
     // this wave's points.  A sweep writes at most kWaveSweep points to each
     // child: when neither child's current chunk can end inside it (fast
     // sweep), only the lanes' new counts are kept; otherwise every slot's run
@@ -1681,65 +1511,33 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     const uint32_t oc = g.cbo + g.po, nc = g.cbn + g.pn - kPnOff;
     const bool fast = oc + kWaveSweep <= cx.end && nc + kWaveSweep <= cy.end;
     uint32_t ax = 0, ay = 0;
-    if (DQ_PS_ABLATE_PART) {   // (timing experiment: no partition at all)
-      so.cnt += mask_count(om);
-      sn.cnt += mask_count(nm);
-      x = xn;
-      vs = nvs;
-      full = nfull;
-      continue;
-    }
-#if DQ_PS_STAGE4
-    if (fast) stage4_sweep<false>(sw, om, nm, full, st, g, l, xm, ym, 0u, 0u, ax, ay);
-    else stage4_sweep<true>(sw, om, nm, full, st, g, l, xm, ym, cx.end, cy.end, ax, ay);
-#else
     if (fast) stage_sweep<false>(sw, om, nm, full, st, g, l, xm, ym, 0u, 0u, ax, ay);
     else stage_sweep<true>(sw, om, nm, full, st, g, l, xm, ym, cx.end, cy.end, ax, ay);
-#endif
     chunk_sweep(cx, oc, g.cbo + g.po, mask_count(xm), ax);
     chunk_sweep(cy, nc, g.cbn + g.pn - kPnOff, mask_count(ym), ay);
-#if DQ_PS_STAGE4
-    stage4_flush(st, d, g, l);
-#else
     stage_flush(st, d, g, l);
-#endif
-#if DQ_PS_PREFETCH == 2
     x = xn;
-    xn = xnn;
-#elif DQ_PS_PREFETCH
-    x = xn;
-#else
-    if (nvs < end) fetch_sweep_rs<PLANAR, BGR>(s, nvs, end, x);
-#endif
     vs = nvs;
     full = nfull;
   }
-#if DQ_PS_STAGE4
-  stage4_bytes(st, d, g, g.cbo + g.po, g.cbn + g.pn, l);   // the runs' last partial chunks
-#else
   stage_bytes(st, d, g, g.cbo + g.po, g.cbn + g.pn - kStageRun, l);   // the runs' last partial chunks
-#endif
   chunk_finish(cx);
   chunk_finish(cy);
 }
 
-__global__ __launch_bounds__(kBlock, DQ_PS_WAVES) void partsplit_kernel(RoundArgs a) {
+__global__ __launch_bounds__(kBlock, 4) void partsplit_kernel(RoundArgs a) {
   if (a.counts && blockIdx.x >= a.counts[1]) return;   // planned round: grid is an upper bound
   const PartTile pt = a.ptiles[blockIdx.x];
   g_cnode& nd = *(g_cnode*)pt.parent;
   g_ctile* tp = (g_ctile*)pt.tile;
   SplitSums so, sn;
-#if DQ_PS_STAGE4
-  __shared__ __attribute__((aligned(16))) uint32_t stage[kTileWaves * kS4Wave / 4];
-  StageMem* st = stage + wave_id() * (kS4Wave / 4);
-#else
   __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
   StageMem* st = stage + wave_id() * kStageWave;
-#endif
   if (nd.planar == SRC_PLANAR) partsplit_run<true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
   else if (nd.planar == SRC_BGR24) partsplit_run<true, true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
   else partsplit_run<false>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
 
+  if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x)) debug_sleep_us(10);
   __shared__ uint32_t red[kTileWaves][16];
   const uint32_t w = wave_id(), l = lane_id();
   uint32_t f[16] = {so.cnt, so.sr, so.sg, so.sb, so.qr, so.qg, so.qb, 0u,
@@ -1932,6 +1730,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
   __syncthreads();
   const bool overflow = run_t > a.tiles_cap || run_p > a.ptiles_cap;
   if (blockIdx.x == 0 && tid == 0) {
+    if (a.debug & kDebugPlanStall) debug_sleep_us(20);
     const uint32_t ab = s_abort ? 1u : (overflow ? 2u : 0u);
     const uint32_t c[3] = {ab ? 0u : run_t, ab ? 0u : run_p, ab};
     for (int k = 0; k < 3; ++k) {
@@ -2345,10 +2144,6 @@ __global__ __launch_bounds__(kBlock) void map_kernel(const MapTask* __restrict__
 //     a per-lane loop.
 // Same keys and the same answer as map_kernel.
 constexpr int kMapQ = 64;
-// The map's output stores: nontemporal (streamed past the caches) or default
-#ifndef DQ_MAP_NT
-#define DQ_MAP_NT 1
-#endif
 // 12 BGR24 bytes (3 words, little-endian) -> 4 packed 0x00RRGGBB words.
 __device__ __forceinline__ u32x4 bgr12_to_px4(uint32_t w0, uint32_t w1, uint32_t w2) {
   u32x4 o;
@@ -2553,13 +2348,10 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
       wave_lds_sync();
     }
     if (have) {
-#if DQ_MAP_NT
+      // (nontemporal: streamed past the caches -- the next call's root pass
+      // found its frame in L2 / MALL instead of the map's output)
       __builtin_nontemporal_store((u32x4){res[0], res[1], res[2], res[3]}, out4 + 2 * g);
       __builtin_nontemporal_store((u32x4){res[4], res[5], res[6], res[7]}, out4 + 2 * g + 1);
-#else
-      out4[2 * g] = (u32x4){res[0], res[1], res[2], res[3]};
-      out4[2 * g + 1] = (u32x4){res[4], res[5], res[6], res[7]};
-#endif
     }
   }
   // tail (n % kMapPx points): the task's first workgroup, whole palette
@@ -2897,16 +2689,10 @@ int launch_block_hist(const BlockHistArgs& a0, int dim, hipStream_t stream) {
 // one lane per 4 pixels of a row, 12 B read as three dwords, 16 B written.
 // HBM-bound: 7 B per pixel.  Rows are blockIdx.y (+ gridDim.y strides).
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-#ifndef DQ_BGR_NT
-#define DQ_BGR_NT 1       // nontemporal (streaming) frame accesses: pack 12.8 -> 10.9 us per 4K frame
-#endif
-#ifndef DQ_BGR_NTU
-#define DQ_BGR_NTU 0      // nontemporal BGR stores in unpack
-#endif
-#ifndef DQ_BGR_ROWCAP
-#define DQ_BGR_ROWCAP 65535u   // grid rows; a workgroup strides over the rest (a cap
-                               // of 270 or 540 rows measured slower)
-#endif
+// Frame reads and packed writes are nontemporal (streaming: pack 12.8 ->
+// 10.9 us per 4K frame); unpack's BGR stores are plain.
+constexpr uint32_t kBgrRowCap = 65535u;   // grid rows; a workgroup strides over the rest (a cap
+                                          // of 270 or 540 rows measured slower)
 
 
 __device__ __forceinline__ void px4_to_bgr12(u32x4 p, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
@@ -2924,18 +2710,12 @@ __global__ __launch_bounds__(256) void bgr24_pack_kernel(const uint8_t* __restri
     const uint8_t* row = bgr + (size_t)y * stride;
     if (FAST) {
       if (4u * i >= width) return;
-#if DQ_BGR_NT
       const __attribute__((address_space(1))) uint32_t* r =
           (const __attribute__((address_space(1))) uint32_t*)(row + 12u * i);
       const u32x3 w = {__builtin_nontemporal_load(r), __builtin_nontemporal_load(r + 1),
                        __builtin_nontemporal_load(r + 2)};
       __builtin_nontemporal_store(bgr12_to_px4(w.x, w.y, w.z),
                                   (__attribute__((address_space(1))) u32x4*)(out + (size_t)y * width + 4u * i));
-#else
-      const u32x3 w = *(const __attribute__((address_space(1))) u32x3*)(row + 12u * i);
-      *(__attribute__((address_space(1))) u32x4*)(out + (size_t)y * width + 4u * i) =
-          bgr12_to_px4(w.x, w.y, w.z);
-#endif
     } else {
       if (i >= width) return;
       const uint8_t* q = row + 3u * i;
@@ -2953,20 +2733,12 @@ __global__ __launch_bounds__(256) void bgr24_unpack_kernel(const uint32_t* __res
     uint8_t* row = bgr + (size_t)y * stride;
     if (FAST) {
       if (4u * i >= width) return;
-#if DQ_BGR_NT
       const u32x4 p = __builtin_nontemporal_load(
           (const __attribute__((address_space(1))) u32x4*)(in + (size_t)y * width + 4u * i));
-#else
-      const u32x4 p = *(const __attribute__((address_space(1))) u32x4*)(in + (size_t)y * width + 4u * i);
-#endif
       uint32_t w0, w1, w2;
       px4_to_bgr12(p, w0, w1, w2);
       const u32x3 w = {w0, w1, w2};
-#if DQ_BGR_NTU
-      __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x3*)(row + 12u * i));
-#else
       *(__attribute__((address_space(1))) u32x3*)(row + 12u * i) = w;
-#endif
     } else {
       if (i >= width) return;
       const uint32_t p = in[(size_t)y * width + i];
@@ -2999,7 +2771,7 @@ static bool bgr24_fast(const void* bgr, uint32_t width, uint32_t stride, const v
 
 static dim3 bgr24_grid(uint32_t width, uint32_t height, bool fast) {
   const uint32_t per_row = fast ? width / 4u : width;
-  return dim3((per_row + 255u) / 256u, height < DQ_BGR_ROWCAP ? height : DQ_BGR_ROWCAP);
+  return dim3((per_row + 255u) / 256u, height < kBgrRowCap ? height : kBgrRowCap);
 }
 
 void launch_bgr24_pack(const uint8_t* bgr, uint32_t width, uint32_t height, uint32_t stride,

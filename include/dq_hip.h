@@ -86,7 +86,8 @@ int dq_hip_quant_batch_dev(int device, int nframes, const uint32_t *const *d_in,
                            void *stream);
 /* dq_hip_block_hist on device pointers (in, quant, mode, ndistinct, keys,
  * counts; quant is required: the mapped frame); palette is host memory.
- * Asynchronous on `stream`. */
+ * Asynchronous on `stream`; with stream NULL the legacy default stream is
+ * ordered after the work (as for every asynchronous entry below). */
 int dq_hip_block_hist_dev(int device, const uint32_t *d_in, uint32_t width,
                           uint32_t height, const uint32_t *palette, int npal,
                           uint32_t dim, uint32_t block_w, uint32_t block_h,
@@ -136,6 +137,8 @@ int dq_hip_quant_rows_dev(int device, int nframes, const uint32_t *const *d_in,
 int dq_hip_comm_unique_id(void *id128);
 int dq_hip_comm_init(int device, int nranks, int rank, const void *id128);
 int dq_hip_comm_destroy(int device);
+/* Ranks of the engine's communicator on `device` (1: none). */
+int dq_hip_comm_size(int device);
 /* Clustering only (quant_varpart_fast, DivQuantCluster.cpp:1099-1179):
  * writes the non-empty cluster colours (cluster-index order, NOT deduped). */
 int dq_hip_cluster_dev(int device, const uint32_t *d_in, uint32_t n,
@@ -221,7 +224,7 @@ void dq_hip_set_planned_rounds(int device, int on);
 int dq_hip_last_planned_rounds(int device);
 
 /* Engine lanes a batch of frames is split over (each: own stream, own host
- * thread; DQ_HIP_LANES, default 2).  lanes = 0 restores the default. */
+ * thread; DQ_HIP_LANES, default 3).  lanes = 0 restores the default. */
 void dq_hip_set_lanes(int lanes);
 int dq_hip_get_lanes(void);
 
@@ -237,6 +240,17 @@ int dq_hip_get_stat(int device, int kind, uint64_t *launches, double *ms,
                     double *bytes);
 int dq_hip_get_stat_units(int device, int kind, double *units);
 const char *dq_hip_stat_name(int kind);
+
+/* ---- build identity and test-only knobs ----------------------------------
+ * dq_hip_build_id: FNV-1a-64 of the sources the library was built from
+ * (tools/source_id.py; a test compares it with the tree beside the .so).
+ * dq_hip_set_debug: interleaving knobs for the hand-off tests (flags of
+ * dq_kernels.h kDebug*: 1 prewarm the 2-means hand-off lines, 2 uneven
+ * workgroup stalls, 4 host delays between status and results, 8 plan-kernel
+ * stall); every lane of `device`; 0 (the default) in production.  Outputs are
+ * identical under every flag. */
+uint64_t dq_hip_build_id(void);
+void dq_hip_set_debug(int device, int flags);
 
 #ifdef __cplusplus
 }

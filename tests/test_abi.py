@@ -139,3 +139,15 @@ def test_synth_frames_and_hash_match_the_fixture_spec(pkg):
         a = pkg.synth_frame(n, f)
         assert np.array_equal(a, fx.xorshift(n, seed=fx.SEED + f))
         assert pkg.fnv1a64(a) == fx.fnv(a)
+
+
+def test_library_built_from_these_sources(pkg):
+    """The .so that travels with the tree was built from the sources beside it:
+    its embedded FNV-1a-64 of csrc/ + include/ (tools/source_id.py, compiled in
+    by the Makefile) equals the same hash of the tree.  A stale library would
+    otherwise be tested and benchmarked in place of HEAD."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("source_id", os.path.join(ROOT, "tools", "source_id.py"))
+    sid = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sid)
+    assert pkg.build_id() == sid.source_id(), "libdivquant_hip.so is stale: run make -C clusteringsegmentation-1_amd"

@@ -94,3 +94,31 @@ def test_row_ranges_partition_the_frame():
             assert all(rr[i][1] == rr[i + 1][0] for i in range(world - 1))
             sizes = [b - a for a, b in rr]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_bench_gpus_2_launches_two_ranks():
+    """`bench.py --gpus 2` with no torchrun environment starts two ranks by
+    itself (torch.distributed.run; gloo on CPU, RCCL on the GPU box), every
+    rank checks the world size, and rank 0 prints ONE line with n_gpus 2."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                             "MASTER_ADDR", "MASTER_PORT")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["dry_run"] is True
+    # the slower rank (20 ms per step) bounds the reported time
+    assert d["ms_per_step"] >= 20.0
+
+
+def test_bench_world_size_must_match_gpus():
+    """A torchrun environment whose world size differs from --gpus is refused
+    (the driver's --gpus N line can only come from N ranks)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", CUDA_VISIBLE_DEVICES="")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "--gpus 2" in p.stderr
