@@ -82,6 +82,7 @@ def lib():
         "dq_hip_last_rounds": ([c.c_int], c.c_int),
         "dq_hip_last_points_swept": ([c.c_int], c.c_uint64),
         "dq_hip_last_points_full": ([c.c_int], c.c_uint64),
+        "dq_hip_last_seq_tiles": ([c.c_int], c.c_uint64),
         "dq_hip_set_fixed_point": ([c.c_int, c.c_int], None),
         "dq_hip_set_planned_rounds": ([c.c_int, c.c_int], None),
         "dq_hip_last_planned_rounds": ([c.c_int], c.c_int),
@@ -517,6 +518,11 @@ def last_points_swept(device=0):
 def last_points_full(device=0):
     """Points the last run would have swept with all max_iters iterations."""
     return int(lib().dq_hip_last_points_full(device))
+
+
+def last_seq_tiles(device=0):
+    """Weighted path: tiles of the last run folded one summand at a time."""
+    return int(lib().dq_hip_last_seq_tiles(device))
 
 
 def set_fixed_point(on, device=0):

@@ -789,6 +789,7 @@ int dq_hip_last_rounds(int device) { return engine_for(device).last_rounds; }
 
 uint64_t dq_hip_last_points_swept(int device) { return engine_for(device).last_points_swept; }
 uint64_t dq_hip_last_points_full(int device) { return engine_for(device).last_points_full; }
+uint64_t dq_hip_last_seq_tiles(int device) { return engine_for(device).last_seq_tiles; }
 void dq_hip_set_fixed_point(int device, int on) { engine_for(device).set_fixed_point(on != 0); }
 void dq_hip_set_planned_rounds(int device, int on) {
   for (int l = 0; l < dq::kMaxLanes; ++l) engine_for(device, l).set_plan(on != 0);

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <chrono>
 #include <deque>
+#include <functional>
 #include <unordered_set>
 
 namespace dq {
@@ -264,6 +265,15 @@ void Engine::ensure_round(size_t rec_cap, size_t tiles_cap, size_t, size_t stagi
   grow_device(&d_sparts_, &cap_sparts_, std::max<size_t>(2 * tiles_cap, 2));
 }
 
+// The per-logical-node totals an allreduce round sums (8 u64 per node).
+void Engine::ensure_totals(size_t nlogical, hipStream_t stream) {
+  if (nlogical * 8 <= cap_tot_ && d_tot_) return;
+  DQ_HIP(hipStreamSynchronize(stream));
+  if (d_tot_) DQ_HIP(hipFree(d_tot_));
+  cap_tot_ = std::max<size_t>(nlogical * 8, 4096);
+  DQ_HIP(hipMalloc((void**)&d_tot_, cap_tot_ * sizeof(uint64_t)));
+}
+
 // Wait for a status word of round `seq`; returns the number of records still
 // active.  Bounded: once the stream has drained the word must be there.
 // The end of a call: an event on the stream, polled with pause (the host's
@@ -357,7 +367,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   debug_host_delay();
   const double tb0 = trace_ ? host_us() : 0.0;
   const int S = nshard_;
-  const bool sharded = S > 1 || comm_ != nullptr;
+  const int mode = tot_mode();
   rounds_.emplace_back();
   const int ri = (int)rounds_.size() - 1;
   Round& R = rounds_[ri];
@@ -382,6 +392,23 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   const int nl = (int)order.size();   // logical nodes
   const int nr = nl * S;              // records
   R.n_own = n_own;
+  // Segments this round reads that a PS_STATS round left unwritten (own
+  // split passes read a node's segment, fused partitions its parent's):
+  // written first by a PS_WRITE partition of their parents, parents first.
+  std::vector<int> mat;
+  std::function<void(int)> need = [&](int x) {
+    if (nodes_[x].points) return;
+    const int p = nodes_[x].parent;
+    need(p);
+    if (std::find(mat.begin(), mat.end(), p) == mat.end()) mat.push_back(p);
+    nodes_[nodes_[p].child_old].points = true;
+    nodes_[nodes_[p].child_new].points = true;
+  };
+  for (int a = 0; a < n_own; ++a) need(order[a]);
+  for (int p : parents) need(p);
+  size_t nmat = 0;
+  for (int p : mat)
+    for (int sh = 0; sh < S; ++sh) nmat += seg(p, sh).ntiles;
   R.nl = nl;
   R.nr = nr;
   DQ_CHECK((size_t)nr <= cap_res_, "round larger than the run's record capacity");
@@ -427,7 +454,8 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
   const size_t o_tiles = al(nr * sizeof(DevNode));
   const size_t o_pt = o_tiles + al(ntiles * sizeof(Tile));
-  const size_t o_ctr = o_pt + al(nptiles * sizeof(PartTile));
+  const size_t o_mpt = o_pt + al(nptiles * sizeof(PartTile));
+  const size_t o_ctr = o_mpt + al(nmat * sizeof(PartTile));
   // (LaunchCtr and status word max_iters: the split epilogue's); then the
   // per-(tile, wave) counts, zero from the staging memset (partsplit adds
   // the fused children's up)
@@ -436,12 +464,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   const size_t o_rd = o_wp + al(ntiles * kTileWaves * sizeof(uint32_t));
   const size_t bytes = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
   R.bytes = bytes;
-  if (sharded && (size_t)nl * 8 > cap_tot_) {
-    DQ_HIP(hipStreamSynchronize(stream));
-    if (d_tot_) DQ_HIP(hipFree(d_tot_));
-    cap_tot_ = std::max<size_t>((size_t)nl * 8, 4096);
-    DQ_HIP(hipMalloc((void**)&d_tot_, cap_tot_ * sizeof(uint64_t)));
-  }
+  if (mode == TOT_ALLREDUCE) ensure_totals(nl, stream);
   // the staging is rewritten: its previous upload must have run
   if (stage_pending_) {
     DQ_HIP(hipEventSynchronize(stage_ev_));
@@ -562,6 +585,22 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
       }
     }
   }
+  {   // the PS_WRITE partition's part tiles (no children split: nothing summed or counted)
+    PartTile* hm = reinterpret_cast<PartTile*>(h_stage_ + o_mpt);
+    int q = 0;
+    for (int p : mat)
+      for (int sh = 0; sh < S; ++sh) {
+        const Seg& ps = seg(p, sh);
+        for (int i = 0; i < ps.ntiles; ++i) {
+          PartTile& pt = hm[q++];
+          pt.tile = ps.dtiles + i;
+          pt.parent = ps.dnode;
+          pt.thr[0] = pt.thr[1] = 256;
+          pt.shift[0] = pt.shift[1] = 0;
+          pt.child[0] = pt.child[1] = -1;
+        }
+      }
+  }
   const double tb1 = trace_ ? host_us() : 0.0;
   // one upload kernel on the round's stream (no copy-engine hop)
   launch_upload(dblk, d_stage_view_, bytes, stream);
@@ -592,6 +631,16 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = nullptr;
   ra.plane = cap_px_;
+  ra.tot_mode = mode;
+  ra.ps_mode = PS_FULL;
+  if (nmat > 0) {
+    RoundArgs ma = ra;
+    ma.ptiles = reinterpret_cast<const PartTile*>(dblk + o_mpt);
+    ma.ps_mode = PS_WRITE;
+    timed_begin(stream);
+    launch_partsplit(ma, (int)nmat, stream);
+    timed_end(ST_PARTITION, 0.0, stream);
+  }
   const double bytes_all = 4.0 * (double)total;
   const int nt = (int)ntiles;
   auto pass = [&](int kind, int st, int tiles, double pbytes, double units) {
@@ -605,11 +654,11 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   auto epilogue = [&](int kind, int it) {
     ra.it = it < 0 ? 0 : it;
     timed_begin(stream);
-    if (sharded) {
+    if (mode == TOT_ALLREDUCE) {
       launch_nodesum(kind, ra, nl, stream);
-      if (comm_) allreduce_totals(nl, stream);
+      allreduce_totals(nl, stream);
     }
-    launch_epilogue(kind, ra, nr, sharded, stream);
+    launch_epilogue(kind, ra, nr, stream);
     timed_end(ST_EPILOGUE, 0.0, stream);
   };
   if (root_round) {
@@ -627,20 +676,21 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   return ri;
 }
 
-// Which records of round ri the next round may split before ri's results
-// exist (speculation): every record of a frame whose splits queued so far
-// stay below k - 1 (the greedy replay may need more); whole unsharded
-// rounds only.  Returns false when nothing is planned.
+// Which logical nodes of round ri the next round may split before ri's
+// results exist (speculation): every node of a frame whose splits queued so
+// far stay below k - 1 (the greedy replay may need more).  Returns false
+// when nothing is planned.
 bool Engine::plan_list(int ri, std::vector<int32_t>* plist) {
   const Round& R = rounds_[ri];
   plist->clear();
-  if (!plan_ || !fixed_point_ || nshard_ != 1 || comm_ != nullptr) return false;
+  if (!plan_ || !fixed_point_) return false;
   // frames of the round: speculate when the frame may need more splits
   for (int a = 0; a < R.nl; ++a) {
     const FrameState& f = frames_[nodes_[R.order[a]].frame];
     if (f.splits_queued < f.job->k - 1) plist->push_back(a);
   }
-  if (plist->empty() || 2 * plist->size() > cap_res_ || plist->size() > (size_t)kPlanMaxParents) {
+  if (plist->empty() || 2 * plist->size() * (size_t)nshard_ > cap_res_ ||
+      plist->size() > (size_t)kPlanMaxParents) {
     plist->clear();
     return false;
   }
@@ -662,25 +712,46 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   R.planned = true;
   R.prev = prev;
   R.plist = plist;
+  const int S = nshard_;
+  const int mode = tot_mode();
   const int np = (int)plist.size();
-  R.nl = R.nr = 2 * np;
+  R.nl = 2 * np;
+  R.nr = R.nl * S;
   R.n_own = 0;
   uint64_t total = 0;
   double part_bytes = 0.0;
   for (int32_t a : plist) {
     const int id = P.order[a];
-    total += seg(id, 0).len;
-    part_bytes += (point_bytes(id) + 3.0) * seg(id, 0).len;
+    for (int sh = 0; sh < S; ++sh) {
+      total += seg(id, sh).len;
+      part_bytes += (point_bytes(id) + 3.0) * seg(id, sh).len;
+    }
     Node& pn = nodes_[id];
     pn.partitioned = true;
     frames_[pn.frame].splits_queued += 2;
   }
   for (int32_t a : plist) R.parents.push_back(P.order[a]);
+  // the last round of every frame it holds: its nodes' children are leaves
+  // unless the greedy replay needs more splits than were speculated -- the
+  // partition only sums (PS_STATS); the points of parents with a child left
+  // active go out after the split epilogue (PS_LATE), the rest only if a
+  // later round reads them (enqueue_host_round, PS_WRITE)
+  R.stats_only = true;
+  for (int32_t a : plist) {
+    const FrameState& f = frames_[nodes_[P.order[a]].frame];
+    R.stats_only = R.stats_only && f.splits_queued >= f.job->k - 1;
+  }
+  if (R.stats_only) part_bytes = 0.0;
+  if (R.stats_only)
+    for (int32_t a : plist)
+      for (int sh = 0; sh < S; ++sh) part_bytes += point_bytes(P.order[a]) * seg(P.order[a], sh).len;
   R.total = R.parent_total = total;
   R.own_total = 0;
   R.tl = round_tile_len(total);
-  R.tiles_cap = std::min<size_t>(total / kSweep + 2 * (size_t)np + 1,
-                                 total / R.tl + (size_t)2 * np * node_tiles_ + 1);
+  // (a record has at most len / kSweep + 1 tiles, and at most
+  // len / tl + node_tiles + 1)
+  R.tiles_cap = std::min<size_t>(total / kSweep + (size_t)R.nr + 1,
+                                 total / R.tl + (size_t)R.nr * (node_tiles_ + 1) + 1);
   R.ptiles_cap = P.tiles_cap;
   DQ_CHECK(R.tiles_cap <= cap_parts_ && 2 * R.ptiles_cap <= cap_sparts_, "planned round above the tile capacity");
   auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
@@ -726,7 +797,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   pa.p1 = reinterpret_cast<const uint8_t*>(d_p1_);
   pa.cap_bytes = 4 * cap_px_;
   pa.debug = debug_;
-  pa.pad = 0;
+  pa.nshard = S;
   RoundArgs& ra = R.ra;
   ra.tiles = R.dt;
   ra.nodes = R.dn;
@@ -741,13 +812,16 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   ra.fixed_point = fixed_point_ ? 1 : 0;
   ra.it = max_iters;
   ra.nn = R.nr;
+  if (mode == TOT_ALLREDUCE) ensure_totals(R.nl, stream);
   ra.tot = d_tot_;
-  ra.nshard = 1;
+  ra.nshard = S;
   ra.debug = debug_;
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = R.dcounts;
   ra.plane = cap_px_;
+  ra.tot_mode = mode;
+  ra.ps_mode = R.stats_only ? PS_STATS : PS_FULL;
   timed_begin(stream);
   launch_plan(pa, stream);
   timed_end(ST_PLAN, 0.0, stream);
@@ -755,8 +829,19 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   launch_partsplit(ra, (int)R.ptiles_cap, stream);
   timed_end(ST_PARTITION, part_bytes, stream, (double)total);
   timed_begin(stream);
-  launch_epilogue(PASS_SPLIT, ra, R.nr, false, stream);
+  if (mode == TOT_ALLREDUCE) {   // (an aborted round's nodesum writes nothing; every rank
+    launch_nodesum(PASS_SPLIT, ra, R.nl, stream);   //  aborts the same rounds: same totals)
+    allreduce_totals(R.nl, stream);
+  }
+  launch_epilogue(PASS_SPLIT, ra, R.nr, stream);
   timed_end(ST_EPILOGUE, 0.0, stream);
+  if (R.stats_only) {   // the points of every parent with a child still active
+    RoundArgs la = ra;
+    la.ps_mode = PS_LATE;
+    timed_begin(stream);
+    launch_partsplit(la, (int)R.ptiles_cap, stream);
+    timed_end(ST_PARTITION, 0.0, stream);
+  }
   if (trace_) tr_build_us_ += host_us() - tb0;
   R.t_enq = trace_ ? host_us() : 0.0;
   return ri;
@@ -774,6 +859,7 @@ void Engine::assign_planned(int ri) {
     R.order.push_back(pn.child_old);
     R.order.push_back(pn.child_new);
   }
+  const int S = nshard_;
   R.tbeg.assign(R.nr, 0);
   R.tend.assign(R.nr, 0);
   int32_t t = 0;
@@ -781,11 +867,13 @@ void Engine::assign_planned(int ri) {
   for (int a = 0; a < R.nl; ++a) {
     Node& n = nodes_[R.order[a]];
     n.queued = true;
-    const uint64_t len = seg(R.order[a], 0).len;
-    const uint64_t tln = tile_len_of(len, R.tl);
-    R.tbeg[a] = t;
-    t += (int32_t)std::max<uint64_t>(1, (len + tln - 1) / tln);
-    R.tend[a] = t;
+    for (int sh = 0; sh < S; ++sh) {   // records a * S + sh, tiles in record order
+      const uint64_t len = seg(R.order[a], sh).len;
+      const uint64_t tln = tile_len_of(len, R.tl);
+      R.tbeg[a * S + sh] = t;
+      t += (int32_t)std::max<uint64_t>(1, (len + tln - 1) / tln);
+      R.tend[a * S + sh] = t;
+    }
     // the cut the plan chose (:388-403), for the children's boxes
     double maxv = n.var[0], cut = n.mean[0];
     int axis = 0;
@@ -794,36 +882,32 @@ void Engine::assign_planned(int ri) {
     n.axis = (int16_t)axis;
     n.thr = (int16_t)split_threshold(cut);
   }
-  for (int p : R.parents) npt += seg(p, 0).ntiles;
+  for (int p : R.parents)
+    for (int sh = 0; sh < S; ++sh) npt += seg(p, sh).ntiles;
   R.ntiles = (size_t)t;
   R.nptiles = npt;
 }
 
-// 2-means iteration `it` of a round: pass + epilogue, one launch when unsharded.
+// 2-means iteration `it` of a round: the pass with the node's epilogue fused
+// (kpass_kernel); across processes the pass writes this process's node
+// totals, then the allreduce and the epilogue kernel.
 void Engine::kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream) {
-  const bool sharded = nshard_ > 1 || comm_ != nullptr;
   const bool last = it == max_iters - 1;
   const int kind = last ? PASS_KLAST : PASS_KMEANS;
   const int st = last ? ST_KLAST : ST_KMEANS;
   RoundArgs& ra = R.ra;
   ra.it = it;
   const double bytes_all = 3.0 * (double)R.total;   // (exact per node: finish_round)
-  if (sharded) {
-    timed_begin(stream);
-    launch_pass(kind, ra, (int)R.ntiles, stream);
-    timed_end(st, bytes_all, stream);
-    if (timing_) R.km_events.push_back({pending_.size() - 1, it});
-    timed_begin(stream);
-    launch_nodesum(kind, ra, R.nl, stream);
-    if (comm_) allreduce_totals(R.nl, stream);
-    launch_epilogue(kind, ra, R.nr, true, stream);
-    timed_end(ST_EPILOGUE, 0.0, stream);
-    return;
-  }
   timed_begin(stream);
   launch_kpass(kind, ra, (int)R.ntiles, stream);
   timed_end(st, bytes_all, stream);
   if (timing_) R.km_events.push_back({pending_.size() - 1, it});
+  if (ra.tot_mode == TOT_ALLREDUCE) {
+    timed_begin(stream);
+    allreduce_totals(R.nl, stream);
+    launch_epilogue(kind, ra, R.nr, stream);
+    timed_end(ST_EPILOGUE, 0.0, stream);
+  }
 }
 
 // Wait for a round's split epilogue, run its 2-means iterations if any record
@@ -842,7 +926,7 @@ void Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specul
   // 2-means iterations go in before its split status is known -- a record
   // final at the split makes them exit at once (~4 us each); C3's last round
   // needs them and otherwise waited ~15 us for the host to see the status.
-  if (speculate && fixed_point_ && S == 1 && comm_ == nullptr)
+  if (speculate && fixed_point_)
     for (; launched < max_iters && launched <= lookahead_; ++launched) kmeans_iter(R, launched, max_iters, stream);
   if (fixed_point_) all_proven = wait_status(stat + max_iters, R.seq, stream) == 0;
   if (R.planned) {   // the plan's counts equal the host's mirror of its layout
@@ -927,6 +1011,12 @@ void Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specul
     collect_timing();
   }
 
+  if (R.stats_only)   // written by PS_LATE iff the node or its sibling was active after its split
+    for (int a = 0; a + 1 < nl; a += 2) {
+      const bool written = !(res[a * S].proven && res[(a + 1) * S].proven);
+      nodes_[R.order[a]].points = written;
+      nodes_[R.order[a + 1]].points = written;
+    }
   for (int a = 0; a < nl; ++a) {
     const int id = R.order[a];
     const NodeResult& r = res[a * S];   // global results: every record agrees
@@ -1219,6 +1309,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     }
     const size_t tiles_cap = px / kSweep + rec_cap * (size_t)node_tiles_ + 64;
     ensure_round(rec_cap, tiles_cap, 0, 0, max_iters, stream);
+    if (tot_mode() == TOT_ALLREDUCE) ensure_totals(rec_cap / S + 64, stream);
   }
   rounds_.clear();
   // Rounds in flight, oldest first.  While the oldest is the only one, the
@@ -1337,6 +1428,7 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     DQ_CHECK(nr * nc <= 0xFFFFFFF0ull, "too many points");
   }
   const uint32_t n = gather ? (uint32_t)(nr * nc) : job.n;
+  if (!h_wactive_) DQ_HIP(hipHostMalloc((void**)&h_wactive_, 64, hipHostMallocDefault));
   ensure_round(2 * (size_t)job.k + 64, 1024, 0, 0, max_iters, stream);   // staging, results
   // scratch: colour table, unique colours + weights, two id buffers (P0/P1)
   const size_t need_scratch = color_table_scratch_bytes(n);
@@ -1375,6 +1467,7 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
   nshard_ = 1;
   last_rounds = last_planned = last_aborted = 0;
   last_points_swept = last_points_full = 0;
+  last_seq_tiles = 0;
   FrameState& f = frames_[0];
   f.job = &job;
   f.s = 0.0;
@@ -1392,46 +1485,115 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
   std::vector<int> active;
   if (job.k > 1) active.push_back(0);
   std::vector<NodeResult> res;
+  std::vector<WTile> tiles;
   while (!active.empty()) {
+    // the round's records and tiles (kWTile points each, at least one per node)
     const int nn = (int)active.size();
-    const size_t rec_bytes = ((size_t)nn * sizeof(WNode) + 255) & ~(size_t)255;
-    const size_t bytes = rec_bytes + (size_t)nn * sizeof(NodeResult);
+    tiles.clear();
+    for (int a = 0; a < nn; ++a) {
+      const Seg& sg = seg(active[a], 0);
+      for (uint32_t o = 0; o == 0 || o < sg.len; o += kWTile)
+        tiles.push_back(WTile{a, sg.off + o, sg.off + std::min<uint32_t>(sg.len, o + kWTile), 0u});
+    }
+    const int nt = (int)tiles.size();
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_tiles = al((size_t)nn * sizeof(WState));
+    const size_t up_bytes = o_tiles + al((size_t)nt * sizeof(WTile));
+    const size_t o_tsum = up_bytes;
+    const size_t o_tpre = o_tsum + al((size_t)nt * 8 * sizeof(double));
+    const size_t o_fold = o_tpre + al((size_t)nt * 8 * sizeof(double));
+    const size_t o_quick = o_fold + al((size_t)nt * kWCh * sizeof(WFold));
+    const size_t o_pbase = o_quick + al((size_t)nt * kWCh * sizeof(WQuick));
+    const size_t o_res = o_pbase + al((size_t)nt * 2 * sizeof(uint32_t));
+    const size_t o_act = o_res + al((size_t)nn * sizeof(NodeResult));
+    const size_t bytes = o_act + 256;
     if (bytes > cap_wnodes_) {
       DQ_HIP(hipStreamSynchronize(stream));
       if (d_wnodes_) DQ_HIP(hipFree(d_wnodes_));
-      cap_wnodes_ = std::max<size_t>(bytes, 1 << 16);
+      cap_wnodes_ = std::max<size_t>(bytes, 1 << 20);
       DQ_HIP(hipMalloc(&d_wnodes_, cap_wnodes_));
     }
     if (stage_pending_) {
       DQ_HIP(hipEventSynchronize(stage_ev_));
       stage_pending_ = false;
     }
-    DQ_CHECK(rec_bytes <= cap_stage_tab_, "staging too small for the weighted round");
-    WNode* hw = reinterpret_cast<WNode*>(h_stage_);
+    if (up_bytes > cap_stage_tab_) {
+      DQ_HIP(hipHostFree(h_stage_));
+      const size_t c = std::max<size_t>(up_bytes, 2 * cap_stage_tab_);
+      DQ_HIP(hipHostMalloc((void**)&h_stage_, c, hipHostMallocCoherent | hipHostMallocMapped));
+      DQ_HIP(hipHostGetDevicePointer((void**)&d_stage_view_, h_stage_, 0));
+      cap_stage_tab_ = c;
+    }
+    WState* hw = reinterpret_cast<WState*>(h_stage_);
+    int t = 0;
+    bool has_root = false;
     for (int a = 0; a < nn; ++a) {
-      const Node& nd = nodes_[active[a]];
+      Node& nd = nodes_[active[a]];
       const Seg& sg = seg(active[a], 0);
-      WNode& w = hw[a];
+      WState& w = hw[a];
       std::memset(&w, 0, sizeof w);
       w.src = nd.buf == BUF_P0 ? d_p0_ : d_p1_;
       w.dst = nd.buf == BUF_P0 ? d_p1_ : d_p0_;
       w.off = sg.off;
       w.len = sg.len;
-      w.tw = nd.w;
-      for (int c = 0; c < 3; ++c) { w.tm[c] = nd.mean[c]; w.tv[c] = nd.var[c]; }
+      w.tile_begin = t;
+      while (t < nt && tiles[t].node == a) ++t;
+      w.tile_end = t;
       w.root = active[a] == 0 ? 1 : 0;
+      has_root |= w.root != 0;
+      w.tw = nd.w;
+      for (int c = 0; c < 3; ++c) {
+        w.tm[c] = nd.mean[c];
+        w.tv[c] = nd.var[c];
+        w.box_lo[c] = nd.lo[c];
+        w.box_hi[c] = nd.hi[c];
+      }
+      if (!w.root) {   // the cut (:388-403); the root's comes from its init folds
+        double maxv = nd.var[0], cut = nd.mean[0];
+        int axis = 0;
+        if (maxv < nd.var[1]) { maxv = nd.var[1]; axis = 1; cut = nd.mean[1]; }
+        if (maxv < nd.var[2]) { axis = 2; cut = nd.mean[2]; }
+        w.axis = axis;
+        w.cut = cut;
+      }
+      w.done_it = -1;
     }
-    launch_upload(d_wnodes_, d_stage_view_, rec_bytes, stream);
+    std::memcpy(h_stage_ + o_tiles, tiles.data(), (size_t)nt * sizeof(WTile));
+    char* db = static_cast<char*>(d_wnodes_);
+    launch_upload(db, d_stage_view_, up_bytes, stream);
     DQ_HIP(hipEventRecord(stage_ev_, stream));
     stage_pending_ = true;
     WArgs wa;
-    wa.nodes = reinterpret_cast<const WNode*>(d_wnodes_);
+    wa.nodes = reinterpret_cast<WState*>(db);
+    wa.tiles = reinterpret_cast<const WTile*>(db + o_tiles);
     wa.ucol = d_wcol_;
     wa.uw = d_ww_;
-    wa.res = reinterpret_cast<NodeResult*>(static_cast<char*>(d_wnodes_) + rec_bytes);
+    wa.tsum = reinterpret_cast<double*>(db + o_tsum);
+    wa.tpre = reinterpret_cast<double*>(db + o_tpre);
+    wa.fold = reinterpret_cast<WFold*>(db + o_fold);
+    wa.quick = reinterpret_cast<WQuick*>(db + o_quick);
+    wa.pbase = reinterpret_cast<uint32_t*>(db + o_pbase);
+    wa.res = reinterpret_cast<NodeResult*>(db + o_res);
+    wa.active = reinterpret_cast<uint32_t*>(db + o_act);
+    wa.nn = nn;
+    wa.ntiles = nt;
     wa.max_iters = max_iters;
     wa.fixed_point = fixed_point_ ? 1 : 0;
-    launch_wsplit(wa, nn, stream);
+    wa.it = 0;
+    wa.pad = 0;
+    if (has_root) launch_wpass(WP_INIT, wa, stream);   // (a round holding the root holds only it)
+    DQ_HIP(hipMemsetAsync(wa.active, 0, 4, stream));
+    launch_wpass(WP_SPLIT, wa, stream);
+    // 2-means passes only when some split is not proven final at the split
+    DQ_HIP(hipMemcpyAsync(h_wactive_, wa.active, 4, hipMemcpyDeviceToHost, stream));
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (*h_wactive_ != 0) {
+      for (int it = 0; it < max_iters; ++it) {
+        wa.it = it;
+        launch_wpass(WP_KM, wa, stream);
+      }
+    }
+    launch_wfinish(wa, stream);
     res.resize(nn);
     DQ_HIP(hipMemcpyAsync(res.data(), wa.res, (size_t)nn * sizeof(NodeResult), hipMemcpyDeviceToHost, stream));
     DQ_HIP(hipStreamSynchronize(stream));
@@ -1440,8 +1602,19 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
       const int id = active[a];
       const NodeResult& r = res[a];
       last_points_swept += seg(id, 0).len;
+      last_seq_tiles += (uint32_t)r.pad;
       if (id == 0)
         for (int c = 0; c < 3; ++c) { nodes_[0].mean[c] = r.tm[c]; nodes_[0].var[c] = r.tv[c]; }
+      {   // the cut the split ran with (the children's boxes)
+        const Node& n = nodes_[id];
+        double maxv = n.var[0], cut = n.mean[0];
+        int axis = 0;
+        if (maxv < n.var[1]) { maxv = n.var[1]; axis = 1; cut = n.mean[1]; }
+        if (maxv < n.var[2]) { axis = 2; cut = n.mean[2]; }
+        nodes_[id].axis = (int16_t)axis;
+        nodes_[id].thr = (int16_t)split_threshold(cut);
+      }
+      DQ_CHECK(r.n_new_local == (uint32_t)r.n_new, "weighted partition count differs from the fold count");
       Node co, cn;
       const int io = (int)nodes_.size();
       const Node& p = nodes_[id];
@@ -1454,6 +1627,12 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
         cn.mean[c] = r.nm[c];
         co.var[c] = r.ov[c];
         cn.var[c] = r.nv[c];
+        co.lo[c] = cn.lo[c] = p.lo[c];
+        co.hi[c] = cn.hi[c] = p.hi[c];
+      }
+      if (r.proven) {   // the halves are the cut's: v_axis < thr | >= thr
+        co.hi[p.axis] = (int16_t)std::min<int>(p.hi[p.axis], p.thr - 1);
+        cn.lo[p.axis] = (int16_t)std::max<int>(p.lo[p.axis], p.thr);
       }
       co.tse = r.tse_old;
       cn.tse = r.tse_new;

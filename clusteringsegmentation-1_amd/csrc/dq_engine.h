@@ -35,9 +35,6 @@ namespace dq {
     if (!(cond)) ::dq::die(#cond, __FILE__, __LINE__, msg);               \
   } while (0)
 
-// Row-range shards a frame may be split into inside ONE process (virtual
-// shards on one GPU: the exact arithmetic of multi-GPU row sharding).
-constexpr int kMaxShard = 8;
 
 // A node of a frame's split tree: one cluster as it exists between splits.
 // Its points are spread over the frame's shards: one local segment per
@@ -49,7 +46,9 @@ struct Node {
   int32_t buf = 0;                   // 0: caller's input, 1: P0, 2: P1
   bool expanded = false;
   bool queued = false;               // in a round enqueued but not yet finished
-  bool partitioned = false;          // children's points written to child_buf(buf)
+  bool partitioned = false;          // children's segments assigned in child_buf(buf)
+  bool points = true;                // its segment holds its points (false: a PS_STATS round
+                                     //   computed its split without writing them)
   double w = 0.0;                    // weight[]   (:290, :862-863)
   double mean[3] = {0, 0, 0};        // mean[]     (:309)
   double var[3] = {0, 0, 0};         // var[]      (:314)
@@ -180,6 +179,7 @@ class Engine {
   int last_aborted = 0;               // planned rounds whose plan found a parent unfinished
   uint64_t last_points_swept = 0;     // sum over passes of points read (all frames)
   uint64_t last_points_full = 0;      // the same without fixed-point finalisation
+  uint64_t last_seq_tiles = 0;        // weighted: tiles folded one summand at a time
 
   void set_timing(bool on) { timing_ = on; }
   bool timing() const { return timing_; }
@@ -247,6 +247,7 @@ class Engine {
     uint32_t* dcounts = nullptr;      // planned: plan_kernel's counts (device)
     RoundArgs ra{};
     bool kmeans = false;              // its split epilogue left records active
+    bool stats_only = false;          // planned, a frame's last: partsplit PS_STATS (+ PS_LATE)
     std::vector<std::pair<size_t, int>> km_events;
     double t_enq = 0;
   };
@@ -370,13 +371,18 @@ class Engine {
   size_t cap_w_ = 0;
   void* d_wscratch_ = nullptr;        // colour-table scratch (sorts)
   size_t cap_wscratch_ = 0;
-  void* d_wnodes_ = nullptr;          // a round's WNode records + results
+  void* d_wnodes_ = nullptr;          // a round's WState records, tiles, fold tables, results
+  uint32_t* h_wactive_ = nullptr;     // pinned: the round's nodes not final after the split
   size_t cap_wnodes_ = 0;
 
   std::vector<Node> nodes_;
   std::vector<Seg> segs_;             // node * nshard_ + shard
   Seg& seg(int node, int shard) { return segs_[(size_t)node * nshard_ + shard]; }
   int nshard_ = 1;                    // shard records per logical node in this run
+  // where a pass's node totals come from (TotMode): own record, the node's
+  // shard records in this process, or an allreduce across processes
+  int tot_mode() const { return comm_ ? TOT_ALLREDUCE : (nshard_ > 1 ? TOT_NODE : TOT_OWN); }
+  void ensure_totals(size_t nlogical, hipStream_t stream);
   uint64_t* d_tot_ = nullptr;         // sharded rounds: per logical node totals
   size_t cap_tot_ = 0;
   void* comm_ = nullptr;              // ncclComm_t across processes (row-tile sharding)

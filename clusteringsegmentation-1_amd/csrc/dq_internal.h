@@ -20,6 +20,10 @@
 
 namespace dq {
 
+// Row-range shards a frame may be split into inside ONE process (virtual
+// shards on one GPU: the exact arithmetic of multi-GPU row sharding).
+constexpr int kMaxShard = 8;
+
 // Pass kinds (kernel template parameter).
 enum PassKind : int32_t {
   PASS_INIT = 0,     // root only: count, sums and sums of squares (:49-104)

@@ -50,7 +50,29 @@ struct RoundArgs {
   const uint32_t* counts;   // planned rounds: [tiles, part tiles, aborted] written by
                             //   plan_kernel (grids are upper bounds); nullptr: host-built
   uint64_t plane;           // bytes between the R, G and B planes of P0 / P1
+  int32_t tot_mode;         // where a record's pass totals come from (TotMode)
+  int32_t ps_mode;          // what partsplit_kernel does (PsMode)
 };
+
+// partsplit_kernel's work (RoundArgs::ps_mode):
+//   PS_FULL  -- the parents' points into the children's segments, the
+//               children's split-pass sums and per-(tile, wave) counts;
+//   PS_STATS -- the children's split-pass sums only, nothing written (a
+//               frame's last round: its nodes' children are leaves, and a
+//               node's own points are needed only for its 2-means passes);
+//   PS_LATE  -- after PS_STATS and the split epilogue: the points of every
+//               parent with a child still active (not proven at its split),
+//               for the children's 2-means passes; nothing else;
+//   PS_WRITE -- the points of the listed parents only (a later round needs
+//               the segments of nodes a PS_STATS round left unwritten).
+enum PsMode : int32_t { PS_FULL = 0, PS_STATS = 1, PS_LATE = 2, PS_WRITE = 3 };
+
+// How the FP64 update of a pass gets the node's totals (RoundArgs::tot_mode):
+// the record's own tile partials (one shard, no communicator); the partials
+// of every shard record of the logical node (virtual row shards in this
+// process); or RoundArgs::tot, the logical node's totals of this process
+// allreduced across processes (RCCL) before the epilogue.
+enum TotMode : int32_t { TOT_OWN = 0, TOT_NODE = 1, TOT_ALLREDUCE = 2 };
 
 // A round planned on the device (plan_kernel): the children of every listed
 // record of the previous round are this round's nodes, record 2i = the old
@@ -62,7 +84,7 @@ struct PlanArgs {
   const DevNode* pn;        // previous round: records
   const NodeResult* pres;   //                 results (device copy)
   const Tile* ptiles;       //                 tiles (the part tiles point into them)
-  const int32_t* plist;     // parent records to split (host-coherent pinned memory)
+  const int32_t* plist;     // parent (logical) nodes to split (host-coherent pinned memory)
   int32_t np;
   int32_t node_tiles;       // tiles per record at least (Engine::tile_len)
   uint32_t tl;              // tile length of the round (Engine::tile_len)
@@ -78,7 +100,7 @@ struct PlanArgs {
   const uint8_t* p1;        //   other one of its src)
   uint64_t cap_bytes;       // bytes per working buffer
   int32_t debug;            // kDebug* flags
-  int32_t pad;
+  int32_t nshard;           // records per logical node (record = node * nshard + shard)
 };
 constexpr int kPlanMaxParents = 6144;
 
@@ -104,15 +126,17 @@ void launch_upload(void* dst, const void* src_dev_view, size_t bytes, hipStream_
 
 // One statistics pass over tiles [0, ntiles) of the round (one workgroup per tile).
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
-// A 2-means pass with its epilogue fused (unsharded rounds; kpass_kernel).
+// A 2-means pass with its epilogue fused (kpass_kernel): the logical node's
+// last workgroup runs the FP64 update of every shard record of the node; with
+// TOT_ALLREDUCE it only writes the node's totals to a.tot (the allreduce and
+// launch_epilogue follow).
 void launch_kpass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
-// The FP64 update after a pass, one workgroup per node record: sums the
-// node's tile partials (from_totals: reads the node's global totals instead)
-// and publishes the next pass's decision (or the split's results).
-void launch_epilogue(int kind, const RoundArgs& a, int nnodes, bool from_totals,
-                     hipStream_t stream);
-// Sharded rounds: per logical node, the sums of the pass over all its shard
-// records' tiles into a.tot (to be allreduced across processes).
+// The FP64 update after a pass, one workgroup per node record: the node's
+// totals per a.tot_mode, the record's own partials for its local counts;
+// publishes the next pass's decision (or the split's results).
+void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream);
+// TOT_ALLREDUCE rounds: per logical node, the sums of the pass over all its
+// shard records' tiles into a.tot (to be allreduced across processes).
 void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stream);
 // Fused partition + split pass over the round's PartTiles: writes each
 // parent's points into its two children's segments (old half first, then new

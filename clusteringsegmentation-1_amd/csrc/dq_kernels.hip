@@ -633,6 +633,7 @@ __device__ __forceinline__ void block_sum7(uint64_t acc[7], uint64_t (*red)[8], 
 template <int KIND>
 __global__ __launch_bounds__(kBlock) void nodesum_kernel(RoundArgs a) {
   constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
+  if (a.counts && a.counts[2] != 0) return;   // planned round aborted by its plan
   __shared__ uint64_t red[kBlock / 64][8];
   const DevNode* w0 = a.nodes + (size_t)blockIdx.x * a.nshard;
   uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -790,10 +791,12 @@ __device__ __forceinline__ void arrive(LaunchCtr* c, uint32_t rec, uint32_t nn, 
 
 // ---------------------------------------------------------------------------
 // Epilogue: ONE WORKGROUP per node record of the round.
-//   * the node's sums: its own partials (FROM_TOT: the logical node's global
-//     totals from nodesum + allreduce; its own partials then only give the
-//     record's local new-half size), summed by all kEpiBlock lanes (a record
-//     of an early round has ~1000 tile partials), then reduced in LDS;
+//   * the node's sums (MODE, TotMode): its own partials (TOT_OWN), those of
+//     every shard record of the logical node (TOT_NODE), or the node's
+//     totals from nodesum + allreduce (TOT_ALLREDUCE); its own partials
+//     always give the record's local new-half size.  Summed by all kEpiBlock
+//     lanes (a record of an early round has ~1000 tile partials), then
+//     reduced in LDS;
 //   * wave 0, lane 0 runs the FP64 update (node_update) -- every record of a
 //     logical node runs it on the same totals, so all agree bit for bit;
 //   * a record whose split became final: the partition's per-(tile, wave)
@@ -811,7 +814,7 @@ constexpr int kEpiBlock = 256;
 // and the cursor scan then read LDS, not one dependent global round trip
 // after another; the updated record is written back once.
 constexpr int kEpiStageTiles = 1024;
-template <int KIND, bool FROM_TOT>
+template <int KIND, int MODE>
 __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
   constexpr bool kMeans = KIND == PASS_KMEANS || KIND == PASS_KLAST;
   if (a.counts && a.counts[2] != 0) return;   // planned round aborted by its plan
@@ -835,19 +838,30 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
   __shared__ NodeResult sres;
   __shared__ uint64_t red[kEpiBlock / 64][8];
   uint64_t tot[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t own_new = 0;   // the record's own new-side count (its partition share)
   if (!skip) {
     uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
     sum_record<KIND, kEpiBlock>(a, w, acc, (int)threadIdx.x);
+    own_new = acc[F_CNT];
+    if (MODE == TOT_NODE) {   // every shard record of the logical node
+      const int r0 = (int)(blockIdx.x / a.nshard) * a.nshard;
+      for (int r = r0; r < r0 + a.nshard; ++r)
+        if (r != (int)blockIdx.x) sum_record<KIND, kEpiBlock>(a, a.nodes + r, acc, (int)threadIdx.x);
+    }
+    own_new = wave_sum_u64(own_new);
 #pragma unroll
     for (int k = 0; k < F_NUM; ++k) acc[k] = wave_sum_u64(acc[k]);
     if (lane == 0) {
 #pragma unroll
       for (int k = 0; k < F_NUM; ++k) red[wave_id()][k] = acc[k];
+      red[wave_id()][7] = own_new;
     }
     __syncthreads();
+    own_new = 0;
 #pragma unroll
     for (int k = 0; k < F_NUM; ++k)
       for (int v = 0; v < kEpiBlock / 64; ++v) tot[k] += red[v][k];   // (every lane)
+    for (int v = 0; v < kEpiBlock / 64; ++v) own_new += red[v][7];
   }
   // lane 0 of wave 0: the FP64 update; the workgroup: the partition cursors
   // of a record whose split became final; wave 0: results + arrival
@@ -856,8 +870,8 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
   if (threadIdx.x == 0) {
     int fin = 0;
     if (!skip) {
-      const uint32_t local_new = (uint32_t)tot[F_CNT];
-      if (FROM_TOT) {
+      const uint32_t local_new = (uint32_t)own_new;
+      if (MODE == TOT_ALLREDUCE) {
         const uint64_t* g = a.tot + (size_t)(blockIdx.x / a.nshard) * 8;
         for (int k = 0; k < F_NUM; ++k) tot[k] = g[k];
       }
@@ -894,62 +908,90 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// 2-means pass with its epilogue fused (unsharded rounds): pass_kernel's
-// sweep, then the record's LAST workgroup to finish runs the record's
-// epilogue (one wave; exactly epilogue_kernel<KIND, false>).  Partials and
-// per-wave counts are stored at agent scope and read back at agent scope
-// (the XCDs' L2s are not coherent with each other); every workgroup drains
-// its stores (barrier: vmcnt(0)) before counting itself in.  A record final
-// in an earlier launch arrives through its first tile's workgroup.
+// 2-means pass with its epilogue fused: pass_kernel's sweep, then the LOGICAL
+// node's last workgroup to finish (over the tiles of all its shard records)
+// runs the node's epilogue in one wave: the node's totals, then lane s the
+// FP64 update of shard record s (every record on the same totals, so all
+// agree bit for bit), each record's partition cursors, results and arrival --
+// exactly epilogue_kernel<KIND, TOT_OWN / TOT_NODE> for the records.  With
+// TOT_ALLREDUCE the wave only writes the node's totals of this process to
+// a.tot; the allreduce and epilogue_kernel<KIND, TOT_ALLREDUCE> follow.
+// Partials and per-wave counts: see the hand-off comment in kpass_kernel.
 template <int KIND>
-__device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int rec, NodeResult* sres) {
-  DevNode* w = a.nodes + rec;
+__device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int node, NodeResult* sres) {
+  const int S = a.nshard, r0 = node * S;
   const uint32_t lane = lane_id();
-  const int tb = w->tile_begin, te = w->tile_end;
-  uint64_t acc[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
   const uint32_t* pp = reinterpret_cast<const uint32_t*>(a.parts);
-  for (int i = tb + (int)lane; i < te; i += 64)
+  uint64_t tot[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t my_new = 0;   // lane s: shard record s's own new-side count
+  for (int sh = 0; sh < S; ++sh) {
+    const DevNode* w = a.nodes + r0 + sh;
+    const int tb = w->tile_begin, te = w->tile_end;
+    uint64_t acc[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
+    for (int i = tb + (int)lane; i < te; i += 64)
 #pragma unroll
-    for (int k = 0; k < F_NUM; ++k)
-      acc[k] += __hip_atomic_load(pp + (size_t)i * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint64_t tot[F_NUM];
+      for (int k = 0; k < F_NUM; ++k)
+        acc[k] += __hip_atomic_load(pp + (size_t)i * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-  for (int k = 0; k < F_NUM; ++k) tot[k] = wave_sum_u64(acc[k]);
-  int fin = 0;
-  if (lane == 0) {
-    fin = node_update<KIND>(w, sres, tot, a.fixed_point != 0) ? 1 : 0;
-    if (fin) {
-      for (int c = 0; c < 3; ++c) { sres->tm[c] = w->tm[c]; sres->tv[c] = w->tv[c]; }
-      w->n_new_local = (uint32_t)tot[F_CNT];
-      sres->n_new_local = (uint32_t)tot[F_CNT];
-      sres->done_it = w->done_it;
+    for (int k = 0; k < F_NUM; ++k) {
+      const uint64_t v = wave_sum_u64(acc[k]);
+      tot[k] += v;
+      if (k == F_CNT && lane == (uint32_t)sh) my_new = (uint32_t)v;
     }
   }
-  const bool final_results = __shfl(fin, 0, 64) != 0;
-  if (final_results) record_cursors<true>(a.tiles, a.wparts, tb, te, lane);
+  if (a.tot_mode == TOT_ALLREDUCE) {   // this process's node totals, for the allreduce
+    if (lane < (uint32_t)F_NUM + 1) {
+      uint64_t v = 0;
+#pragma unroll
+      for (int k = 0; k < F_NUM; ++k) v = lane == (uint32_t)k ? tot[k] : v;
+      a.tot[(size_t)node * 8 + lane] = v;
+    }
+    return;
+  }
+  int fin = 0;
+  if (lane < (uint32_t)S) {
+    DevNode* w = a.nodes + r0 + lane;
+    NodeResult* r = sres + lane;
+    fin = node_update<KIND>(w, r, tot, a.fixed_point != 0) ? 1 : 0;
+    if (fin) {
+      for (int c = 0; c < 3; ++c) { r->tm[c] = w->tm[c]; r->tv[c] = w->tv[c]; }
+      w->n_new_local = my_new;
+      r->n_new_local = my_new;
+      r->done_it = w->done_it;
+    }
+  }
+  const bool final_results = __shfl(fin, 0, 64) != 0;   // (every record of the node agrees)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (final_results) store_result(a.hres + rec, a.dres ? a.dres + rec : nullptr, *sres, lane, w->len, a.seq);
+  if (final_results) {
+    for (int sh = 0; sh < S; ++sh) {
+      const DevNode* w = a.nodes + r0 + sh;
+      record_cursors<true>(a.tiles, a.wparts, w->tile_begin, w->tile_end, lane);
+      store_result(a.hres + r0 + sh, a.dres ? a.dres + r0 + sh : nullptr, sres[sh], lane, w->len, a.seq);
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0)
-    arrive(a.ctr + a.it, (uint32_t)rec, (uint32_t)a.nn, !final_results, a.hstat + a.it, a.seq);
+  if (lane < (uint32_t)S)
+    arrive(a.ctr + a.it, (uint32_t)(r0 + lane), (uint32_t)a.nn, !final_results, a.hstat + a.it, a.seq);
 }
 
 template <int KIND>
 __global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const int rec = t.node;
+  const int S = a.nshard;
+  const int node = S == 1 ? rec : rec / S;
   const DevNode& nd = a.nodes[rec];
   if (nd.done_it != 0) {   // final in an earlier launch: its first tile arrives for it
-    if ((int)blockIdx.x == nd.tile_begin && threadIdx.x == 0)
+    if (a.tot_mode != TOT_ALLREDUCE && (int)blockIdx.x == nd.tile_begin && threadIdx.x == 0)
       arrive(a.ctr + a.it, (uint32_t)rec, (uint32_t)a.nn, false, a.hstat + a.it, a.seq);
-    return;
+    return;   // (TOT_ALLREDUCE: the epilogue kernel arrives for every record)
   }
   const Params q = nd.prm;
   __shared__ uint32_t red[kBlock / 64][8];
   __shared__ int slast;
-  __shared__ NodeResult sres;
+  __shared__ NodeResult sres[kMaxShard];
   LaneSums s;
   uint32_t ws, we;
   wave_range(t.start, t.end, wave_id(), ws, we);
@@ -960,10 +1002,11 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) 
 #pragma unroll
   for (int k = 0; k < F_NUM; ++k) f[k] = wave_sum_u32(f[k]);
   const uint32_t vsum = wave_sum_u32(s.vcnt);
-  if (a.debug & kDebugPrewarm) {   // (tests) the record's hand-off lines into this CU's caches
+  if (a.debug & kDebugPrewarm) {   // (tests) the node's hand-off lines into this CU's caches
     const uint32_t* pp = reinterpret_cast<const uint32_t*>(a.parts);
+    const int tb0 = a.nodes[node * S].tile_begin, te0 = a.nodes[node * S + S - 1].tile_end;
     uint32_t x = 0;
-    for (int i = nd.tile_begin + (int)lane_id(); i < nd.tile_end; i += 64) {
+    for (int i = tb0 + (int)lane_id(); i < te0; i += 64) {
       for (int k = 0; k < 8; ++k) x += pp[(size_t)i * 8 + k];
       for (int k = 0; k < 8; ++k) x += __hip_atomic_load(pp + (size_t)i * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int ww = 0; ww < kTileWaves; ++ww) x += a.wparts[(size_t)i * kTileWaves + ww];
@@ -984,7 +1027,7 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) 
     for (int w = 0; w < kBlock / 64; ++w) x += red[w][threadIdx.x];
     __hip_atomic_store(a.parts[blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // Hand-off to the record's last arriver (the gfx950 agent-
+  // Hand-off to the node's last arriver (the gfx950 agent-
   // scope protocol of MI355X_MICROARCH.md "inter-workgroup visibility"):
   //   producer (every workgroup): the partial and the per-wave counts are
   //     write-through (sc1) stores; EVERY wave drains them (asm vmcnt(0):
@@ -998,9 +1041,10 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const bool last = __hip_atomic_fetch_add(a.rdone + (size_t)a.it * a.nn + rec, 1u, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) ==
-                      (uint32_t)(nd.tile_end - nd.tile_begin) - 1;
+    const int ntiles = S == 1 ? nd.tile_end - nd.tile_begin
+                              : a.nodes[node * S + S - 1].tile_end - a.nodes[node * S].tile_begin;
+    const bool last = __hip_atomic_fetch_add(a.rdone + (size_t)a.it * a.nn + node, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)ntiles - 1;
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1008,7 +1052,7 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) 
     slast = last;
   }
   __syncthreads();
-  if (slast && wave_id() == 0) kmeans_epilogue_wave<KIND>(a, rec, &sres);
+  if (slast && wave_id() == 0) kmeans_epilogue_wave<KIND>(a, node, sres);
 }
 
 // ---------------------------------------------------------------------------
@@ -1266,7 +1310,7 @@ struct Stage {
 // ballot (a full sweep: a lane's rank among the new points is its lane id
 // minus its rank among the old ones).  PRE: also count, per lane, the
 // children's split-new points (xm / ym) at child positions below ex / ey.
-template <bool PRE>
+template <bool PRE, bool STORE = true>
 __device__ __forceinline__ void stage_sweep(const Sweep& w, const SweepMask& om, const SweepMask& nm, bool full,
                                             uint8_t* st, Stage& g, uint32_t l, const SweepMask& xm,
                                             const SweepMask& ym, uint32_t ex, uint32_t ey, uint32_t& ax,
@@ -1277,9 +1321,11 @@ __device__ __forceinline__ void stage_sweep(const Sweep& w, const SweepMask& om,
   const uint32_t exs = ex - g.cbo, eys = ey - g.cbn;
   auto put = [&](int s, uint32_t lp) {
     const int j = s >> 2, sh = 8 * (s & 3);
-    st[lp] = (uint8_t)(w.r[j] >> sh);
-    st[kStagePlane + lp] = (uint8_t)(w.g[j] >> sh);
-    st[2 * kStagePlane + lp] = (uint8_t)(w.b[j] >> sh);
+    if (STORE) {   // (STORE false: the run positions only, for the children's counts)
+      st[lp] = (uint8_t)(w.r[j] >> sh);
+      st[kStagePlane + lp] = (uint8_t)(w.g[j] >> sh);
+      st[2 * kStagePlane + lp] = (uint8_t)(w.b[j] >> sh);
+    }
     if (PRE) {
       ax += (uint32_t)(slot_in(xm, s) && lp < exs);
       ay += (uint32_t)(slot_in(ym, s) && lp - kStageRun < eys);
@@ -1395,7 +1441,7 @@ typedef uint8_t StageMem;
 // read from a PartTile made these flat loads)
 typedef const __attribute__((address_space(1))) DevNode g_cnode;
 typedef const __attribute__((address_space(1))) Tile g_ctile;
-template <bool PLANAR, bool BGR = false>
+template <bool PLANAR, bool BGR, int MODE>
 __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g_ctile* tp,
                                               const DevNode* nodes, uint32_t* wparts, uint64_t plane,
                                               StageMem* st, SplitSums& so, SplitSums& sn) {
@@ -1428,9 +1474,10 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   const bool cut = nd.proven != 0;
   const uint32_t sh0 = (uint32_t)pt.shift[0], sh1 = (uint32_t)pt.shift[1];
   const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
-  ChunkAcc cx, cy;
-  chunk_init(cx, nodes, wparts, pt.child[0], oc0);
-  chunk_init(cy, nodes, wparts, pt.child[1], nc0);
+  constexpr bool kStore = MODE != PS_STATS, kSums = MODE == PS_FULL || MODE == PS_STATS;
+  ChunkAcc cx, cy;   // (the children's per-(tile, wave) counts: PS_FULL and PS_STATS)
+  chunk_init(cx, nodes, wparts, kSums ? pt.child[0] : -1, oc0);
+  chunk_init(cy, nodes, wparts, kSums ? pt.child[1] : -1, nc0);
   Stage g;
   constexpr uint32_t kPnOff = kStageRun;
   g.cbo = oc0 & ~15u;
@@ -1502,8 +1549,10 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
       xm.m[j] &= om.m[j];   // new for the old child
       ym.m[j] &= nm.m[j];   // new for the new child
     }
-    add_sums_bytes(sw, xm, so);
-    add_sums_bytes(sw, ym, sn);
+    if (kSums) {
+      add_sums_bytes(sw, xm, so);
+      add_sums_bytes(sw, ym, sn);
+    }
     // this wave's points.  A sweep writes at most kWaveSweep points to each
     // child: when neither child's current chunk can end inside it (fast
     // sweep), only the lanes' new counts are kept; otherwise every slot's run
@@ -1511,34 +1560,40 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     const uint32_t oc = g.cbo + g.po, nc = g.cbn + g.pn - kPnOff;
     const bool fast = oc + kWaveSweep <= cx.end && nc + kWaveSweep <= cy.end;
     uint32_t ax = 0, ay = 0;
-    if (fast) stage_sweep<false>(sw, om, nm, full, st, g, l, xm, ym, 0u, 0u, ax, ay);
-    else stage_sweep<true>(sw, om, nm, full, st, g, l, xm, ym, cx.end, cy.end, ax, ay);
+    // (PS_STATS: the run positions only -- the children's per-(tile, wave)
+    // counts are the partition cursors a later round may need -- no stores)
+    if (fast) stage_sweep<false, kStore>(sw, om, nm, full, st, g, l, xm, ym, 0u, 0u, ax, ay);
+    else stage_sweep<true, kStore>(sw, om, nm, full, st, g, l, xm, ym, cx.end, cy.end, ax, ay);
     chunk_sweep(cx, oc, g.cbo + g.po, mask_count(xm), ax);
     chunk_sweep(cy, nc, g.cbn + g.pn - kPnOff, mask_count(ym), ay);
-    stage_flush(st, d, g, l);
+    if (kStore) stage_flush(st, d, g, l);
     x = xn;
     vs = nvs;
     full = nfull;
   }
-  stage_bytes(st, d, g, g.cbo + g.po, g.cbn + g.pn - kStageRun, l);   // the runs' last partial chunks
+  if (kStore) stage_bytes(st, d, g, g.cbo + g.po, g.cbn + g.pn - kStageRun, l);   // the runs' last partial chunks
   chunk_finish(cx);
   chunk_finish(cy);
 }
 
-__global__ __launch_bounds__(kBlock, 4) void partsplit_kernel(RoundArgs a) {
-  if (a.counts && blockIdx.x >= a.counts[1]) return;   // planned round: grid is an upper bound
+template <int MODE>
+__device__ __forceinline__ void partsplit_body(const RoundArgs& a, uint8_t* stage, uint32_t (*red)[16]) {
   const PartTile pt = a.ptiles[blockIdx.x];
   g_cnode& nd = *(g_cnode*)pt.parent;
   g_ctile* tp = (g_ctile*)pt.tile;
+  if (MODE == PS_LATE) {   // only parents with a child still active after its split epilogue
+    const bool a0 = pt.child[0] >= 0 && a.nodes[pt.child[0]].done_it == 0;
+    const bool a1 = pt.child[1] >= 0 && a.nodes[pt.child[1]].done_it == 0;
+    if (!a0 && !a1) return;
+  }
   SplitSums so, sn;
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
   StageMem* st = stage + wave_id() * kStageWave;
-  if (nd.planar == SRC_PLANAR) partsplit_run<true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
-  else if (nd.planar == SRC_BGR24) partsplit_run<true, true>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
-  else partsplit_run<false>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
+  if (nd.planar == SRC_PLANAR) partsplit_run<true, false, MODE>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
+  else if (nd.planar == SRC_BGR24) partsplit_run<true, true, MODE>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
+  else partsplit_run<false, false, MODE>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
+  if (MODE == PS_WRITE || MODE == PS_LATE) return;   // (no sums: the round's sparts stay)
 
   if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x)) debug_sleep_us(10);
-  __shared__ uint32_t red[kTileWaves][16];
   const uint32_t w = wave_id(), l = lane_id();
   uint32_t f[16] = {so.cnt, so.sr, so.sg, so.sb, so.qr, so.qg, so.qb, 0u,
                     sn.cnt, sn.sr, sn.sg, sn.sb, sn.qr, sn.qg, sn.qb, 0u};
@@ -1555,6 +1610,18 @@ __global__ __launch_bounds__(kBlock, 4) void partsplit_kernel(RoundArgs a) {
     for (int ww = 0; ww < kTileWaves; ++ww) x += red[ww][threadIdx.x];
     // (2 TilePartials: 16 words)
     __hip_atomic_store(a.sparts[2 * blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(kBlock, 4) void partsplit_kernel(RoundArgs a) {
+  if (a.counts && blockIdx.x >= a.counts[1]) return;   // planned round: grid is an upper bound
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
+  __shared__ uint32_t red[kTileWaves][16];
+  switch (a.ps_mode) {
+    case PS_STATS: partsplit_body<PS_STATS>(a, stage, red); break;
+    case PS_LATE: partsplit_body<PS_LATE>(a, stage, red); break;
+    case PS_WRITE: partsplit_body<PS_WRITE>(a, stage, red); break;
+    default: partsplit_body<PS_FULL>(a, stage, red); break;
   }
 }
 
@@ -1663,10 +1730,16 @@ __device__ void plan_child(const PlanArgs& a, const DevNode& P, const NodeResult
 // grid: nb_rec + nb_tile workgroups.  Every workgroup checks that all listed
 // parents are final (else the round aborts) and scans all parents' tile
 // counts into LDS (children's tiles, part tiles: exclusive bases).  Then
-// workgroup b < nb_rec writes the two child records of parents
+// workgroup b < nb_rec writes the child records of (parent, shard) pairs
 // [b * kPlanBlock, ...) (one lane each); the others write one child tile and
-// one part tile per lane (output slot -> parent by binary search), so a
-// parent with ~1000 tiles is spread over the grid.
+// one part tile per lane (output slot -> parent by binary search, then the
+// shard record by a walk over the parent's S records), so a parent with
+// ~1000 tiles is spread over the grid.
+// Shards (a.nshard = S): logical parent i has records pi*S + s; its children
+// are logical nodes 2i (old half) and 2i+1 (new half) with records
+// (2i+side)*S + s, tiles in record order (old half's shards, then the new
+// half's), part tiles in the parent's record order -- Engine::enqueue_host_
+// round's layout.
 constexpr int kPlanBlock = 256;
 __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t nb_rec) {
   __shared__ uint32_t s_cb[kPlanMaxParents + 1];   // children's tiles before parent i
@@ -1674,8 +1747,9 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
   __shared__ uint32_t s_abort;
   __shared__ uint32_t s_w[kPlanBlock / 64][2];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const int32_t np = a.np;
-  auto parent = [&](int32_t i) -> int32_t { return a.plist ? a.plist[i] : i; };
+  const int32_t np = a.np, S = a.nshard;
+  auto parent = [&](int32_t i) -> int32_t { return a.plist ? a.plist[i] : i; };   // logical, in prev
+  auto ntl = [&](uint32_t len) { return plan_ntiles(len, a.tl, a.node_tiles); };
   if (tid == 0) s_abort = 0;
   // clear [LaunchCtr | wparts | rdone] (grid-stride)
   for (uint32_t i = blockIdx.x * kPlanBlock + tid; i < a.nzero; i += gridDim.x * kPlanBlock) a.zero[i] = 0u;
@@ -1694,11 +1768,14 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     for (int e = 0; e < kPlanPer; ++e) {
       t[e] = q[e] = 0;
       if (i0 + e < np) {
-        const DevNode& P = a.pn[parent(i0 + e)];
-        bad |= P.done_it == 0;
-        const uint32_t nn = P.n_new_local;
-        t[e] = plan_ntiles(P.len - nn, a.tl, a.node_tiles) + plan_ntiles(nn, a.tl, a.node_tiles);
-        q[e] = (uint32_t)(P.tile_end - P.tile_begin);
+        const DevNode* P0 = a.pn + (size_t)parent(i0 + e) * S;
+        bad |= P0->done_it == 0;   // (every shard record of a node agrees)
+        for (int sh = 0; sh < S; ++sh) {
+          const DevNode& P = P0[sh];
+          const uint32_t nn = P.n_new_local;
+          t[e] += ntl(P.len - nn) + ntl(nn);
+          q[e] += (uint32_t)(P.tile_end - P.tile_begin);
+        }
       }
       lt += t[e];
       lp += q[e];
@@ -1740,17 +1817,29 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
   }
   if (s_abort || overflow) return;
   if (blockIdx.x < nb_rec) {
-    // (2a) records: parent i -> children 2i (old half), 2i+1 (new half)
-    const int32_t i = (int32_t)(blockIdx.x * kPlanBlock + tid);
-    if (i >= np) return;
-    const int32_t ai = parent(i);
-    const DevNode& P = a.pn[ai];
-    const NodeResult& r = a.pres[ai];
+    // (2a) records: (parent i, shard sh) -> records (2i)*S + sh (old half),
+    //      (2i+1)*S + sh (new half)
+    const int32_t u = (int32_t)(blockIdx.x * kPlanBlock + tid);
+    if (u >= np * S) return;
+    const int32_t i = u / S, sh = u - i * S;
+    const int32_t ai = parent(i) * S;
+    uint32_t told = 0, tnew_all = 0, tnew = 0, pbo = 0;   // tiles / part tiles before this shard's
+    for (int x = 0; x < S; ++x) {
+      const DevNode& Q = a.pn[ai + x];
+      const uint32_t nn = Q.n_new_local;
+      if (x < sh) {
+        told += ntl(Q.len - nn);
+        tnew += ntl(nn);
+        pbo += (uint32_t)(Q.tile_end - Q.tile_begin);
+      }
+      tnew_all += ntl(Q.len - nn);
+    }
+    const DevNode& P = a.pn[ai + sh];
+    const NodeResult& r = a.pres[ai + sh];
     const uint32_t nn = P.n_new_local, lo = P.len - nn;
-    const uint32_t t0 = plan_ntiles(lo, a.tl, a.node_tiles);
-    const int32_t pb = (int32_t)s_pb[i], pe = (int32_t)s_pb[i + 1];
-    plan_child(a, P, r, 0, 2 * i, P.off, lo, (int32_t)s_cb[i], pb, pe);
-    plan_child(a, P, r, 1, 2 * i + 1, P.off + lo, nn, (int32_t)(s_cb[i] + t0), pb, pe);
+    const int32_t pb = (int32_t)(s_pb[i] + pbo), pe = pb + (P.tile_end - P.tile_begin);
+    plan_child(a, P, r, 0, (2 * i) * S + sh, P.off, lo, (int32_t)(s_cb[i] + told), pb, pe);
+    plan_child(a, P, r, 1, (2 * i + 1) * S + sh, P.off + lo, nn, (int32_t)(s_cb[i] + tnew_all + tnew), pb, pe);
     return;
   }
   // (2b) one child tile and one part tile per lane
@@ -1765,16 +1854,25 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
   };
   if (j < run_t) {
     const int32_t i = find(s_cb, j);
-    const DevNode& P = a.pn[parent(i)];
-    const uint32_t nn = P.n_new_local, lo = P.len - nn;
-    const uint32_t t0 = plan_ntiles(lo, a.tl, a.node_tiles);
+    const int32_t ai = parent(i) * S;
     uint32_t k = j - s_cb[i];
-    const int side = k >= t0 ? 1 : 0;
-    if (side) k -= t0;
-    const uint32_t off = side ? P.off + lo : P.off, len = side ? nn : lo;
+    // the child record holding slot k: old half's shards, then the new half's
+    int side = 0, sh = 0;
+    uint32_t off = 0, len = 0;
+    for (int v = 0; v < 2 * S; ++v) {
+      const DevNode& Q = a.pn[ai + (v % S)];
+      const uint32_t nn = Q.n_new_local, lo = Q.len - nn;
+      const uint32_t l = v < S ? lo : nn, nt = ntl(l);
+      side = v < S ? 0 : 1;
+      sh = v % S;
+      off = v < S ? Q.off : Q.off + lo;
+      len = l;
+      if (k < nt) break;
+      k -= nt;
+    }
     const uint32_t tln = plan_tile_len(len, a.tl, a.node_tiles);
     Tile* tt = a.ct + j;
-    tt->node = 2 * i + side;
+    tt->node = (2 * i + side) * S + sh;
     tt->start = off + k * tln;
     tt->end = off + min(len, (k + 1) * tln);
     tt->pad = 0;
@@ -1782,12 +1880,19 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
   }
   if (j < run_p) {
     const int32_t i = find(s_pb, j);
-    const int32_t ai = parent(i);
-    const DevNode& P = a.pn[ai];
-    const NodeResult& r = a.pres[ai];
+    const int32_t ai = parent(i) * S;
+    uint32_t k = j - s_pb[i];
+    int sh = 0;
+    for (; sh < S - 1; ++sh) {
+      const uint32_t nt = (uint32_t)(a.pn[ai + sh].tile_end - a.pn[ai + sh].tile_begin);
+      if (k < nt) break;
+      k -= nt;
+    }
+    const DevNode& P = a.pn[ai + sh];
+    const NodeResult& r = a.pres[ai + sh];
     PartTile* pt = a.cpt + j;
-    pt->tile = a.ptiles + P.tile_begin + (j - s_pb[i]);
-    pt->parent = a.pn + ai;
+    pt->tile = a.ptiles + P.tile_begin + k;
+    pt->parent = a.pn + ai + sh;
     int32_t thr0, sh0, thr1, sh1;
     plan_cut(r, 0, &thr0, &sh0);
     plan_cut(r, 1, &thr1, &sh1);
@@ -1795,8 +1900,8 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     pt->thr[1] = thr1;
     pt->shift[0] = sh0;
     pt->shift[1] = sh1;
-    pt->child[0] = 2 * i;
-    pt->child[1] = 2 * i + 1;
+    pt->child[0] = (2 * i) * S + sh;
+    pt->child[1] = (2 * i + 1) * S + sh;
   }
 }
 
@@ -2388,25 +2493,20 @@ void launch_kpass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) 
   else kpass_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a);
 }
 
-void launch_epilogue(int kind, const RoundArgs& a, int nnodes, bool from_totals,
-                     hipStream_t stream) {
+void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream) {
   if (nnodes <= 0) return;
   const dim3 g(nnodes), b(kEpiBlock);
-  if (from_totals) {
-    switch (kind) {
-      case PASS_INIT: epilogue_kernel<PASS_INIT, true><<<g, b, 0, stream>>>(a); break;
-      case PASS_SPLIT: epilogue_kernel<PASS_SPLIT, true><<<g, b, 0, stream>>>(a); break;
-      case PASS_KMEANS: epilogue_kernel<PASS_KMEANS, true><<<g, b, 0, stream>>>(a); break;
-      default: epilogue_kernel<PASS_KLAST, true><<<g, b, 0, stream>>>(a); break;
-    }
-    return;
+#define DQ_EPI(MODE)                                                                \
+  switch (kind) {                                                                   \
+    case PASS_INIT: epilogue_kernel<PASS_INIT, MODE><<<g, b, 0, stream>>>(a); break;   \
+    case PASS_SPLIT: epilogue_kernel<PASS_SPLIT, MODE><<<g, b, 0, stream>>>(a); break; \
+    case PASS_KMEANS: epilogue_kernel<PASS_KMEANS, MODE><<<g, b, 0, stream>>>(a); break; \
+    default: epilogue_kernel<PASS_KLAST, MODE><<<g, b, 0, stream>>>(a); break;          \
   }
-  switch (kind) {
-    case PASS_INIT: epilogue_kernel<PASS_INIT, false><<<g, b, 0, stream>>>(a); break;
-    case PASS_SPLIT: epilogue_kernel<PASS_SPLIT, false><<<g, b, 0, stream>>>(a); break;
-    case PASS_KMEANS: epilogue_kernel<PASS_KMEANS, false><<<g, b, 0, stream>>>(a); break;
-    default: epilogue_kernel<PASS_KLAST, false><<<g, b, 0, stream>>>(a); break;
-  }
+  if (a.tot_mode == TOT_ALLREDUCE) DQ_EPI(TOT_ALLREDUCE)
+  else if (a.tot_mode == TOT_NODE) DQ_EPI(TOT_NODE)
+  else DQ_EPI(TOT_OWN)
+#undef DQ_EPI
 }
 
 void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stream) {
@@ -2426,7 +2526,7 @@ void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream) {
 }
 
 void launch_plan(const PlanArgs& a, hipStream_t stream) {
-  const uint32_t nb_rec = (uint32_t)max(1, (a.np + kPlanBlock - 1) / kPlanBlock);
+  const uint32_t nb_rec = (uint32_t)max(1, (a.np * a.nshard + kPlanBlock - 1) / kPlanBlock);
   const uint32_t nb_tile = (max(a.tiles_cap, a.ptiles_cap) + kPlanBlock - 1) / kPlanBlock;
   plan_kernel<<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
 }

@@ -17,25 +17,90 @@ size_t color_table_scratch_bytes(uint32_t n);
 int launch_color_table(const uint32_t* px, uint32_t n, double norm, void* scratch, size_t scratch_bytes,
                        uint32_t* ucol, double* uw, uint32_t* h_nu, hipStream_t stream);
 
-// One node of a weighted round: its points are ids into (ucol, uw) at
-// src[off .. off+len) in point order; the split writes the old half to
-// dst[off ..), then the new half (both in point order).
-struct alignas(16) WNode {
-  const uint32_t* src;
-  uint32_t* dst;
+// ---------------------------------------------------------------------------
+// DivQuantCluster<false,*,true> (DivQuantCluster.cpp:133-1097) over a round of
+// nodes.  Every weighted statistic is a SEQUENTIAL FP64 fold s += x_i over a
+// node's points in point order (:73-85, :496-517, :719-770).  The passes
+// reproduce each fold exactly with the whole GPU (dq_weighted.hip, "exact
+// parallel fold"): tiles of kWTile points classify every summand by the
+// binade its running sum is certain to lie in, reduce RNE(x / ulp) as exact
+// integers per binade run, and a per-node chain applies runs and the rare
+// uncertain summands ("specials": binade crossings, ties) in order.
+constexpr uint32_t kWTile = 4096;   // points per tile (256 lanes x 16 consecutive points)
+constexpr int kWCh = 7;              // folds per pass: w*R, w*G, w*B, w, w*R^2, w*G^2, w*B^2
+enum WPass : int32_t { WP_INIT = 0, WP_SPLIT = 1, WP_KM = 2 };
+
+// One node of a weighted round: its record and the state carried across the
+// round's passes (written by the chain kernel).
+struct alignas(16) WState {
+  const uint32_t* src;        // point ids (into ucol / uw) at src[off .. off+len), point order
+  uint32_t* dst;              // the children's ids: old half at dst[off ..), then the new half
   uint32_t off, len;
+  int32_t tile_begin, tile_end;
+  int32_t root;               // 1: the init folds first (DivQuantClusterInitMeanAndVar, :36-123)
+  int32_t done;               // 0: active; 1: the split is final
   double tw;                  // weight[old_index] (root: 1.0, :329)
-  double tm[3], tv[3];        // mean / var of the node (root: from its init folds)
-  int32_t root, pad;
+  double tm[3], tv[3];        // node mean / var (root: from the init folds)
+  int32_t box_lo[3], box_hi[3];   // a box holding every point (R, G, B)
+  int32_t axis, iter;         // cut axis (:388-403); 2-means passes completed
+  double cut;                 // split: new iff cut < v_axis (:473)
+  double lhs, rr, rg, rb;     // 2-means: old iff lhs < rr*R + rg*G + rb*B (:683)
+  double prev[4];             // the last pass's sums and weight (fixed-point test)
+  double nw, ow, nm[3], om[3], nsq[3];
+  uint32_t n_new;             // new-side points of the final membership
+  int32_t done_it;            // 2-means iterations at finalisation
+  int32_t proven;             // final at the split: the cut is the 2-means fixed point
+  uint32_t seq_tiles;         // tiles whose folds ran one summand at a time (diagnostic)
 };
+
+struct alignas(16) WTile {
+  int32_t node;               // index into the round's WState array
+  uint32_t start, end;        // positions in the node's id buffer (absolute)
+  uint32_t pad;
+};
+
+// A tile's contribution to one fold, as the chain applies it: its summands
+// in tile order as at most kWSeg segments -- a run of binade e adding the
+// exact integer sum M of RNE(x / 2^(e-52)), or one special summand x added
+// in hardware.  nseg < 0: not describable (too many specials or binades):
+// the chain folds the tile's summands one at a time.
+constexpr int kWSeg = 32;
+constexpr int32_t kWSpecial = -100002;   // segment kind: a special summand (v = its bits)
+struct alignas(16) WSegment {
+  int32_t e;                  // binade of a run, or kWSpecial
+  int32_t pad;
+  int64_t v;                  // run: M; special: the summand's bits
+};
+struct alignas(16) WFold {
+  int32_t nseg, pad[3];
+  WSegment seg[kWSeg];
+};
+// The chain's quick form of a tile's fold: one run (e, M) and nothing else,
+// or kWComplex (read the WFold).
+constexpr int32_t kWComplex = -100000;
+struct alignas(16) WQuick {
+  int32_t e;
+  uint32_t cnt;               // (channel 0's record: the tile's taken points)
+  int64_t m;
+};
+
 struct WArgs {
-  const WNode* nodes;
+  WState* nodes;
+  const WTile* tiles;
   const uint32_t* ucol;
   const double* uw;
-  NodeResult* res;            // device, one per node
-  int32_t max_iters;
-  int32_t fixed_point;
+  double* tsum;               // [tile][8] the tile's sums (any order: an estimate)
+  double* tpre;               // [tile][8] exclusive node prefix of tsum
+  WFold* fold;                // [tile][kWCh]
+  WQuick* quick;              // [tile][kWCh]
+  uint32_t* pbase;            // [tile][2] partition bases (old, new) inside the node
+  uint32_t* active;           // device word: nodes not final after the pass
+  NodeResult* res;            // [node]
+  int32_t nn, ntiles, max_iters, fixed_point, it, pad;
 };
+void launch_wpass(int pass, const WArgs& a, hipStream_t stream);   // one statistics pass + epilogues
+void launch_wfinish(const WArgs& a, hipStream_t stream);           // partition + results
+
 // cut_bits + calc_color_table's decimated walk (DivQuantUni.cpp:28-100,
 // DivQuantMapColors.cpp:120-125): out[t] for t = a*nc + b (a < nr, b < nc) is
 // in[b*dec + a*dec*stride] with each channel shifted right by sr / sg / sb --
@@ -45,7 +110,5 @@ void launch_cut_gather(const uint32_t* in, uint32_t* out, uint32_t nr, uint32_t 
                        uint32_t stride, uint32_t sr, uint32_t sg, uint32_t sb, hipStream_t stream);
 // dst[i] = i (the root's point ids)
 void launch_iota(uint32_t* dst, uint32_t n, hipStream_t stream);
-// DivQuantCluster<false,*,true>'s split of every node (one workgroup each).
-void launch_wsplit(const WArgs& a, int nnodes, hipStream_t stream);
 
 }  // namespace dq

@@ -13,15 +13,27 @@
 //     unique colours with counts and first occurrences, a second sort by
 //     (hash bucket, first occurrence descending) -- the order the reference's
 //     prepended hash chains emit, weights norm * count (:184-195);
-//   * wsplit_kernel: ONE workgroup per node of a round runs the node's whole
-//     split -- (root) the init folds, the split pass, the local 2-means
-//     iterations to a fixed point or max_iters, the FP64 epilogue, and the
-//     stable partition of its points into its children's segments.  Per
-//     chunk of 256 points all lanes evaluate the decisions and the products
-//     (w * R, ...); lane 0 then adds them in point order (products of points
-//     not taken are +0.0, which leaves a non-negative sum bit-identical).
-//     The fold is sequential by definition; the nodes of a round run in
-//     parallel.
+//   * the node splits of a round, pass by pass over tiles of every node:
+//     the init folds (root), the split pass, the local 2-means passes to a
+//     fixed point or max_iters, each an EXACT PARALLEL FOLD (below), the
+//     reference's FP64 epilogue, then a stable partition of each node's
+//     points into its children's segments (point order kept).
+//
+// Exact parallel fold.  s_{i+1} = fl(s_i + x_i), s_0 = 0, x_i >= 0.  While
+// s_i and the exact s_i + x_i lie in one binade [2^e, 2^(e+1)), the sum is
+// rounded to the grid u = 2^(e-52) and s_{i+1} = s_i + u * RNE(x_i / u)
+// unless x_i / u is exactly halfway (a tie, decided by s_i's parity).  So a
+// run of summands inside one binade adds u * (an exact integer sum) -- in any
+// order, on any number of workgroups.  The binade each summand sees is
+// bounded from an estimate of the prefix (the tiles' sums scanned in any
+// order): |s_i - prefix_i| <= i * 2^-53 * s_i and the estimate's own error
+// is as small, so a summand whose interval [P(1-2^-20), (P+x)(1+2^-20)]
+// lies in one binade is a run member; the others (binade crossings, ties,
+// the first summand) are "specials" the chain adds in hardware, in order.
+// The chain (one wave per node) applies each tile's runs and specials in
+// sequence order, checks every run against the running sum's binade, and
+// folds a tile summand by summand whenever its description does not apply.
+// The result is the sequential fold's double, bit for bit.
 // MUST be compiled with -ffp-contract=off (the Makefile does).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -76,244 +88,639 @@ __global__ void ct_final_kernel(const uint32_t* __restrict__ sval, const uint32_
   }
 }
 
-// --- node splits ------------------------------------------------------------
-constexpr int kWBlock = 256;
-enum WMode : int { W_INIT = 0, W_SPLIT, W_KM, W_KMSQ, W_SQ };
 
-struct WDecision {
-  int32_t axis;
-  double cut;                 // split: new iff cut < v_axis (:473)
-  double lhs, rr, rg, rb;     // 2-means: old iff lhs < rr*R + rg*G + rb*B (:683)
+// --- weighted node splits: exact parallel folds --------------------------------
+constexpr int kWThreads = 256;
+constexpr int kWPer = (int)kWTile / kWThreads;   // consecutive points per lane
+constexpr int32_t kWNone = -100001;             // quick form: no summand changes the sum
+constexpr double kWMargin = 0x1p-20;            // relative bound on |s_i - prefix estimate|
+
+__device__ __forceinline__ bool w_take(int pass, const WState& st, uint32_t R, uint32_t G, uint32_t B) {
+  if (pass == WP_INIT) return true;
+  const double red = (double)R, green = (double)G, blue = (double)B;
+  if (pass == WP_SPLIT) return st.cut < (st.axis == 0 ? red : (st.axis == 1 ? green : blue));   // :473
+  return !(st.lhs < ((st.rr * red) + (st.rg * green) + (st.rb * blue)));                         // :683
+}
+
+// The reference's summands (:73-85, :496-517, :719-770): w*R (R converted),
+// w*(R*R) (the product in uint32), the weight itself.
+__device__ __forceinline__ double w_prod(int ch, uint32_t R, uint32_t G, uint32_t B, double w) {
+  switch (ch) {
+    case 0: return w * (double)R;
+    case 1: return w * (double)G;
+    case 2: return w * (double)B;
+    case 3: return w;
+    case 4: return w * (double)(R * R);
+    case 5: return w * (double)(G * G);
+    default: return w * (double)(B * B);
+  }
+}
+
+struct WPts {
+  uint32_t R[kWPer], G[kWPer], B[kWPer];
+  double w[kWPer];
+  uint32_t take;   // bit k: point k of this lane is a summand of the pass
 };
 
-// One pass over the node's points in point order.  Chains (lane 0, in
-// order): INIT: sum w*R, w*G, w*B, w*(R*R), w*(G*G), w*(B*B) over all points;
-// SPLIT / KM: w*R, w*G, w*B, w over the new side; KMSQ: those + w*(R*R)...;
-// SQ: w*(R*R), w*(G*G), w*(B*B) over the new side.  cnt: points taken.
-template <int MODE>
-__device__ void wpass(const WNode& nd, const uint32_t* __restrict__ ucol, const double* __restrict__ uw,
-                      const WDecision& d, double (*s_prod)[kWBlock], uint32_t* s_cnt, double acc[7],
-                      uint32_t* cnt) {
-  constexpr int NC = MODE == W_INIT ? 6 : (MODE == W_KMSQ ? 7 : (MODE == W_SQ ? 3 : 4));
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t base = 0; base < nd.len; base += kWBlock) {
-    const uint32_t i = base + tid;
-    double p[7] = {0, 0, 0, 0, 0, 0, 0};
-    bool take = false;
-    if (i < nd.len) {
-      const uint32_t id = nd.src[nd.off + i];
-      const uint32_t c = ucol[id];
-      const double w = uw[id];
-      const uint32_t R = (c >> 16) & 0xFF, G = (c >> 8) & 0xFF, B = c & 0xFF;
-      const double red = (double)R, green = (double)G, blue = (double)B;
-      if (MODE == W_INIT) take = true;
-      else if (MODE == W_SPLIT) take = d.cut < (d.axis == 0 ? red : (d.axis == 1 ? green : blue));
-      else take = !(d.lhs < ((d.rr * red) + (d.rg * green) + (d.rb * blue)));
-      if (take) {
-        if (MODE == W_INIT) {
-          p[0] = w * red; p[1] = w * green; p[2] = w * blue;
-          p[3] = w * (double)(R * R); p[4] = w * (double)(G * G); p[5] = w * (double)(B * B);
-        } else if (MODE == W_SQ) {
-          p[0] = w * (double)(R * R); p[1] = w * (double)(G * G); p[2] = w * (double)(B * B);
-        } else {
-          p[0] = w * red; p[1] = w * green; p[2] = w * blue; p[3] = w;
-          if (MODE == W_KMSQ) {
-            p[4] = w * (double)(R * R); p[5] = w * (double)(G * G); p[6] = w * (double)(B * B);
-          }
+__device__ __forceinline__ void w_load(const WArgs& a, const WState& st, const WTile& t, int pass, WPts& q) {
+  q.take = 0;
+  const uint32_t p0 = t.start + (uint32_t)kWPer * threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kWPer; ++k) {
+    const uint32_t p = p0 + (uint32_t)k;
+    q.R[k] = q.G[k] = q.B[k] = 0;
+    q.w[k] = 0.0;
+    if (p < t.end) {
+      const uint32_t id = st.src[p];
+      const uint32_t c = a.ucol[id];
+      q.w[k] = a.uw[id];
+      q.R[k] = (c >> 16) & 0xFF;
+      q.G[k] = (c >> 8) & 0xFF;
+      q.B[k] = c & 0xFF;
+      if (w_take(pass, st, q.R[k], q.G[k], q.B[k])) q.take |= 1u << k;
+    }
+  }
+}
+
+__device__ __forceinline__ double w_x(const WPts& q, int k, int ch) {
+  return ((q.take >> k) & 1u) ? w_prod(ch, q.R[k], q.G[k], q.B[k], q.w[k]) : 0.0;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Pass step 1: per tile, its summands' sums in any order (an estimate of the
+// fold, for the prefix) and the summand count.
+__global__ __launch_bounds__(kWThreads) void wk_tilesum(WArgs a, int pass) {
+  const WTile t = a.tiles[blockIdx.x];
+  const WState& st = a.nodes[t.node];
+  if (st.done) return;
+  WPts q;
+  w_load(a, st, t, pass, q);
+  __shared__ double red[kWThreads / 64][8];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int ch = 0; ch < kWCh; ++ch) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) v += w_x(q, k, ch);
+    v = wave_sum_f64(v);
+    if (lane == 0) red[wv][ch] = v;
+  }
+  const uint32_t c = (uint32_t)__popc(q.take);
+  uint32_t cs = c;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) cs += __shfl_xor(cs, o, 64);
+  if (lane == 0) red[wv][7] = (double)cs;
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    double v = 0.0;
+    for (int w = 0; w < kWThreads / 64; ++w) v += red[w][threadIdx.x];
+    a.tsum[(size_t)blockIdx.x * 8 + threadIdx.x] = v;
+  }
+}
+
+// Pass step 2: per node (one wave), the exclusive prefix of its tiles' sums.
+__global__ __launch_bounds__(64) void wk_prefix(WArgs a) {
+  const WState& st = a.nodes[blockIdx.x];
+  if (st.done) return;
+  const int lane = (int)threadIdx.x;
+  for (int ch = 0; ch < kWCh; ++ch) {
+    double run = 0.0;
+    for (int b = st.tile_begin; b < st.tile_end; b += 64) {
+      const int i = b + lane;
+      const double v = i < st.tile_end ? a.tsum[(size_t)i * 8 + ch] : 0.0;
+      double inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += u;
+      }
+      const double ex = lane == 0 ? 0.0 : __shfl_up(inc, 1, 64);
+      if (i < st.tile_end) a.tpre[(size_t)i * 8 + ch] = run + ex;
+      run += __shfl(inc, 63, 64);
+    }
+  }
+}
+
+// ilogb of a positive normal double (its binade's exponent)
+__device__ __forceinline__ int w_binade(double v) {
+  return (int)((__double_as_longlong(v) >> 52) & 0x7FF) - 1023;
+}
+
+// Pass step 3: per tile and fold, each summand's class (zero, run member of
+// binade e with integer RNE(x / 2^(e-52)), or special) from the prefix
+// estimate, then the tile's description: the ordered segments.  Run members
+// are binned by (specials before them, binade - e0) -- both never decrease
+// along the tile, so the bins in (sp, de) order, each special after the
+// bins of its group, are the tile's segments in sequence order.
+constexpr int kWSpMax = 16;    // specials per tile and fold described
+constexpr int kWDeMax = 16;    // binades per tile and fold described
+constexpr int kWBins = (kWSpMax + 1) * kWDeMax;
+__global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
+  const WTile t = a.tiles[blockIdx.x];
+  const WState& st = a.nodes[t.node];
+  if (st.done) return;
+  WPts q;
+  w_load(a, st, t, pass, q);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ double s_wt[kWThreads / 64];
+  __shared__ int s_i[kWThreads / 64][2];
+  __shared__ unsigned long long s_bins[kWBins];
+  __shared__ double s_sp[kWSpMax];
+  __shared__ int s_over;
+  __shared__ int s_rank[kWBins + 1];
+  for (int ch = 0; ch < kWCh; ++ch) {
+    double x[kWPer];
+    double T = 0.0;
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) {
+      x[k] = w_x(q, k, ch);
+      T += x[k];
+    }
+    // block exclusive scan of the lanes' totals (an estimate: any rounding)
+    double inc = T;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const double u = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += u;
+    }
+    if (lane == 63) s_wt[wv] = inc;
+    for (int b = (int)threadIdx.x; b < kWBins; b += kWThreads) s_bins[b] = 0ull;
+    if (threadIdx.x == 0) s_over = 0;
+    __syncthreads();
+    double P = a.tpre[(size_t)blockIdx.x * 8 + ch];
+    for (uint32_t w = 0; w < wv; ++w) P += s_wt[w];
+    P += lane == 0 ? 0.0 : __shfl_up(inc, 1, 64);
+    // classes
+    int e[kWPer];
+    int64_t m[kWPer];
+    uint32_t spm = 0;   // bit k: special
+    int emin = 0x7FFFFFFF;
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) {
+      e[k] = kWNone;
+      m[k] = 0;
+      if (x[k] != 0.0) {
+        const double lo = P * (1.0 - kWMargin), hi = (P + x[k]) * (1.0 + kWMargin);
+        bool special = !(lo > 0.0);
+        int el = 0;
+        if (!special) {
+          el = w_binade(lo);
+          special = el != w_binade(hi);
+        }
+        if (!special) {
+          const double tt = ldexp(x[k], 52 - el);   // exact (x < 2^(el+1))
+          const double fl = floor(tt), fr = tt - fl;
+          special = fr == 0.5;                      // a tie: the parity of s decides
+          m[k] = (int64_t)fl + (fr > 0.5 ? 1 : 0);
+          e[k] = el;
+          emin = min(emin, el);
+        }
+        if (special) spm |= 1u << k;
+      }
+      P += x[k];
+    }
+    // specials before each lane (exclusive scan of counts), the tile's e0
+    const int nsl = __popc(spm);
+    int si = nsl;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(si, o, 64);
+      if (lane >= (uint32_t)o) si += u;
+    }
+    int wmin = emin;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) wmin = min(wmin, __shfl_xor(wmin, o, 64));
+    if (lane == 63) s_i[wv][0] = si;
+    if (lane == 0) s_i[wv][1] = wmin;
+    __syncthreads();
+    int spb = si - nsl, e0 = 0x7FFFFFFF, nsp = 0;
+    for (int w = 0; w < kWThreads / 64; ++w) {
+      if ((uint32_t)w < wv) spb += s_i[w][0];
+      nsp += s_i[w][0];
+      e0 = min(e0, s_i[w][1]);
+    }
+    bool over = nsp > kWSpMax;
+#pragma unroll
+    for (int k = 0; k < kWPer; ++k) {
+      if ((spm >> k) & 1u) {
+        if (spb < kWSpMax) s_sp[spb] = x[k];
+        ++spb;
+      } else if (e[k] != kWNone) {
+        const int b = e[k] - e0;
+        if (spb > kWSpMax || b >= kWDeMax) over = true;
+        else if (m[k] != 0) atomicAdd(&s_bins[spb * kWDeMax + b], (unsigned long long)m[k]);
+      }
+    }
+    if (over) s_over = 1;   // (benign race: every writer stores 1)
+    __syncthreads();
+    // wave 0: the bins' ranks among the nonzero ones (flattened (sp, de) order)
+    if (wv == 0) {
+      int run = 0;
+      for (int b0 = 0; b0 < kWBins; b0 += 64) {
+        const int b = b0 + (int)lane;
+        const bool nz = b < kWBins && s_bins[b] != 0ull;
+        const uint64_t bm = __ballot(nz);
+        if (b < kWBins) s_rank[b] = run + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        run += (int)__popcll(bm);
+      }
+      if (lane == 0) s_rank[kWBins] = run;
+    }
+    __syncthreads();
+    const int nbin = s_rank[kWBins];
+    const int nseg = (s_over || nsp > kWSpMax || nbin + nsp > kWSeg) ? -1 : nbin + nsp;
+    WFold& f = a.fold[(size_t)blockIdx.x * kWCh + ch];
+    if (nseg >= 0) {
+      // run bin (sp, de) at rank + sp; special sp after its group's bins
+      for (int b = (int)threadIdx.x; b < kWBins; b += kWThreads) {
+        const unsigned long long v = s_bins[b];
+        if (v) {
+          const int sp = b / kWDeMax;
+          WSegment& g = f.seg[s_rank[b] + sp];
+          g.e = e0 + (b - sp * kWDeMax);
+          g.pad = 0;
+          g.v = (int64_t)v;
         }
       }
-    }
-#pragma unroll
-    for (int k = 0; k < NC; ++k) s_prod[k][tid] = p[k];
-    const uint64_t m = __ballot(take);
-    if ((tid & 63) == 0) s_cnt[tid >> 6] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (tid == 0) {
-      const uint32_t nj = min((uint32_t)kWBlock, nd.len - base);
-      for (uint32_t j = 0; j < nj; ++j) {
-#pragma unroll
-        for (int k = 0; k < NC; ++k) acc[k] += s_prod[k][j];
+      if ((int)threadIdx.x < nsp) {
+        const int sp = (int)threadIdx.x;
+        WSegment& g = f.seg[s_rank[(sp + 1) * kWDeMax] + sp];
+        g.e = kWSpecial;
+        g.pad = 0;
+        g.v = __double_as_longlong(s_sp[sp]);
       }
-      *cnt += s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
     }
-    __syncthreads();
+    if (threadIdx.x == 0) {
+      f.nseg = nseg;
+      WQuick& qk = a.quick[(size_t)blockIdx.x * kWCh + ch];
+      if (nseg == 0) {
+        qk.e = kWNone;
+        qk.m = 0;
+      } else if (nseg == 1 && nsp == 0) {
+        int bz = 0;
+        while (s_bins[bz] == 0ull) ++bz;
+        qk.e = e0 + bz;
+        qk.m = (int64_t)s_bins[bz];
+      } else {
+        qk.e = kWComplex;
+        qk.m = 0;
+      }
+    }
+    __syncthreads();   // (shared arrays reused by the next fold)
+  }
+  if (threadIdx.x == 0) a.quick[(size_t)blockIdx.x * kWCh].cnt = (uint32_t)a.tsum[(size_t)blockIdx.x * 8 + 7];
+}
+
+// s += u_e * M for a run of binade e; false if s is not in binade e or the
+// run would leave it (the description does not apply: fold the summands).
+__device__ __forceinline__ bool w_apply_run(double& s, int e, int64_t M) {
+  if (!(s > 0.0) || w_binade(s) != e) return false;
+  const int64_t si = (int64_t)ldexp(s, 52 - e) + M;   // (s / u exact: s is on the grid)
+  if (si > (1ll << 53)) return false;
+  s = ldexp((double)si, e - 52);                      // exact (si <= 2^53)
+  return true;
+}
+
+// Every lane of the wave holds the same s (uniform); the tile's summands of
+// fold ch added one at a time, in order (64 per load).
+__device__ void w_fold_tile_seq(const WArgs& a, const WState& st, const WTile& t, int pass, int ch, double& s) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t b = t.start; b < t.end; b += 64) {
+    const uint32_t p = b + lane;
+    double x = 0.0;
+    if (p < t.end) {
+      const uint32_t id = st.src[p];
+      const uint32_t c = a.ucol[id];
+      const uint32_t R = (c >> 16) & 0xFF, G = (c >> 8) & 0xFF, B = c & 0xFF;
+      if (w_take(pass, st, R, G, B)) x = w_prod(ch, R, G, B, a.uw[id]);
+    }
+    const uint32_t n = min(64u, t.end - b);
+    for (uint32_t j = 0; j < n; ++j) s += __shfl(x, (int)j, 64);
   }
 }
 
-__device__ void w_decision_from_means(const double om[3], const double nm[3], WDecision* d) {
-  d->lhs = 0.5 * (om[0] * om[0] - nm[0] * nm[0] + om[1] * om[1] - nm[1] * nm[1] + om[2] * om[2] -
-                  nm[2] * nm[2]);                                        // :616-619
-  d->rr = om[0] - nm[0];
-  d->rg = om[1] - nm[1];
-  d->rb = om[2] - nm[2];
+// A tile's description applied to s (fold ch); sequential when it does not apply.
+__device__ void w_apply_tile(const WArgs& a, const WState& st, int ti, int pass, int ch, double& s) {
+  const WFold& f = a.fold[(size_t)ti * kWCh + ch];
+  bool ok = f.nseg >= 0;
+  double v = s;
+  for (int i = 0; ok && i < f.nseg; ++i) {
+    const WSegment g = f.seg[i];
+    if (g.e == kWSpecial) v += __longlong_as_double(g.v);
+    else ok = w_apply_run(v, g.e, g.v);
+  }
+  if (ok) {
+    s = v;
+    return;
+  }
+  const WTile t = a.tiles[ti];
+  if ((threadIdx.x & 63) == 0) atomicAdd((uint32_t*)&a.nodes[t.node].seq_tiles, 1u);
+  w_fold_tile_seq(a, st, t, pass, ch, s);
 }
 
-}  // namespace
+__device__ void w_cut(WState& w, const double tm[3], const double tv[3]) {   // :388-403
+  double maxv = tv[0], cut = tm[0];
+  int axis = 0;
+  if (maxv < tv[1]) { maxv = tv[1]; axis = 1; cut = tm[1]; }
+  if (maxv < tv[2]) { axis = 2; cut = tm[2]; }
+  w.axis = axis;
+  w.cut = cut;
+}
 
-__global__ __launch_bounds__(kWBlock) void wsplit_kernel(WArgs a) {
-  const WNode nd = a.nodes[blockIdx.x];
-  __shared__ double s_prod[7][kWBlock];
-  __shared__ uint32_t s_cnt[kWBlock / 64];
-  __shared__ WDecision s_dec;
-  __shared__ uint32_t s_flag;
-  __shared__ uint32_t s_wc[kWBlock / 64][2];
-  const uint32_t tid = threadIdx.x;
-  // lane 0's state
-  double tm[3], tv[3], om[3], nm[3], nw = 0.0, ow = 0.0, nsq[3] = {0, 0, 0};
-  double prev[4] = {0, 0, 0, 0};
-  uint32_t n_new = 0;
-  const double tw = nd.tw;
-  int done_it = -1;
-  // (root) DivQuantClusterInitMeanAndVar, weighted (:49-104)
-  if (nd.root) {
-    double acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    uint32_t cnt = 0;
-    wpass<W_INIT>(nd, a.ucol, a.uw, s_dec, s_prod, s_cnt, acc, &cnt);
-    if (tid == 0)
-      for (int c = 0; c < 3; ++c) {
-        tm[c] = acc[c];
-        tv[c] = acc[3 + c];
-        tv[c] -= tm[c] * tm[c];   // var -= SQR(mean) (:99-101)
+__device__ int32_t w_threshold(double cut) {   // cut < v <=> v >= thr (integer v in [0, 255])
+  if (!(cut == cut)) return 256;
+  if (cut < 0.0) return 0;
+  if (cut >= 255.0) return 256;
+  return (int32_t)floor(cut) + 1;
+}
+
+// The first 2-means decision after the split keeps every point of the node's
+// box on its side of the cut (dq_kernels.hip cut_is_fixed_point, the same
+// corner test and margin): the first 2-means pass then folds exactly the
+// split's summands and is a fixed point.
+__device__ bool w_cut_is_fixed_point(const WState& w) {
+  const double M = (fabs(w.rr) + fabs(w.rg) + fabs(w.rb)) * 255.0 + fabs(w.lhs);
+  if (!(M > 1e-30 && M < 1e30)) return false;
+  const double mg = 1e-12 * M;
+  const double c[3] = {w.rr, w.rg, w.rb};
+  const int thr = w_threshold(w.cut);
+  for (int side = 0; side < 2; ++side) {
+    int lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) { lo[k] = w.box_lo[k]; hi[k] = w.box_hi[k]; }
+    if (side) lo[w.axis] = max(lo[w.axis], thr);
+    else hi[w.axis] = min(hi[w.axis], thr - 1);
+    if (lo[w.axis] > hi[w.axis]) continue;
+    double ext = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      const double x = c[k] * (double)lo[k], y = c[k] * (double)hi[k];
+      ext += side ? fmax(x, y) : fmin(x, y);
+    }
+    if (side ? !(ext <= w.lhs - mg) : !(ext >= w.lhs + mg)) return false;
+  }
+  return true;
+}
+
+__device__ void w_decision(WState& w) {   // :616-623
+  w.lhs = 0.5 * (w.om[0] * w.om[0] - w.nm[0] * w.nm[0] + w.om[1] * w.om[1] - w.nm[1] * w.nm[1] +
+                 w.om[2] * w.om[2] - w.nm[2] * w.nm[2]);
+  w.rr = w.om[0] - w.nm[0];
+  w.rg = w.om[1] - w.nm[1];
+  w.rb = w.om[2] - w.nm[2];
+}
+
+// Pass step 4: per node (one wave), the folds in sequence order -- tiles in
+// chunks of 64 (one per lane): consecutive run tiles of one binade applied as
+// one integer sum, the others one by one -- then the reference's FP64
+// epilogue of the pass (lane-uniform; lane 0 stores).
+__global__ __launch_bounds__(64) void wk_chain(WArgs a, int pass) {
+  WState& st = a.nodes[blockIdx.x];
+  if (st.done) return;
+  const uint32_t lane = threadIdx.x;
+  double acc[kWCh];
+  uint32_t cnt = 0;
+  for (int ch = 0; ch < kWCh; ++ch) acc[ch] = 0.0;
+  for (int b = st.tile_begin; b < st.tile_end; b += 64) {
+    const int ti = b + (int)lane;
+    const bool have = ti < st.tile_end;
+    const int nt = min(64, st.tile_end - b);
+    uint32_t c = have ? a.quick[(size_t)ti * kWCh].cnt : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+    cnt += c;
+    WQuick q7[kWCh];   // (every fold's record of the lane's tile in flight together)
+#pragma unroll
+    for (int ch = 0; ch < kWCh; ++ch) {
+      q7[ch].e = kWNone;
+      q7[ch].m = 0;
+      if (have) q7[ch] = a.quick[(size_t)ti * kWCh + ch];
+    }
+    for (int ch = 0; ch < kWCh; ++ch) {
+      const WQuick qk = q7[ch];
+      double s = acc[ch];
+      // walk: [pos, next complex) by binade groups, then the complex tile
+      const uint64_t cm = __ballot(have && qk.e == kWComplex);
+      int pos = 0;
+      while (pos < nt) {
+        const uint64_t rest = cm & (pos >= 64 ? 0ull : (~0ull << pos));
+        const int nc = rest ? (int)__builtin_ctzll(rest) : nt;
+        // quick tiles [pos, nc): groups of equal binade, ascending -- sequence
+        // order when the binades never decrease along the tiles (they do not
+        // when every summand is classified right); otherwise tile by tile
+        const bool run = have && (int)lane >= pos && (int)lane < nc && qk.e != kWNone && qk.e != kWComplex;
+        uint64_t live = __ballot(run);
+        int pmax = run ? qk.e : -0x7FFFFFFF;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int u = __shfl_up(pmax, o, 64);
+          if (lane >= (uint32_t)o) pmax = max(pmax, u);
+        }
+        const int before = lane == 0 ? -0x7FFFFFFF : __shfl_up(pmax, 1, 64);
+        if (__ballot(run && qk.e < before)) {
+          for (int j = pos; j < nc; ++j) {
+            const int ej = __shfl(qk.e, j, 64);
+            const int64_t mj = __shfl(qk.m, j, 64);
+            if (ej != kWNone && !w_apply_run(s, ej, mj)) w_apply_tile(a, st, b + j, pass, ch, s);
+          }
+          live = 0;
+        }
+        while (live) {
+          int emin = ((live >> lane) & 1ull) ? qk.e : 0x7FFFFFFF;
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) emin = min(emin, __shfl_xor(emin, o, 64));
+          const bool mine = ((live >> lane) & 1ull) && qk.e == emin;
+          const uint64_t grp = __ballot(mine);
+          int64_t M = mine ? qk.m : 0;
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) M += __shfl_xor(M, o, 64);
+          if (!w_apply_run(s, emin, M)) {   // tile by tile (each one's own check)
+            for (uint64_t g = grp; g; g &= g - 1) {
+              const int j = (int)__builtin_ctzll(g);
+              const int64_t mj = __shfl(qk.m, j, 64);
+              if (!w_apply_run(s, emin, mj)) w_apply_tile(a, st, b + j, pass, ch, s);
+            }
+          }
+          live &= ~grp;
+        }
+        if (nc < nt) w_apply_tile(a, st, b + nc, pass, ch, s);
+        pos = nc + 1;
       }
-  } else if (tid == 0) {
-    for (int c = 0; c < 3; ++c) { tm[c] = nd.tm[c]; tv[c] = nd.tv[c]; }
+      acc[ch] = s;
+    }
   }
-  // cut axis / position (:388-403)
-  if (tid == 0) {
-    double maxv = tv[0], cut = tm[0];
-    int axis = 0;
-    if (maxv < tv[1]) { maxv = tv[1]; axis = 1; cut = tm[1]; }
-    if (maxv < tv[2]) { axis = 2; cut = tm[2]; }
-    s_dec.axis = axis;
-    s_dec.cut = cut;
+  // the pass's epilogue (every lane computes the same values; lane 0 stores)
+  WState w = st;
+  if (pass == WP_INIT) {   // DivQuantClusterInitMeanAndVar (:90-104), weighted
+    double tm[3], tv[3];
+    for (int c2 = 0; c2 < 3; ++c2) {
+      tm[c2] = acc[c2];
+      tv[c2] = acc[4 + c2];
+      tv[c2] -= tm[c2] * tm[c2];
+      w.tm[c2] = tm[c2];
+      w.tv[c2] = tv[c2];
+    }
+    w_cut(w, tm, tv);
+  } else if (pass == WP_SPLIT) {   // :561-598 (weighted: no data_weight scaling)
+    w.nw = acc[3];
+    w.ow = w.tw - w.nw;
+    for (int c2 = 0; c2 < 3; ++c2) {
+      w.nm[c2] = acc[c2];
+      w.nm[c2] /= w.nw;
+    }
+    for (int c2 = 0; c2 < 3; ++c2) w.om[c2] = (w.tw * w.tm[c2] - w.nw * w.nm[c2]) / w.ow;
+    for (int c2 = 0; c2 < 4; ++c2) w.prev[c2] = acc[c2];
+    w_decision(w);
+    w.n_new = cnt;
+    w.iter = 0;
+    if (a.fixed_point && cnt != 0 && w.ow > 0.0 && w_cut_is_fixed_point(w)) {
+      // the first 2-means pass would fold the split's summands again: the
+      // fixed point, with the split's squares (same membership, same order)
+      for (int c2 = 0; c2 < 3; ++c2) w.nsq[c2] = acc[4 + c2];
+      w.iter = 1;
+      w.done_it = 1;
+      w.proven = 1;
+      w.done = 1;
+    }
+  } else {   // 2-means pass a.it (:613-811)
+    const bool last = a.it == a.max_iters - 1;
+    const bool fixed = a.fixed_point && !last &&
+                       __double_as_longlong(acc[0]) == __double_as_longlong(w.prev[0]) &&
+                       __double_as_longlong(acc[1]) == __double_as_longlong(w.prev[1]) &&
+                       __double_as_longlong(acc[2]) == __double_as_longlong(w.prev[2]) &&
+                       __double_as_longlong(acc[3]) == __double_as_longlong(w.prev[3]);
+    w.nw = acc[3];
+    w.n_new = cnt;
+    for (int c2 = 0; c2 < 3; ++c2) {
+      w.nm[c2] = acc[c2];
+      w.nm[c2] /= w.nw;                                                  // :800-802
+    }
+    w.ow = w.tw - w.nw;                                                  // :805
+    for (int c2 = 0; c2 < 3; ++c2) w.om[c2] = (w.tw * w.tm[c2] - w.nw * w.nm[c2]) / w.ow;   // :808-810
+    for (int c2 = 0; c2 < 3; ++c2) w.nsq[c2] = acc[4 + c2];
+    for (int c2 = 0; c2 < 4; ++c2) w.prev[c2] = acc[c2];
+    w.iter = a.it + 1;
+    if (last || fixed) {
+      w.done_it = a.it + 1;
+      w.done = 1;
+    } else {
+      w_decision(w);   // the next pass's decision
+    }
   }
+  if (lane == 0) {
+    st = w;
+    if (!w.done && pass != WP_INIT) atomicAdd(a.active, 1u);
+  }
+}
+
+// Round end, step 1: per tile, the new-side count of the final membership.
+__global__ __launch_bounds__(kWThreads) void wk_part_count(WArgs a) {
+  const WTile t = a.tiles[blockIdx.x];
+  const WState& st = a.nodes[t.node];
+  WPts q;
+  w_load(a, st, t, WP_KM, q);
+  uint32_t c = (uint32_t)__popc(q.take);
+  __shared__ uint32_t red[kWThreads / 64];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
   __syncthreads();
-  {   // split pass (:438-559), then :561-598
-    double acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    uint32_t cnt = 0;
-    const WDecision d = s_dec;
-    wpass<W_SPLIT>(nd, a.ucol, a.uw, d, s_prod, s_cnt, acc, &cnt);
-    if (tid == 0) {
-      nw = acc[3];
-      ow = tw - nw;
-      for (int c = 0; c < 3; ++c) {
-        nm[c] = acc[c];
-        nm[c] /= nw;
-      }
-      for (int c = 0; c < 3; ++c) om[c] = (tw * tm[c] - nw * nm[c]) / ow;
-      prev[0] = acc[0]; prev[1] = acc[1]; prev[2] = acc[2]; prev[3] = acc[3];
-      w_decision_from_means(om, nm, &s_dec);
-    }
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t v = 0;
+    for (int w = 0; w < kWThreads / 64; ++w) v += red[w];
+    a.pbase[(size_t)blockIdx.x * 2 + 1] = v;
   }
-  // local 2-means (:613-811), to a fixed point or max_iters
-  for (int it = 0; it < a.max_iters; ++it) {
-    const bool last = it == a.max_iters - 1;
-    const WDecision d = s_dec;
-    double acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    uint32_t cnt = 0;
-    if (last) wpass<W_KMSQ>(nd, a.ucol, a.uw, d, s_prod, s_cnt, acc, &cnt);
-    else wpass<W_KM>(nd, a.ucol, a.uw, d, s_prod, s_cnt, acc, &cnt);
-    if (tid == 0) {
-      // the state (sums, weight) equal to the previous pass's: every later
-      // iteration recomputes the same means and decision (a fixed point)
-      const bool fixed = a.fixed_point && !last &&
-                         __double_as_longlong(acc[0]) == __double_as_longlong(prev[0]) &&
-                         __double_as_longlong(acc[1]) == __double_as_longlong(prev[1]) &&
-                         __double_as_longlong(acc[2]) == __double_as_longlong(prev[2]) &&
-                         __double_as_longlong(acc[3]) == __double_as_longlong(prev[3]);
-      nw = acc[3];
-      n_new = cnt;
-      for (int c = 0; c < 3; ++c) {
-        nm[c] = acc[c];
-        nm[c] /= nw;                                             // :800-802
-      }
-      ow = tw - nw;                                              // :805
-      for (int c = 0; c < 3; ++c) om[c] = (tw * tm[c] - nw * nm[c]) / ow;   // :808-810
-      for (int c = 0; c < 3; ++c) nsq[c] = acc[4 + c];
-      for (int c = 0; c < 4; ++c) prev[c] = acc[c];
-      s_flag = last ? 1u : (fixed ? 2u : 0u);
-      if (!last && !fixed) w_decision_from_means(om, nm, &s_dec);   // next pass's decision
-      if (last || fixed) done_it = it + 1;
+}
+
+// Step 2: per node (one wave), the tiles' old / new bases; the node's results
+// (:820-871) into res.
+__global__ __launch_bounds__(64) void wk_part_scan(WArgs a) {
+  const WState& st = a.nodes[blockIdx.x];
+  const int lane = (int)threadIdx.x;
+  uint32_t run_o = 0, run_n = 0;
+  for (int b = st.tile_begin; b < st.tile_end; b += 64) {
+    const int i = b + lane;
+    uint32_t nw = 0, ol = 0;
+    if (i < st.tile_end) {
+      const WTile t = a.tiles[i];
+      nw = a.pbase[(size_t)i * 2 + 1];
+      ol = (t.end - t.start) - nw;
     }
-    __syncthreads();
-    const uint32_t fl = s_flag;
-    __syncthreads();
-    if (fl == 2u) {   // fixed point: the sums of squares of this membership (decision d)
-      double sq[7] = {0, 0, 0, 0, 0, 0, 0};
-      uint32_t c2 = 0;
-      wpass<W_SQ>(nd, a.ucol, a.uw, d, s_prod, s_cnt, sq, &c2);
-      if (tid == 0)
-        for (int c = 0; c < 3; ++c) nsq[c] = sq[c];
+    uint32_t io = ol, in = nw;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(io, o, 64), v = __shfl_up(in, o, 64);
+      if (lane >= o) { io += u; in += v; }
     }
-    if (fl != 0u) break;
+    if (i < st.tile_end) {
+      a.pbase[(size_t)i * 2] = run_o + io - ol;
+      a.pbase[(size_t)i * 2 + 1] = run_n + in - nw;
+    }
+    run_o += __shfl(io, 63, 64);
+    run_n += __shfl(in, 63, 64);
   }
-  // results (:820-871)
-  if (tid == 0) {
+  if (lane == 0) {
     NodeResult r;
     double nv[3], ov[3];
-    for (int c = 0; c < 3; ++c) nv[c] = nsq[c] / nw - nm[c] * nm[c];   // :836-838
+    for (int c = 0; c < 3; ++c) nv[c] = st.nsq[c] / st.nw - st.nm[c] * st.nm[c];   // :836-838
     for (int c = 0; c < 3; ++c) {
-      const double dn = nm[c] - tm[c];
-      const double dox = om[c] - tm[c];
-      ov[c] = ((tw * tv[c] - nw * (nv[c] + dn * dn)) / ow) - dox * dox;   // :845-855
+      const double dn = st.nm[c] - st.tm[c];
+      const double dox = st.om[c] - st.tm[c];
+      ov[c] = ((st.tw * st.tv[c] - st.nw * (nv[c] + dn * dn)) / st.ow) - dox * dox;   // :845-855
     }
     for (int c = 0; c < 3; ++c) {
-      r.om[c] = om[c]; r.nm[c] = nm[c]; r.nv[c] = nv[c]; r.ov[c] = ov[c];
-      r.tm[c] = tm[c]; r.tv[c] = tv[c];
+      r.om[c] = st.om[c]; r.nm[c] = st.nm[c]; r.nv[c] = nv[c]; r.ov[c] = ov[c];
+      r.tm[c] = st.tm[c]; r.tv[c] = st.tv[c];
     }
-    r.nw = nw;
-    r.ow = ow;
-    r.tse_old = ow * (ov[0] + ov[1] + ov[2]);   // :870-871
-    r.tse_new = nw * (nv[0] + nv[1] + nv[2]);
-    r.n_new = n_new;
-    r.n_new_local = n_new;
-    r.done_it = done_it;
-    r.proven = 0;
-    r.pad = 0;
-    r.len_local = nd.len;
+    r.nw = st.nw;
+    r.ow = st.ow;
+    r.tse_old = st.ow * (ov[0] + ov[1] + ov[2]);   // :870-871
+    r.tse_new = st.nw * (nv[0] + nv[1] + nv[2]);
+    r.n_new = st.n_new;
+    r.n_new_local = run_n;
+    r.done_it = st.done_it;
+    r.proven = st.proven;
+    r.pad = (int32_t)st.seq_tiles;
+    r.len_local = st.len;
     r.tag = 0;
     a.res[blockIdx.x] = r;
   }
-  // stable partition of the points by the final decision: old half first
-  // (point order kept in both halves: the reference's gather visits
-  // member[] in index order, :894-1026)
+}
+
+// Step 3: per tile, the stable partition of its ids by the final decision
+// (old half first; point order kept in both halves, as the reference's
+// gather by ascending index, :894-1026).
+__global__ __launch_bounds__(kWThreads) void wk_part_scatter(WArgs a) {
+  const WTile t = a.tiles[blockIdx.x];
+  const WState& st = a.nodes[t.node];
+  WPts q;
+  w_load(a, st, t, WP_KM, q);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t p0 = t.start + (uint32_t)kWPer * threadIdx.x;
+  const uint32_t nv = p0 < t.end ? min((uint32_t)kWPer, t.end - p0) : 0u;
+  const uint32_t nn = (uint32_t)__popc(q.take), no = nv - nn;
+  uint32_t io = no, in = nn;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(io, o, 64), v = __shfl_up(in, o, 64);
+    if (lane >= (uint32_t)o) { io += u; in += v; }
+  }
+  __shared__ uint32_t s_w[kWThreads / 64][2];
+  if (lane == 63) { s_w[wv][0] = io; s_w[wv][1] = in; }
   __syncthreads();
-  const WDecision d = s_dec;
-  __shared__ uint32_t s_nnew;
-  if (tid == 0) s_nnew = n_new;
-  __syncthreads();
-  const uint32_t n_old = nd.len - s_nnew;
-  uint32_t run_o = 0, run_n = 0;
-  const uint32_t lane = tid & 63, wv = tid >> 6;
-  for (uint32_t base = 0; base < nd.len; base += kWBlock) {
-    const uint32_t i = base + tid;
-    const bool valid = i < nd.len;
-    uint32_t id = 0;
-    bool nw_side = false;
-    if (valid) {
-      id = nd.src[nd.off + i];
-      const uint32_t c = a.ucol[id];
-      const double red = (double)((c >> 16) & 0xFF), green = (double)((c >> 8) & 0xFF), blue = (double)(c & 0xFF);
-      nw_side = !(d.lhs < ((d.rr * red) + (d.rg * green) + (d.rb * blue)));
-    }
-    const uint64_t mo = __ballot(valid && !nw_side), mn = __ballot(valid && nw_side);
-    if (lane == 0) {
-      s_wc[wv][0] = (uint32_t)__popcll(mo);
-      s_wc[wv][1] = (uint32_t)__popcll(mn);
-    }
-    __syncthreads();
-    uint32_t bo = run_o, bn = run_n;
-    for (uint32_t w = 0; w < wv; ++w) { bo += s_wc[w][0]; bn += s_wc[w][1]; }
-    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    if (valid) {
-      if (nw_side) nd.dst[nd.off + n_old + bn + (uint32_t)__popcll(mn & below)] = id;
-      else nd.dst[nd.off + bo + (uint32_t)__popcll(mo & below)] = id;
-    }
-    for (uint32_t w = 0; w < kWBlock / 64; ++w) { run_o += s_wc[w][0]; run_n += s_wc[w][1]; }
-    __syncthreads();
+  uint32_t bo = a.pbase[(size_t)blockIdx.x * 2] + io - no, bn = a.pbase[(size_t)blockIdx.x * 2 + 1] + in - nn;
+  for (uint32_t w = 0; w < wv; ++w) { bo += s_w[w][0]; bn += s_w[w][1]; }
+  const uint32_t n_old = st.len - st.n_new;
+  for (uint32_t k = 0; k < nv; ++k) {
+    const uint32_t id = st.src[p0 + k];
+    if ((q.take >> k) & 1u) st.dst[st.off + n_old + bn++] = id;
+    else st.dst[st.off + bo++] = id;
   }
 }
+}  // namespace
 
 // --- launchers ----------------------------------------------------------------
 static inline uint32_t grid_for(uint32_t n) {
@@ -407,9 +814,20 @@ void launch_iota(uint32_t* dst, uint32_t n, hipStream_t stream) {
   iota_kernel<<<dim3(grid_for(n)), dim3(256), 0, stream>>>(dst, n);
 }
 
-void launch_wsplit(const WArgs& a, int nnodes, hipStream_t stream) {
-  if (nnodes <= 0) return;
-  wsplit_kernel<<<dim3(nnodes), dim3(kWBlock), 0, stream>>>(a);
+
+void launch_wpass(int pass, const WArgs& a, hipStream_t stream) {
+  if (a.ntiles <= 0 || a.nn <= 0) return;
+  wk_tilesum<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
+  wk_prefix<<<dim3(a.nn), dim3(64), 0, stream>>>(a);
+  wk_classify<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
+  wk_chain<<<dim3(a.nn), dim3(64), 0, stream>>>(a, pass);
+}
+
+void launch_wfinish(const WArgs& a, hipStream_t stream) {
+  if (a.ntiles <= 0 || a.nn <= 0) return;
+  wk_part_count<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a);
+  wk_part_scan<<<dim3(a.nn), dim3(64), 0, stream>>>(a);
+  wk_part_scatter<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a);
 }
 
 }  // namespace dq

@@ -208,6 +208,9 @@ uint64_t dq_hip_last_points_swept(int device);
 /* Points the last run would have swept without fixed-point finalisation
  * (every split: split pass + max_iters 2-means passes, as the reference). */
 uint64_t dq_hip_last_points_full(int device);
+/* Weighted path: tiles of the last run whose folds ran one summand at a time
+ * (the exact parallel fold's fallback). */
+uint64_t dq_hip_last_seq_tiles(int device);
 /* Fixed-point finalisation (default on; DQ_HIP_FULL_ITERS=1 turns the default
  * off).  A split whose 2-means pass reproduces the previous pass's exact
  * integer sums is final: the remaining iterations of the reference's loop

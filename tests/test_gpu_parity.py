@@ -225,6 +225,25 @@ def test_weighted_vs_oracle_sweep(gpu):
     assert np.array_equal(ct, rct[:kk.value])
 
 
+@pytest.mark.parametrize("n,mask,k", [(300000, 0xFFFFFF, 4), (600000, 0xFEFEFE, 16), (1 << 20, 0xFCFCFC, 64)])
+def test_weighted_multi_tile_vs_oracle(gpu, n, mask, k):
+    """The weighted path's exact parallel folds on nodes of many tiles (10^5 -
+    10^6 unique colours: every pass's folds run over hundreds of 4096-point
+    tiles, with binade crossings inside tiles and across them) against the
+    oracle's sequential folds: colortable, output and centroid doubles."""
+    px = fx.xorshift(n, seed=fx.SEED + n) & mask
+    out, ct = gpu.quant_recurse(px, k, 0)
+    ref_out = np.zeros(n, np.uint32)
+    ref_ct = np.zeros(k, np.uint32)
+    kk = ctypes.c_uint32(k)
+    fx.oracle().dqo_quant_recurse_weighted(ctypes.c_uint32(n), fx.vp(px), fx.vp(ref_out), ctypes.byref(kk),
+                                           fx.vp(ref_ct))
+    assert np.array_equal(ct, ref_ct[:kk.value]), (n, k)
+    assert np.array_equal(out, ref_out), (n, k)
+    # (tiles folded summand by summand: the fallback, not the rule)
+    assert gpu.last_seq_tiles() <= gpu.last_rounds() * 8, gpu.last_seq_tiles()
+
+
 def test_oracle_random_sweep(gpu):
     """Fresh seeded inputs (not in any fixture) against the CPU oracle."""
     rng = np.random.default_rng(12345)
