@@ -1934,38 +1934,44 @@ __global__ __launch_bounds__(256) void upload_kernel(u32x4* __restrict__ dst, co
 // One LANE per cell (grid.x = kCells / kBlock): every lane of a wave reads
 // the same palette entry at the same time (LDS broadcast); each lane keeps
 // its loose candidate list in a transposed LDS array.
-__global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __restrict__ tasks) {
+template <int BR, int BG, int BB>
+__global__ __launch_bounds__(BR * BG * BB) void build_cells_kernel(const MapTask* __restrict__ tasks) {
+  constexpr int kThreads = BR * BG * BB;
+  constexpr int kWaves = kThreads / 64;
   const MapTask tk = tasks[blockIdx.y];
   const int k = tk.k;
   extern __shared__ uint32_t spal_c[];   // k colours, then k region-list entries (u16)
   uint16_t* slist = reinterpret_cast<uint16_t*>(spal_c + k);
-  __shared__ uint32_t scand[kCellCap * kBlock];   // [i][thread]
-  __shared__ int sred[kBlock / 64];
-  __shared__ uint32_t swoff[kBlock / 64 + 1];
-  for (int i = threadIdx.x; i < k; i += kBlock) spal_c[i] = as_g(tk.pal)[i];
+  __shared__ uint32_t scand[kCellCap * kThreads];   // [i][thread]
+  __shared__ int sred[kWaves];
+  __shared__ uint32_t swoff[kWaves + 1];
+  for (int i = threadIdx.x; i < k; i += kThreads) spal_c[i] = as_g(tk.pal)[i];
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   auto far2 = [](int v, int lo, int hi) { const int x = max(v - lo, hi - v); return x * x; };
   auto near2 = [](int v, int lo, int hi) {
     const int x = max(max(lo - v, v - hi), 0);
     return x * x;
   };
-  // This workgroup's cells: a 4 x 8 x 8 block of the 32^3 grid (R x G x B),
+  // This workgroup's cells: a BR x BG x BB block of the 32^3 grid (R x G x B),
   // so that one region list serves all of them.  For a cell C inside the
   // region R, C's candidates {e : near2(e,C) <= min_f far2(f,C)} are
   // candidates of R (near2(e,R) <= near2(e,C), far2(f,C) <= far2(f,R)), and
   // C's minimiser of far2 is one too: scanning R's list (palette order)
   // gives exactly the bound and the candidates of a scan over the palette.
-  static_assert(kCellBits == 5 && kBlock == 256, "4 x 8 x 8 cells per workgroup");
-  const uint32_t bb = blockIdx.x & 3u, bg = (blockIdx.x >> 2) & 3u, br = blockIdx.x >> 4;
-  const uint32_t c0 = br * 4 + (tid >> 6), c1 = bg * 8 + ((tid >> 3) & 7u), c2 = bb * 8 + (tid & 7u);
+  constexpr int kSide = 1 << kCellBits;
+  static_assert(kSide % BR == 0 && kSide % BG == 0 && kSide % BB == 0 && kThreads % 64 == 0,
+                "whole blocks of cells, whole waves");
+  constexpr uint32_t nbb = kSide / BB, nbg = kSide / BG;
+  const uint32_t bb = blockIdx.x % nbb, bg = (blockIdx.x / nbb) % nbg, br = blockIdx.x / (nbb * nbg);
+  const uint32_t c0 = br * BR + tid / (BG * BB), c1 = bg * BG + (tid / BB) % BG, c2 = bb * BB + tid % BB;
   const uint32_t cell = (c0 << (2 * kCellBits)) | (c1 << kCellBits) | c2;
   const int cw = 1 << (8 - kCellBits);
-  const int rlo0 = (int)br * 4 * cw, rlo1 = (int)bg * 8 * cw, rlo2 = (int)bb * 8 * cw;
-  const int rhi0 = rlo0 + 4 * cw - 1, rhi1 = rlo1 + 8 * cw - 1, rhi2 = rlo2 + 8 * cw - 1;
+  const int rlo0 = (int)br * BR * cw, rlo1 = (int)bg * BG * cw, rlo2 = (int)bb * BB * cw;
+  const int rhi0 = rlo0 + BR * cw - 1, rhi1 = rlo1 + BG * cw - 1, rhi2 = rlo2 + BB * cw - 1;
   __syncthreads();
   // region bound: min over entries of the max distance to the region
   int rb = 0x7FFFFFFF;
-  for (int e = (int)tid; e < k; e += kBlock) {
+  for (int e = (int)tid; e < k; e += kThreads) {
     const uint32_t q = spal_c[e];
     rb = min(rb, far2((q >> 16) & 0xFF, rlo0, rhi0) + far2((q >> 8) & 0xFF, rlo1, rhi1) +
                      far2(q & 0xFF, rlo2, rhi2));
@@ -1976,10 +1982,10 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
   __syncthreads();
   rb = sred[0];
 #pragma unroll
-  for (int w = 1; w < kBlock / 64; ++w) rb = min(rb, sred[w]);
-  // region list in palette order: chunks of kBlock entries, ballot-ranked
+  for (int w = 1; w < kWaves; ++w) rb = min(rb, sred[w]);
+  // region list in palette order: chunks of one entry per thread, ballot-ranked
   uint32_t nlist = 0;
-  for (int base = 0; base < k; base += kBlock) {
+  for (int base = 0; base < k; base += kThreads) {
     const int e = base + (int)tid;
     bool in = false;
     if (e < k) {
@@ -1993,7 +1999,7 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
     uint32_t off = nlist;
     for (uint32_t w = 0; w < wv; ++w) off += swoff[w];
     if (in) slist[off + mbcnt64(m)] = (uint16_t)e;
-    for (int w = 0; w < kBlock / 64; ++w) nlist += swoff[w];
+    for (int w = 0; w < kWaves; ++w) nlist += swoff[w];
     __syncthreads();
   }
   const int lo0 = (int)c0 * cw, lo1 = (int)c1 * cw, lo2 = (int)c2 * cw;
@@ -2013,7 +2019,7 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
     const uint32_t q = spal_c[e];
     const bool cand = near2((q >> 16) & 0xFF, lo0, hi0) + near2((q >> 8) & 0xFF, lo1, hi1) +
                           near2(q & 0xFF, lo2, hi2) <= bound;
-    if (cand && count < (uint32_t)kCellCap) scand[count * kBlock + tid] = e;
+    if (cand && count < (uint32_t)kCellCap) scand[count * kThreads + tid] = e;
     count += cand ? 1u : 0u;
   }
   // (b) dominance by the 4 candidates with the smallest max distance (as
@@ -2026,7 +2032,7 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
     int rf[kRefs] = {0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF, 0x7FFFFFFF};
     uint32_t rq[kRefs] = {0u, 0u, 0u, 0u};
     for (uint32_t i = 0; i < count; ++i) {   // the 4 smallest (far2, colour)
-      const uint32_t q = spal_c[scand[i * kBlock + tid]];
+      const uint32_t q = spal_c[scand[i * kThreads + tid]];
       int f = far2((q >> 16) & 0xFF, lo0, hi0) + far2((q >> 8) & 0xFF, lo1, hi1) + far2(q & 0xFF, lo2, hi2);
       uint32_t c = q;
 #pragma unroll
@@ -2044,7 +2050,7 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
     const int nref = (int)min(count, (uint32_t)kRefs);
     uint32_t kept = 0;
     for (uint32_t i = 0; i < count; ++i) {
-      const uint32_t ei = scand[i * kBlock + tid];
+      const uint32_t ei = scand[i * kThreads + tid];
       const uint32_t qe = spal_c[ei];
       const int e0 = (qe >> 16) & 0xFF, e1 = (qe >> 8) & 0xFF, e2 = qe & 0xFF;
       const int ee = e0 * e0 + e1 * e1 + e2 * e2;
@@ -2059,16 +2065,16 @@ __global__ __launch_bounds__(kBlock) void build_cells_kernel(const MapTask* __re
         // (f == e: dx = 0 = rhs, never strict)
         keep = keep && !(2 * dx < ee - (f0 * f0 + f1 * f1 + f2 * f2));
       }
-      if (keep) scand[(kept++) * kBlock + tid] = ei;
+      if (keep) scand[(kept++) * kThreads + tid] = ei;
     }
     fcount = kept;
   }
   uint16_t* lst = tk.cell_idx + (size_t)cell * kCellCap;
-  for (uint32_t i = 0; i < fcount; ++i) lst[i] = (uint16_t)scand[i * kBlock + tid];
+  for (uint32_t i = 0; i < fcount; ++i) lst[i] = (uint16_t)scand[i * kThreads + tid];
   const uint32_t c = brute ? kCellBrute : fcount;
   uint32_t slot[kCellInline];
 #pragma unroll
-  for (int i = 0; i < kCellInline; ++i) slot[i] = (uint32_t)i < fcount ? scand[i * kBlock + tid] : (uint32_t)k;
+  for (int i = 0; i < kCellInline; ++i) slot[i] = (uint32_t)i < fcount ? scand[i * kThreads + tid] : (uint32_t)k;
   uint4 r;
   r.x = c | (slot[0] << 16);
   r.y = slot[1] | (slot[2] << 16);
@@ -2539,16 +2545,24 @@ void launch_upload(void* dst, const void* src, size_t bytes, hipStream_t stream)
 }
 
 void launch_build_cells(const MapTask* tasks, int ntasks, int kmax, hipStream_t stream) {
-  static_assert(kCells % kBlock == 0, "whole cells per workgroup");
   if (ntasks <= 0) return;
   static bool attr = false;
   if (!attr) {   // palettes up to 16384 entries: up to 96 KB of dynamic LDS beside 32 KB static
-    (void)hipFuncSetAttribute((const void*)build_cells_kernel,
+    (void)hipFuncSetAttribute((const void*)build_cells_kernel<4, 8, 8>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+    (void)hipFuncSetAttribute((const void*)build_cells_kernel<4, 4, 4>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
     attr = true;
   }
-  build_cells_kernel<<<dim3(kCells / kBlock, ntasks), dim3(kBlock), (size_t)kmax * 6 + 16,
-                       stream>>>(tasks);
+  const size_t lds = (size_t)kmax * 6 + 16;
+  // A few palettes (one frame per call): 4 x 4 x 4 cells per one-wave
+  // workgroup -- 512 workgroups per palette instead of 128 on 256 CUs, and a
+  // cubic region (32^3 colours) keeps each region's list short.  Batches
+  // keep 256-thread workgroups (the palette staged once per 256 cells).
+  if (ntasks * (kCells / 256) < 2 * 256)
+    build_cells_kernel<4, 4, 4><<<dim3(kCells / 64, ntasks), dim3(64), lds, stream>>>(tasks);
+  else
+    build_cells_kernel<4, 8, 8><<<dim3(kCells / 256, ntasks), dim3(256), lds, stream>>>(tasks);
 }
 
 uint32_t map_groups_per_block(uint32_t n) {

@@ -212,14 +212,15 @@ __device__ __forceinline__ int w_binade(double v) {
 }
 
 // Pass step 3: per tile and fold, each summand's class (zero, run member of
-// binade e with integer RNE(x / 2^(e-52)), or special) from the prefix
-// estimate, then the tile's description: the ordered segments.  Run members
-// are binned by (specials before them, binade - e0) -- both never decrease
-// along the tile, so the bins in (sp, de) order, each special after the
-// bins of its group, are the tile's segments in sequence order.
-constexpr int kWSpMax = 16;    // specials per tile and fold described
-constexpr int kWDeMax = 16;    // binades per tile and fold described
-constexpr int kWBins = (kWSpMax + 1) * kWDeMax;
+// binade e with integer m = RNE(x / 2^(e-52)), or special) from the prefix
+// estimate, then the tile's description: its segments in sequence order --
+// every special, and every maximal stretch of run members with m != 0 and
+// one key (specials before them, binade).  A segment's slot is the number of
+// segments that start before it: block scans of the lanes' specials and
+// segment starts (a lane's first member starts one when its key differs from
+// the last member of the nearest earlier lane that has one).  The slots are
+// sequence order by construction, whatever the keys do along the tile.
+constexpr int kWKeyBias = 1100;   // binade e of a double in [-1074, 1023] -> e + bias in [26, 2123]
 __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
   const WTile t = a.tiles[blockIdx.x];
   const WState& st = a.nodes[t.node];
@@ -227,12 +228,12 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
   WPts q;
   w_load(a, st, t, pass, q);
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  __shared__ double s_wt[kWThreads / 64];
-  __shared__ int s_i[kWThreads / 64][2];
-  __shared__ unsigned long long s_bins[kWBins];
-  __shared__ double s_sp[kWSpMax];
-  __shared__ int s_over;
-  __shared__ int s_rank[kWBins + 1];
+  constexpr int kW = kWThreads / 64;
+  __shared__ double s_wt[kW];
+  __shared__ int s_sp[kW];                 // specials per wave
+  __shared__ int s_wk[kW][3];              // per wave: first / last member key (-1: none), starts
+  __shared__ unsigned long long s_m[kWSeg];
+  __shared__ int s_e[kWSeg];
   for (int ch = 0; ch < kWCh; ++ch) {
     double x[kWPer];
     double T = 0.0;
@@ -249,17 +250,15 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
       if (lane >= (uint32_t)o) inc += u;
     }
     if (lane == 63) s_wt[wv] = inc;
-    for (int b = (int)threadIdx.x; b < kWBins; b += kWThreads) s_bins[b] = 0ull;
-    if (threadIdx.x == 0) s_over = 0;
+    for (int b = (int)threadIdx.x; b < kWSeg; b += kWThreads) s_m[b] = 0ull;
     __syncthreads();
     double P = a.tpre[(size_t)blockIdx.x * 8 + ch];
     for (uint32_t w = 0; w < wv; ++w) P += s_wt[w];
     P += lane == 0 ? 0.0 : __shfl_up(inc, 1, 64);
-    // classes
+    // classes: e[k] (run member, m != 0), kWNone (zero or m = 0) or special
     int e[kWPer];
     int64_t m[kWPer];
     uint32_t spm = 0;   // bit k: special
-    int emin = 0x7FFFFFFF;
 #pragma unroll
     for (int k = 0; k < kWPer; ++k) {
       e[k] = kWNone;
@@ -277,14 +276,13 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
           const double fl = floor(tt), fr = tt - fl;
           special = fr == 0.5;                      // a tie: the parity of s decides
           m[k] = (int64_t)fl + (fr > 0.5 ? 1 : 0);
-          e[k] = el;
-          emin = min(emin, el);
+          if (!special && m[k] != 0) e[k] = el;     // (m = 0: adds nothing)
         }
         if (special) spm |= 1u << k;
       }
       P += x[k];
     }
-    // specials before each lane (exclusive scan of counts), the tile's e0
+    // specials before each lane (block exclusive scan)
     const int nsl = __popc(spm);
     int si = nsl;
 #pragma unroll
@@ -292,80 +290,124 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
       const int u = __shfl_up(si, o, 64);
       if (lane >= (uint32_t)o) si += u;
     }
-    int wmin = emin;
+    if (lane == 63) s_sp[wv] = si;
+    // the lane's member keys: first, last, starts after its first member
+    int spb = si - nsl;   // (wave-local until the block offset is added)
+    __syncthreads();
+    int nsp = 0;
+    for (int w = 0; w < kW; ++w) {
+      if (w < (int)wv) spb += s_sp[w];
+      nsp += s_sp[w];
+    }
+    int kfirst = -1, klast = -1, inner = 0;
+    {
+      int sp = spb;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) wmin = min(wmin, __shfl_xor(wmin, o, 64));
-    if (lane == 63) s_i[wv][0] = si;
-    if (lane == 0) s_i[wv][1] = wmin;
-    __syncthreads();
-    int spb = si - nsl, e0 = 0x7FFFFFFF, nsp = 0;
-    for (int w = 0; w < kWThreads / 64; ++w) {
-      if ((uint32_t)w < wv) spb += s_i[w][0];
-      nsp += s_i[w][0];
-      e0 = min(e0, s_i[w][1]);
-    }
-    bool over = nsp > kWSpMax;
-#pragma unroll
-    for (int k = 0; k < kWPer; ++k) {
-      if ((spm >> k) & 1u) {
-        if (spb < kWSpMax) s_sp[spb] = x[k];
-        ++spb;
-      } else if (e[k] != kWNone) {
-        const int b = e[k] - e0;
-        if (spb > kWSpMax || b >= kWDeMax) over = true;
-        else if (m[k] != 0) atomicAdd(&s_bins[spb * kWDeMax + b], (unsigned long long)m[k]);
-      }
-    }
-    if (over) s_over = 1;   // (benign race: every writer stores 1)
-    __syncthreads();
-    // wave 0: the bins' ranks among the nonzero ones (flattened (sp, de) order)
-    if (wv == 0) {
-      int run = 0;
-      for (int b0 = 0; b0 < kWBins; b0 += 64) {
-        const int b = b0 + (int)lane;
-        const bool nz = b < kWBins && s_bins[b] != 0ull;
-        const uint64_t bm = __ballot(nz);
-        if (b < kWBins) s_rank[b] = run + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-        run += (int)__popcll(bm);
-      }
-      if (lane == 0) s_rank[kWBins] = run;
-    }
-    __syncthreads();
-    const int nbin = s_rank[kWBins];
-    const int nseg = (s_over || nsp > kWSpMax || nbin + nsp > kWSeg) ? -1 : nbin + nsp;
-    WFold& f = a.fold[(size_t)blockIdx.x * kWCh + ch];
-    if (nseg >= 0) {
-      // run bin (sp, de) at rank + sp; special sp after its group's bins
-      for (int b = (int)threadIdx.x; b < kWBins; b += kWThreads) {
-        const unsigned long long v = s_bins[b];
-        if (v) {
-          const int sp = b / kWDeMax;
-          WSegment& g = f.seg[s_rank[b] + sp];
-          g.e = e0 + (b - sp * kWDeMax);
-          g.pad = 0;
-          g.v = (int64_t)v;
+      for (int k = 0; k < kWPer; ++k) {
+        if ((spm >> k) & 1u) {
+          ++sp;
+        } else if (e[k] != kWNone) {
+          const int key = (sp << 12) | (e[k] + kWKeyBias);
+          if (kfirst < 0) kfirst = key;
+          else if (key != klast) ++inner;
+          klast = key;
         }
       }
-      if ((int)threadIdx.x < nsp) {
-        const int sp = (int)threadIdx.x;
-        WSegment& g = f.seg[s_rank[(sp + 1) * kWDeMax] + sp];
-        g.e = kWSpecial;
+    }
+    // the nearest earlier lane of the wave with members: its last key
+    const uint64_t hm = __ballot(kfirst >= 0);
+    const uint64_t before = hm & ((1ull << lane) - 1ull);
+    const int jp = before ? 63 - __builtin_clzll(before) : 0;
+    const int kprev_w = __shfl(klast, jp, 64);
+    const bool first_known = before != 0;   // else: from the earlier waves
+    int starts = inner + ((kfirst >= 0 && first_known && kfirst != kprev_w) ? 1 : 0);
+    // wave aggregates: first member key (of the wave's first lane with
+    // members), last member key, starts except that first lane's first one
+    int ws = starts;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ws += __shfl_xor(ws, o, 64);
+    const int jf = hm ? __builtin_ctzll(hm) : 0, jl = hm ? 63 - __builtin_clzll(hm) : 0;
+    const int wfirst = __shfl(kfirst, jf, 64), wlast = __shfl(klast, jl, 64);
+    if (lane == 0) {
+      s_wk[wv][0] = hm ? wfirst : -1;
+      s_wk[wv][1] = hm ? wlast : -1;
+      s_wk[wv][2] = ws;
+    }
+    __syncthreads();
+    // starts before this wave, and the last member key before it
+    int sbefore = 0, kprev = -1, ntot = 0, kp = -1;
+    for (int w = 0; w < kW; ++w) {
+      const int f = s_wk[w][0], l = s_wk[w][1];
+      const int add = s_wk[w][2] + ((f >= 0 && f != kp) ? 1 : 0);
+      if (w < (int)wv) sbefore += add;
+      if (w == (int)wv) kprev = kp;
+      ntot += add;
+      if (l >= 0) kp = l;
+    }
+    if (kfirst >= 0 && !first_known && kfirst != kprev) starts += 1;
+    int sx = starts;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(sx, o, 64);
+      if (lane >= (uint32_t)o) sx += u;
+    }
+    // place: a run member's slot = (segment starts up to it) - 1 + specials
+    // before it; a special's = segment starts before it + its special index
+    const int nseg = ntot + nsp;
+    {
+      int r = sbefore + sx - starts;
+      int sp = spb;
+      int key = first_known ? kprev_w : kprev;
+      int cur = -1;                 // slot of the lane's open accumulation
+      unsigned long long acc = 0ull;
+#pragma unroll
+      for (int k = 0; k < kWPer; ++k) {
+        if ((spm >> k) & 1u) {
+          const int slot = r + sp;
+          if (slot < kWSeg) {
+            s_e[slot] = kWSpecial;
+            s_m[slot] = (unsigned long long)__double_as_longlong(x[k]);
+          }
+          ++sp;
+        } else if (e[k] != kWNone) {
+          const int kk = (sp << 12) | (e[k] + kWKeyBias);
+          if (kk != key) {
+            ++r;
+            key = kk;
+          }
+          const int slot = r - 1 + sp;
+          if (slot != cur) {
+            if (cur >= 0 && cur < kWSeg) atomicAdd(&s_m[cur], acc);
+            cur = slot;
+            acc = 0ull;
+            if (slot < kWSeg) s_e[slot] = e[k];   // (every writer of a slot stores the same e)
+          }
+          acc += (unsigned long long)m[k];
+        }
+      }
+      if (cur >= 0 && cur < kWSeg) atomicAdd(&s_m[cur], acc);
+    }
+    __syncthreads();
+    WFold& f = a.fold[(size_t)blockIdx.x * kWCh + ch];
+    const int ns = nseg > kWSeg ? -1 : nseg;
+    if (ns > 0) {
+      for (int i = (int)threadIdx.x; i < ns; i += kWThreads) {
+        WSegment g;
+        g.e = s_e[i];
         g.pad = 0;
-        g.v = __double_as_longlong(s_sp[sp]);
+        g.v = (int64_t)s_m[i];
+        f.seg[i] = g;
       }
     }
     if (threadIdx.x == 0) {
-      f.nseg = nseg;
+      f.nseg = ns;
       WQuick& qk = a.quick[(size_t)blockIdx.x * kWCh + ch];
-      if (nseg == 0) {
+      if (ns == 0) {
         qk.e = kWNone;
         qk.m = 0;
-      } else if (nseg == 1 && nsp == 0) {
-        int bz = 0;
-        while (s_bins[bz] == 0ull) ++bz;
-        qk.e = e0 + bz;
-        qk.m = (int64_t)s_bins[bz];
+      } else if (ns == 1 && nsp == 0) {
+        qk.e = s_e[0];
+        qk.m = (int64_t)s_m[0];
       } else {
         qk.e = kWComplex;
         qk.m = 0;

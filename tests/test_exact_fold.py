@@ -6,7 +6,7 @@ from a prefix estimate: a summand whose running sum provably stays in one
 binade [2^e, 2^(e+1)) adds u * RNE(x / u), u = 2^(e-52), exactly; the rest
 ("specials": the first summand, binade crossings, ties) are added in order.
 This file restates that algorithm in numpy with the GPU's tile size, margin,
-segment limits and chain rules, and checks it bit for bit against the
+segment limit and chain rules, and checks it bit for bit against the
 sequential fold on summand sequences shaped like the reference's (weights
 count / N times channel values and their squares, zeros for points not
 taken), including sequences built to land on binade boundaries and ties.
@@ -18,7 +18,7 @@ import pytest
 
 TILE = 4096
 MARGIN = 2.0 ** -20
-SP_MAX, DE_MAX, SEG_MAX = 16, 16, 32
+SEG_MAX = 64        # kWSeg
 
 
 def seq_fold(x):
@@ -56,33 +56,23 @@ def classify_tile(x, p0):
             kinds.append("sp"); es.append(None); ms.append(0)
             continue
         kinds.append("run"); es.append(e); ms.append(int(fl) + (1 if fr > 0.5 else 0))
-    runs = [e for k, e in zip(kinds, es) if k == "run"]
-    e0 = min(runs) if runs else 0
-    nsp = kinds.count("sp")
-    if nsp > SP_MAX:
-        return None
-    bins = {}
-    sps = []
-    spb = 0
+    # segments in sequence order: each special, and each maximal stretch of
+    # run members (m != 0) with one (specials before, binade) key
+    segs = []
+    key = None
+    nsp = 0
     for k, e, m, xi in zip(kinds, es, ms, x.tolist()):
         if k == "sp":
-            sps.append(xi)
-            spb += 1
-        elif k == "run":
-            if spb > SP_MAX or e - e0 >= DE_MAX:
-                return None
-            bins[(spb, e - e0)] = bins.get((spb, e - e0), 0) + m
-    segs = []
-    for sp in range(nsp + 1):
-        for de in range(DE_MAX):
-            m = bins.get((sp, de), 0)
-            if m:
-                segs.append(("run", e0 + de, m))
-        if sp < nsp:
-            segs.append(("sp", sps[sp]))
+            segs.append(("sp", xi))
+            nsp += 1
+        elif k == "run" and m != 0:
+            if (nsp, e) != key:
+                key = (nsp, e)
+                segs.append(["run", e, 0])
+            segs[-1][2] += m
     if len(segs) > SEG_MAX:
         return None
-    return segs
+    return [tuple(g) for g in segs]
 
 
 def apply_run(s, e, m):
@@ -164,10 +154,113 @@ def test_binade_boundaries_and_ties():
         assert got.hex() == seq_fold(x).hex(), trial
 
 
-def test_describable_tiles_are_the_rule():
-    """Only a node's first tile (many binade crossings from s = 0) may need
-    the summand-by-summand fold on the reference-like sequences."""
-    x = summands(400000, 11, "sum")
-    got, seq_tiles = parallel_fold(x)
-    assert got.hex() == seq_fold(x).hex()
-    assert seq_tiles <= 1
+@pytest.mark.parametrize("kind", ["sum", "sq", "w"])
+def test_every_tile_is_described(kind):
+    """No tile needs the summand-by-summand fold on reference-like sequences,
+    the node's first tile included (its sum crosses a binade every few
+    summands from s = 0: 20-40 segments, within kWSeg)."""
+    for seed in range(4):
+        x = summands(120000, 11 + seed, kind)
+        got, seq_tiles = parallel_fold(x)
+        assert got.hex() == seq_fold(x).hex()
+        assert seq_tiles == 0, (kind, seed)
+
+
+def slots_like_the_kernel(kinds, keys, lanes=256, per=16, wave=64):
+    """wk_classify's distributed slot assignment (dq_weighted.hip): per lane
+    its first / last member key and inner starts, the nearest earlier lane
+    with members inside the wave, wave aggregates, then each item's slot.
+    kinds[i]: 0 zero, 1 run member (key[i]), 2 special.  Returns {i: slot}."""
+    L = [list(range(l * per, (l + 1) * per)) for l in range(lanes)]
+    nsl = [sum(kinds[i] == 2 for i in L[l]) for l in range(lanes)]
+    spb = [sum(nsl[:l]) for l in range(lanes)]
+    nsp = sum(nsl)
+    kf, kl, inner = [-1] * lanes, [-1] * lanes, [0] * lanes
+    for l in range(lanes):
+        sp = spb[l]
+        for i in L[l]:
+            if kinds[i] == 2:
+                sp += 1
+            elif kinds[i] == 1:
+                k = (sp << 12) | keys[i]
+                if kf[l] < 0:
+                    kf[l] = k
+                elif k != kl[l]:
+                    inner[l] += 1
+                kl[l] = k
+    nw = lanes // wave
+    starts, known, kprev_w = [0] * lanes, [False] * lanes, [-1] * lanes
+    for l in range(lanes):
+        w0 = (l // wave) * wave
+        prev = [j for j in range(w0, l) if kf[j] >= 0]
+        known[l] = bool(prev)
+        kprev_w[l] = kl[prev[-1]] if prev else -1
+        starts[l] = inner[l] + (1 if kf[l] >= 0 and known[l] and kf[l] != kprev_w[l] else 0)
+    agg = []
+    for w in range(nw):
+        ls = [l for l in range(w * wave, (w + 1) * wave) if kf[l] >= 0]
+        agg.append((kf[ls[0]] if ls else -1, kl[ls[-1]] if ls else -1,
+                    sum(starts[w * wave:(w + 1) * wave])))
+    slot = {}
+    kp, sb, kprev = -1, [0] * nw, [-1] * nw
+    acc = 0
+    for w in range(nw):
+        f, lk, ws = agg[w]
+        add = ws + (1 if f >= 0 and f != kp else 0)
+        sb[w], kprev[w] = acc, kp
+        acc += add
+        if lk >= 0:
+            kp = lk
+    ntot = acc
+    for l in range(lanes):
+        w = l // wave
+        if kf[l] >= 0 and not known[l] and kf[l] != kprev[w]:
+            starts[l] += 1
+    for l in range(lanes):
+        w = l // wave
+        r = sb[w] + sum(starts[w * wave:l])
+        sp = spb[l]
+        key = kprev_w[l] if known[l] else kprev[w]
+        for i in L[l]:
+            if kinds[i] == 2:
+                slot[i] = r + sp
+                sp += 1
+            elif kinds[i] == 1:
+                k = (sp << 12) | keys[i]
+                if k != key:
+                    r += 1
+                    key = k
+                slot[i] = r - 1 + sp
+    return slot, ntot + nsp
+
+
+def test_kernel_slot_assignment_is_sequence_order():
+    """The kernel's scan-based slots equal the sequential segmentation's,
+    for class patterns with empty lanes, empty waves, keys that repeat
+    across specials, and keys that go down."""
+    rng = np.random.default_rng(5)
+    for trial in range(60):
+        n = 4096
+        kinds = rng.choice([0, 1, 2], n, p=[0.5, 0.49, 0.01]).tolist()
+        if trial % 3 == 0:   # an empty wave and empty lanes
+            for i in range(1024, 2048):
+                kinds[i] = 0
+        keys = np.cumsum(rng.random(n) < 0.002).tolist() if trial % 2 else rng.integers(0, 3, n).tolist()
+        keys = [int(k) + 26 for k in keys]
+        slot, nseg = slots_like_the_kernel(kinds, keys)
+        # sequential reference
+        exp, cur, s, sp = {}, None, -1, 0
+        for i in range(n):
+            if kinds[i] == 2:
+                s += 1
+                exp[i] = s
+                sp += 1
+                cur = None
+            elif kinds[i] == 1:
+                k = (sp, keys[i])
+                if k != cur:
+                    s += 1
+                    cur = k
+                exp[i] = s
+        assert slot == exp, trial
+        assert nseg == s + 1

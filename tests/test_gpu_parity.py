@@ -240,8 +240,9 @@ def test_weighted_multi_tile_vs_oracle(gpu, n, mask, k):
                                            fx.vp(ref_ct))
     assert np.array_equal(ct, ref_ct[:kk.value]), (n, k)
     assert np.array_equal(out, ref_out), (n, k)
-    # (tiles folded summand by summand: the fallback, not the rule)
-    assert gpu.last_seq_tiles() <= gpu.last_rounds() * 8, gpu.last_seq_tiles()
+    # (tiles folded summand by summand: the fallback, not the rule -- none
+    # on these frames in the CPU model, tests/test_exact_fold.py)
+    assert gpu.last_seq_tiles() <= gpu.last_rounds(), gpu.last_seq_tiles()
 
 
 def test_oracle_random_sweep(gpu):
