@@ -1,0 +1,47 @@
+"""Compare a bench line's roofline with rocprofv3 --stats of the same command.
+
+    python3 tools/roofline_check.py BENCH_JSON PROF_DIR
+
+Prints the line's dominant kernel, its HIP-event average launch, the
+rocprofv3 average of the same kernel, their ratio, and the roofline fraction
+recomputed from the rocprof average (algorithmic bytes per launch / average
+duration / peak)."""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main():
+    line = [ln for ln in open(sys.argv[1]) if ln.startswith("{")][-1]
+    d = json.loads(line)
+    roof = d["roofline"]
+    sym = roof["kernel"].split("<")[0]
+    tmpl = roof["kernel"][len(sym):]
+    stats = glob.glob(os.path.join(sys.argv[2], "**", "*kernel_stats.csv"), recursive=True)
+    if not stats:
+        raise SystemExit("no kernel_stats.csv under %s" % sys.argv[2])
+    rows = list(csv.DictReader(open(stats[0])))
+    # rocprof spells template arguments as integers (PASS_KMEANS -> 2)
+    want = {"<PASS_KMEANS>": "<2>", "<PASS_KLAST>": "<3>"}.get(tmpl, tmpl)
+    hit = [r for r in rows if ("dq::" + sym + want + "(") in r["Name"] or
+           (not want and ("dq::" + sym + "(") in r["Name"])]
+    if not hit:
+        raise SystemExit("kernel %s not in %s" % (roof["kernel"], stats[0]))
+    r = hit[0]
+    avg_us = float(r["AverageNs"]) / 1e3
+    frac = roof["alg_bytes_per_launch"] / (avg_us * 1e-6) / 1e9 / roof["peak"]
+    print(json.dumps({
+        "bench_value": d["value"], "bench_ms_per_step": d["ms_per_step"], "verified": d["verified"]["ok"],
+        "kernel": roof["kernel"], "bench_avg_launch_us": roof["avg_launch_us"],
+        "bench_launches": roof["launches"], "bench_frac": roof["frac"],
+        "rocprof_name": r["Name"], "rocprof_calls": int(r["Calls"]), "rocprof_avg_us": round(avg_us, 2),
+        "ratio_rocprof_over_bench": round(avg_us / roof["avg_launch_us"], 4),
+        "frac_from_rocprof_avg": round(frac, 4),
+        "stats_file": os.path.relpath(stats[0], os.path.dirname(os.path.abspath(sys.argv[1]))),
+    }, indent=1))
+
+
+if __name__ == "__main__":
+    main()
