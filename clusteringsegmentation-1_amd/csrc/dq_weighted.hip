@@ -199,7 +199,8 @@ __global__ __launch_bounds__(64) void wk_prefix(WArgs a) {
         const double u = __shfl_up(inc, o, 64);
         if (lane >= o) inc += u;
       }
-      const double ex = lane == 0 ? 0.0 : __shfl_up(inc, 1, 64);
+      const double up = __shfl_up(inc, 1, 64);   // (every lane: a shuffle's source lane must be active)
+      const double ex = lane == 0 ? 0.0 : up;
       if (i < st.tile_end) a.tpre[(size_t)i * 8 + ch] = run + ex;
       run += __shfl(inc, 63, 64);
     }
@@ -254,7 +255,8 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
     __syncthreads();
     double P = a.tpre[(size_t)blockIdx.x * 8 + ch];
     for (uint32_t w = 0; w < wv; ++w) P += s_wt[w];
-    P += lane == 0 ? 0.0 : __shfl_up(inc, 1, 64);
+    const double up = __shfl_up(inc, 1, 64);   // (every lane: a shuffle's source lane must be active)
+    P += lane == 0 ? 0.0 : up;
     // classes: e[k] (run member, m != 0), kWNone (zero or m = 0) or special
     int e[kWPer];
     int64_t m[kWPer];
@@ -561,7 +563,8 @@ __global__ __launch_bounds__(64) void wk_chain(WArgs a, int pass) {
           const int u = __shfl_up(pmax, o, 64);
           if (lane >= (uint32_t)o) pmax = max(pmax, u);
         }
-        const int before = lane == 0 ? -0x7FFFFFFF : __shfl_up(pmax, 1, 64);
+        const int up = __shfl_up(pmax, 1, 64);     // (every lane: a shuffle's source lane must be active)
+        const int before = lane == 0 ? -0x7FFFFFFF : up;
         if (__ballot(run && qk.e < before)) {
           for (int j = pos; j < nc; ++j) {
             const int ej = __shfl(qk.e, j, 64);
