@@ -67,6 +67,8 @@ Engine::Engine(int device) : device_(device) {
   if (const char* v = getenv("DQ_HIP_SPEC_KMEANS")) speculate_kmeans_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_SPIN_SYNC")) spin_sync_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_PLAN")) plan_ = v[0] != '0';
+  if (const char* v = getenv("DQ_HIP_EAGER_REPLAN")) eager_replan_ = v[0] != '0';
+  if (const char* v = getenv("DQ_HIP_STATS_ONLY")) stats_only_ = v[0] != '0';
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
 }
@@ -240,11 +242,11 @@ void Engine::ensure_round(size_t rec_cap, size_t tiles_cap, size_t, size_t stagi
     if (d_dres_) DQ_HIP(hipFree(d_dres_));
     if (h_plist_) DQ_HIP(hipHostFree(h_plist_));
     const size_t c = std::max<size_t>(rec_cap, 256);
-    DQ_HIP(hipHostMalloc((void**)&h_res_, 2 * c * sizeof(NodeResult), hipHostMallocCoherent | hipHostMallocMapped));
-    std::memset(h_res_, 0, 2 * c * sizeof(NodeResult));
+    DQ_HIP(hipHostMalloc((void**)&h_res_, kSlots * c * sizeof(NodeResult), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(h_res_, 0, kSlots * c * sizeof(NodeResult));
     DQ_HIP(hipHostGetDevicePointer((void**)&d_res_, h_res_, 0));
-    DQ_HIP(hipMalloc((void**)&d_dres_, 2 * c * sizeof(NodeResult)));
-    DQ_HIP(hipHostMalloc((void**)&h_plist_, 2 * c * sizeof(int32_t), hipHostMallocCoherent | hipHostMallocMapped));
+    DQ_HIP(hipMalloc((void**)&d_dres_, kSlots * c * sizeof(NodeResult)));
+    DQ_HIP(hipHostMalloc((void**)&h_plist_, kSlots * c * sizeof(int32_t), hipHostMallocCoherent | hipHostMallocMapped));
     DQ_HIP(hipHostGetDevicePointer((void**)&d_plist_, h_plist_, 0));
     cap_res_ = c;
     cap_plist_ = c;
@@ -252,13 +254,13 @@ void Engine::ensure_round(size_t rec_cap, size_t tiles_cap, size_t, size_t stagi
   if ((size_t)max_iters + 1 > cap_stat_ || !h_stat_) {
     if (h_stat_) DQ_HIP(hipHostFree(h_stat_));
     cap_stat_ = std::max<size_t>((size_t)max_iters + 1, 32);
-    DQ_HIP(hipHostMalloc((void**)&h_stat_, 2 * cap_stat_ * sizeof(uint64_t), hipHostMallocCoherent | hipHostMallocMapped));
-    std::memset(h_stat_, 0, 2 * cap_stat_ * sizeof(uint64_t));
+    DQ_HIP(hipHostMalloc((void**)&h_stat_, kSlots * cap_stat_ * sizeof(uint64_t), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(h_stat_, 0, kSlots * cap_stat_ * sizeof(uint64_t));
     DQ_HIP(hipHostGetDevicePointer((void**)&d_stat_, h_stat_, 0));
   }
   if (!h_counts_) {
-    DQ_HIP(hipHostMalloc((void**)&h_counts_, 2 * 4 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
-    std::memset(h_counts_, 0, 2 * 4 * sizeof(uint32_t));
+    DQ_HIP(hipHostMalloc((void**)&h_counts_, kSlots * 4 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(h_counts_, 0, kSlots * 4 * sizeof(uint32_t));
     DQ_HIP(hipHostGetDevicePointer((void**)&d_counts_h_, h_counts_, 0));
   }
   grow_device(&d_parts_, &cap_parts_, tiles_cap);
@@ -609,7 +611,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   if (trace_) tr_build_us_ += host_us() - tb0;
 
   R.seq = ++seq_;
-  R.par = (int)(R.seq & 1);
+  R.par = (int)(R.seq % kSlots);
   RoundArgs& ra = R.ra;
   ra.tiles = dt;
   ra.nodes = dn;
@@ -703,7 +705,7 @@ bool Engine::plan_list(int ri, std::vector<int32_t>* plist) {
 // counts); if a listed record is not final after its split epilogue the plan
 // aborts the round (the host plans it again once `prev` has converged).
 int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, int max_iters,
-                                  hipStream_t stream) {
+                                  hipStream_t stream, const uint32_t* cancel) {
   const double tb0 = trace_ ? host_us() : 0.0;
   rounds_.emplace_back();
   const int ri = (int)rounds_.size() - 1;
@@ -736,7 +738,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   // partition only sums (PS_STATS); the points of parents with a child left
   // active go out after the split epilogue (PS_LATE), the rest only if a
   // later round reads them (enqueue_host_round, PS_WRITE)
-  R.stats_only = true;
+  R.stats_only = stats_only_;
   for (int32_t a : plist) {
     const FrameState& f = frames_[nodes_[P.order[a]].frame];
     R.stats_only = R.stats_only && f.splits_queued >= f.job->k - 1;
@@ -769,7 +771,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   R.dt = reinterpret_cast<Tile*>(dblk + o_tiles);
   R.dcounts = reinterpret_cast<uint32_t*>(dblk + o_cnt);
   R.seq = ++seq_;
-  R.par = (int)(R.seq & 1);
+  R.par = (int)(R.seq % kSlots);
   // the plan list: identity unless some frames do not speculate
   bool ident = true;
   for (int i = 0; i < np; ++i) ident = ident && plist[i] == i && np == P.nl;
@@ -798,6 +800,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   pa.cap_bytes = 4 * cap_px_;
   pa.debug = debug_;
   pa.nshard = S;
+  pa.cancel = cancel;
   RoundArgs& ra = R.ra;
   ra.tiles = R.dt;
   ra.nodes = R.dn;
@@ -913,8 +916,8 @@ void Engine::kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream) {
 // Wait for a round's split epilogue, run its 2-means iterations if any record
 // is still active (host-polled, `lookahead_` launched past the one awaited),
 // then take its results: children nodes, segments, the parents' tiles.
-void Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool speculate) {
-  Round& R = rounds_[ri];
+int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool speculate, int successor) {
+  Round& R = rounds_[ri];   // (rounds_ is a deque: enqueueing below keeps R valid)
   const int S = nshard_;
   const double tw0 = tr_wait_us_;
   const double tf0 = trace_ ? host_us() : 0.0;
@@ -939,6 +942,20 @@ void Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specul
   }
   debug_host_delay();
   R.kmeans = !all_proven;
+  // A planned successor queued behind this round aborts when a record it
+  // splits is still active after the split epilogue (nearly always so when
+  // 2-means runs).  Then every remaining iteration goes in now (a record final
+  // earlier makes them exit at once, ~2 us each) and the successor is planned
+  // again right behind them: the GPU moves on without waiting for the host to
+  // see the last iteration (~25 us per 2-means round).  The re-plan cancels
+  // itself if the first plan ran after all; run() keeps whichever is live.
+  int replan = -1;
+  if (!all_proven && successor >= 0 && eager_replan_) {
+    for (; launched < max_iters; ++launched) kmeans_iter(R, launched, max_iters, stream);
+    const std::vector<int32_t> pl = rounds_[successor].plist;
+    for (int32_t a : pl) frames_[nodes_[R.order[a]].frame].splits_queued -= 2;   // (re-counted below)
+    replan = enqueue_planned_round(ri, pl, max_iters, stream, rounds_[successor].dcounts);
+  }
   while (!all_proven) {
     while (launched < max_iters && launched <= known + lookahead_) {
       kmeans_iter(R, launched, max_iters, stream);
@@ -1089,6 +1106,7 @@ void Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specul
                  R.planned ? "planned" : "host", nl, R.nr, R.ntiles, R.nptiles, R.bytes,
                  tf0 - R.t_enq, tr_wait_us_ - tw0, launched, tp1 - tp0, R.kmeans ? " kmeans" : "");
   }
+  return replan;
 }
 
 // ---------------------------------------------------------------------------
@@ -1323,7 +1341,8 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   while (!q.empty()) {
     const int ri = q.front();
     if (q.size() == 1 && plan_list(ri, &plist)) q.push_back(enqueue_planned_round(ri, plist, max_iters, stream));
-    finish_round(ri, max_iters, stream, q.size() == 1 && speculate_kmeans_);
+    const int succ = q.size() >= 2 && rounds_[q[1]].planned && rounds_[q[1]].prev == ri ? q[1] : -1;
+    const int replan = finish_round(ri, max_iters, stream, q.size() == 1 && speculate_kmeans_, succ);
     q.pop_front();
     last_rounds++;
     if (rounds_[ri].planned) last_planned++;
@@ -1337,10 +1356,16 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
       if (ab == 1) {
         q.pop_front();
         last_aborted++;
-        const std::vector<int32_t> pl = rounds_[pi].plist;
-        for (int32_t a : pl) frames_[nodes_[rounds_[ri].order[a]].frame].splits_queued -= 2;
-        q.push_front(enqueue_planned_round(ri, pl, max_iters, stream));
+        if (replan >= 0) {   // already planned again behind ri's iterations
+          q.push_front(replan);
+        } else {
+          const std::vector<int32_t> pl = rounds_[pi].plist;
+          for (int32_t a : pl) frames_[nodes_[rounds_[ri].order[a]].frame].splits_queued -= 2;
+          q.push_front(enqueue_planned_round(ri, pl, max_iters, stream));
+        }
       }
+      // (ab == 0 with a re-plan: the re-plan cancels itself on the device;
+      // the split accounting moved to it is the first plan's)
     }
     for (int p : q)
       if (rounds_[p].planned && rounds_[p].prev == ri) assign_planned(p);

@@ -17,6 +17,7 @@
 
 #include <mutex>
 #include <queue>
+#include <deque>
 #include <vector>
 
 #include "dq_internal.h"
@@ -229,7 +230,7 @@ class Engine {
   // from exist (their records: the children of `plist`'s records of `prev`).
   struct Round {
     uint64_t seq = 0;
-    int par = 0;                      // status / result slot parity
+    int par = 0;                      // status / result slot (seq % kSlots)
     bool root = false, planned = false;
     int prev = -1;                    // planned: the round it is planned from
     std::vector<int32_t> plist;       // planned: records of `prev` split in it
@@ -251,7 +252,7 @@ class Engine {
     std::vector<std::pair<size_t, int>> km_events;
     double t_enq = 0;
   };
-  std::vector<Round> rounds_;
+  std::deque<Round> rounds_;          // (a deque: references stay valid while rounds are added)
 
   void ensure_pixels(size_t total);
   void ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t staging_bytes,
@@ -262,9 +263,11 @@ class Engine {
                          hipStream_t stream);
   bool plan_list(int ri, std::vector<int32_t>* plist);
   int enqueue_planned_round(int prev, const std::vector<int32_t>& plist, int max_iters,
-                            hipStream_t stream);
+                            hipStream_t stream, const uint32_t* cancel = nullptr);
   void assign_planned(int ri);
-  void finish_round(int ri, int max_iters, hipStream_t stream, bool speculate = false);
+  // successor: a planned round queued from ri (-1: none).  Returns the index
+  // of a re-plan of it enqueued behind ri's 2-means iterations, or -1.
+  int finish_round(int ri, int max_iters, hipStream_t stream, bool speculate = false, int successor = -1);
   void kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream);
   uint64_t tile_len_of(uint64_t len, uint64_t tl) const;
   uint64_t round_tile_len(uint64_t total) const;
@@ -317,8 +320,11 @@ class Engine {
   TilePartial* d_sparts_ = nullptr;   // per PartTile of the round
   size_t cap_parts_ = 0, cap_sparts_ = 0;
   // host-coherent pinned memory the epilogues write (results, status words),
-  // two slots (round parity: a planned round runs while the host finishes
-  // the previous one); the results' device copy the plans read
+  // kSlots slots by round sequence (a planned round runs while the host
+  // finishes the previous one; a re-plan can be queued behind a planned
+  // round the host has not resolved yet); the results' device copy the plans
+  // read
+  static constexpr int kSlots = 3;
   NodeResult* h_res_ = nullptr;
   NodeResult* d_res_ = nullptr;       // device view of h_res_
   NodeResult* d_dres_ = nullptr;      // device memory
@@ -335,6 +341,9 @@ class Engine {
   hipEvent_t stage_ev_ = nullptr;     // the last upload of h_stage_
   bool stage_pending_ = false;
   bool plan_ = true;                  // device-planned rounds (DQ_HIP_PLAN=0: host only)
+  bool stats_only_ = true;            // a frame's last planned round: PS_STATS + PS_LATE (DQ_HIP_STATS_ONLY)
+  bool eager_replan_ = true;          // finish_round: all 2-means iterations + the re-plan at
+                                      //   once when a planned successor waits (DQ_HIP_EAGER_REPLAN)
   uint64_t seq_ = 0;                  // round sequence number
   int lookahead_ = 2;                 // 2-means iterations queued past the one awaited
                                       //   (1: C3 0.543-0.554 ms, 2: 0.518-0.525, 4: 0.520-0.532)

@@ -94,8 +94,11 @@ struct PlanArgs {
   PartTile* cpt;
   uint32_t* zero;           // [LaunchCtr | wparts | rdone] words to clear
   uint32_t nzero;
-  uint32_t* counts;         // device: tiles, part tiles, aborted (2: overflow)
+  uint32_t* counts;         // device: tiles, part tiles, aborted (1: a listed parent not
+                            //   final, 2: overflow, 3: cancelled -- see `cancel`)
   uint32_t* hcounts;        // host-coherent mirror of counts
+  const uint32_t* cancel;   // a re-plan (Engine::finish_round): the counts of the first
+                            //   plan of the same round; it cancels itself if that one ran
   const uint8_t* p0;        // the two working buffers (a child's dst is the
   const uint8_t* p1;        //   other one of its src)
   uint64_t cap_bytes;       // bytes per working buffer

@@ -1803,19 +1803,21 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     __syncthreads();   // (s_w reuse)
   }
   if (__any(bad) && lane == 0) s_abort = 1;
+  // a re-plan whose first plan ran (did not abort) is not needed
+  const bool cancelled = a.cancel && a.cancel[2] == 0;
   if (tid == 0) { s_cb[np] = run_t; s_pb[np] = run_p; }
   __syncthreads();
   const bool overflow = run_t > a.tiles_cap || run_p > a.ptiles_cap;
   if (blockIdx.x == 0 && tid == 0) {
     if (a.debug & kDebugPlanStall) debug_sleep_us(20);
-    const uint32_t ab = s_abort ? 1u : (overflow ? 2u : 0u);
+    const uint32_t ab = cancelled ? 3u : (s_abort ? 1u : (overflow ? 2u : 0u));
     const uint32_t c[3] = {ab ? 0u : run_t, ab ? 0u : run_p, ab};
     for (int k = 0; k < 3; ++k) {
       a.counts[k] = c[k];
       __hip_atomic_store(a.hcounts + k, c[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
-  if (s_abort || overflow) return;
+  if (cancelled || s_abort || overflow) return;
   if (blockIdx.x < nb_rec) {
     // (2a) records: (parent i, shard sh) -> records (2i)*S + sh (old half),
     //      (2i+1)*S + sh (new half)

@@ -24,7 +24,7 @@ echo "[measure] roofline pair"
 bash tools/gpu_roofline.sh $1/roof
 for c in c3 c2; do
   echo "[measure] $c timeline"
-  timeout -k 10 120 rocprofv3 --kernel-trace -d $O/tl_$c -o run -- python3 -u tools/c2_trace.py $c 6 \
+  timeout -k 10 120 rocprofv3 --kernel-trace -f csv -d $O/tl_$c -o run -- python3 -u tools/c2_trace.py $c 6 \
     > $O/tl_$c.log 2>&1 || { tail -20 $O/tl_$c.log; exit 1; }
   python3 tools/timeline.py $O/tl_$c 70 > $O/timeline_$c.txt
   tail -16 $O/timeline_$c.txt
