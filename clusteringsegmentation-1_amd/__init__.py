@@ -32,7 +32,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DQ_HIP_LIB") or os.path.join(PKG_DIR, "libdivquant_hip.so")
 
 STAT_KINDS = ["pass_init", "pass_split", "pass_kmeans", "pass_klast",
-              "epilogue", "partition", "map_cells", "map", "plan"]
+              "epilogue", "partition", "map_cells", "map", "plan", "kloop"]
 
 _lib = None
 
@@ -86,6 +86,8 @@ def lib():
         "dq_hip_set_fixed_point": ([c.c_int, c.c_int], None),
         "dq_hip_set_planned_rounds": ([c.c_int, c.c_int], None),
         "dq_hip_last_planned_rounds": ([c.c_int], c.c_int),
+        "dq_hip_set_loop_max": ([c.c_int, c.c_uint32], None),
+        "dq_hip_last_loop_rounds": ([c.c_int], c.c_int),
         "dq_hip_set_timing": ([c.c_int, c.c_int], None),
         "dq_hip_reset_stats": ([c.c_int], None),
         "dq_hip_get_stat": ([c.c_int, c.c_int, c.POINTER(c.c_uint64), c.POINTER(c.c_double),
@@ -537,6 +539,15 @@ def set_planned_rounds(on, device=0):
 
 def last_planned_rounds(device=0):
     return lib().dq_hip_last_planned_rounds(device)
+
+
+def set_loop_max(max_points, device=0):
+    """kloop_kernel eligibility: records of at most max_points points (0: off)."""
+    lib().dq_hip_set_loop_max(device, int(max_points))
+
+
+def last_loop_rounds(device=0):
+    return lib().dq_hip_last_loop_rounds(device)
 
 
 def set_lanes(lanes):

@@ -796,6 +796,12 @@ void dq_hip_set_planned_rounds(int device, int on) {
 }
 int dq_hip_last_planned_rounds(int device) { return engine_for(device).last_planned; }
 
+void dq_hip_set_loop_max(int device, uint32_t max_points) {
+  for (int l = 0; l < dq::kMaxLanes; ++l) engine_for(device, l).set_loop_max(max_points);
+}
+
+int dq_hip_last_loop_rounds(int device) { return engine_for(device).last_loop_rounds; }
+
 void dq_hip_set_timing(int device, int on) { engine_for(device).set_timing(on != 0); }
 
 void dq_hip_set_debug(int device, int flags) {
@@ -825,7 +831,7 @@ int dq_hip_get_stat_units(int device, int kind, double* units) {
 
 const char* dq_hip_stat_name(int kind) {
   static const char* names[] = {"pass_init", "pass_split", "pass_kmeans", "pass_klast",
-                                "epilogue", "partition", "map_cells", "map", "plan"};
+                                "epilogue", "partition", "map_cells", "map", "plan", "kloop"};
   if (kind < 0 || kind >= dq::ST_COUNT) return "";
   return names[kind];
 }

@@ -69,8 +69,13 @@ Engine::Engine(int device) : device_(device) {
   if (const char* v = getenv("DQ_HIP_PLAN")) plan_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_EAGER_REPLAN")) eager_replan_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_STATS_ONLY")) stats_only_ = v[0] != '0';
+  if (const char* v = getenv("DQ_HIP_KLOOP_SHADOW")) kloop_shadow_ = v[0] == '1';
+  if (const char* v = getenv("DQ_HIP_KLOOP_MAX"))
+    kloop_max_ = (uint32_t)std::max<long>(0, std::min<long>((long)kLoopMaxLen, atol(v)));
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  DQ_HIP(hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_));
+  num_cus_ = std::max(1, num_cus_);
 }
 
 Engine::~Engine() {
@@ -913,6 +918,84 @@ void Engine::kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream) {
   }
 }
 
+bool Engine::loop_ok(const Round& R) const {
+  // (one workgroup per record on one CU: a 2-means pass costs it ~0.1 us per
+  // 1000 points of VALU work, so only small records in rounds of at most one
+  // record per CU beat the ~11 us of a kpass launch per iteration)
+  if (kloop_max_ == 0 || nshard_ != 1 || comm_ || R.root || R.nr > num_cus_) return false;
+  for (int a = 0; a < R.nl; ++a) {
+    const int id = R.order[a];
+    if (nodes_[id].buf == BUF_IN) return false;   // (a root's packed / BGR24 frame)
+    if (segs_[id].len > kloop_max_ || R.tend[a] - R.tbeg[a] > (int32_t)kLoopMaxTiles) return false;
+  }
+  return true;
+}
+
+void Engine::kmeans_loop(Round& R, int max_iters, hipStream_t stream) {
+  ++last_loop_rounds;
+  timed_begin(stream);
+  launch_kloop(R.ra, R.nr, max_iters, stream);
+  timed_end(ST_KLOOP, 0.0, stream);
+  if (timing_) R.loop_event = (long)pending_.size() - 1;
+}
+
+void Engine::shadow_launch(Round& R, int max_iters, hipStream_t stream) {
+  const size_t need = R.nr * sizeof(DevNode) + R.ntiles * sizeof(Tile) + R.nr * sizeof(NodeResult) + 256;
+  if (need > cap_shadow_) {
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (d_shadow_) DQ_HIP(hipFree(d_shadow_));
+    DQ_HIP(hipMalloc(&d_shadow_, 2 * need));
+    cap_shadow_ = 2 * need;
+  }
+  RoundArgs sa = R.ra;
+  char* p = static_cast<char*>(d_shadow_);
+  sa.shadow_nodes = reinterpret_cast<DevNode*>(p);
+  sa.shadow_tiles = reinterpret_cast<Tile*>(p + ((R.nr * sizeof(DevNode) + 63) & ~(size_t)63));
+  sa.shadow_res = reinterpret_cast<NodeResult*>(reinterpret_cast<char*>(sa.shadow_tiles) +
+                                                ((R.ntiles * sizeof(Tile) + 63) & ~(size_t)63));
+  DQ_HIP(hipMemsetAsync(d_shadow_, 0, need, stream));
+  launch_kloop(sa, R.nr, max_iters, stream);
+}
+
+void Engine::shadow_compare(Round& R) {
+  DQ_HIP(hipDeviceSynchronize());
+  std::vector<DevNode> sn(R.nr), rn(R.nr);
+  std::vector<Tile> st(R.ntiles), rt(R.ntiles);
+  std::vector<NodeResult> sr(R.nr);
+  char* p = static_cast<char*>(d_shadow_);
+  const size_t ot = (R.nr * sizeof(DevNode) + 63) & ~(size_t)63;
+  const size_t orr = ot + ((R.ntiles * sizeof(Tile) + 63) & ~(size_t)63);
+  DQ_HIP(hipMemcpy(sn.data(), p, R.nr * sizeof(DevNode), hipMemcpyDeviceToHost));
+  DQ_HIP(hipMemcpy(st.data(), p + ot, R.ntiles * sizeof(Tile), hipMemcpyDeviceToHost));
+  DQ_HIP(hipMemcpy(sr.data(), p + orr, R.nr * sizeof(NodeResult), hipMemcpyDeviceToHost));
+  DQ_HIP(hipMemcpy(rn.data(), R.dn, R.nr * sizeof(DevNode), hipMemcpyDeviceToHost));
+  DQ_HIP(hipMemcpy(rt.data(), R.dt, R.ntiles * sizeof(Tile), hipMemcpyDeviceToHost));
+  const NodeResult* res = h_res_ + (size_t)R.par * cap_res_;
+  int bad = 0, checked = 0;
+  for (int r = 0; r < R.nr; ++r) {
+    if (res[r].proven) continue;   // final at the split: kloop skipped it
+    ++checked;
+    const DevNode& a = sn[r];
+    const DevNode& b = rn[r];
+    char why[256] = "";
+    if (a.n_new_local != b.n_new_local) std::snprintf(why, sizeof why, "n_new_local %u vs %u", a.n_new_local, b.n_new_local);
+    else if (a.done_it != b.done_it) std::snprintf(why, sizeof why, "done_it %d vs %d", a.done_it, b.done_it);
+    else if (std::memcmp(&a.prm, &b.prm, sizeof(Params)) != 0) std::snprintf(why, sizeof why, "prm");
+    else if (std::memcmp(&sr[r], &res[r], offsetof(NodeResult, pad)) != 0) std::snprintf(why, sizeof why, "result");
+    else
+      for (int i = b.tile_begin; i < b.tile_end && !why[0]; ++i)
+        if (std::memcmp(st[i].old_base, rt[i].old_base, sizeof rt[i].old_base) != 0 ||
+            std::memcmp(st[i].new_base, rt[i].new_base, sizeof rt[i].new_base) != 0)
+          std::snprintf(why, sizeof why, "tile %d cursors (old_base[0] %u vs %u, new_base[0] %u vs %u)", i,
+                        st[i].old_base[0], rt[i].old_base[0], st[i].new_base[0], rt[i].new_base[0]);
+    if (why[0] && bad++ < 8)
+      std::fprintf(stderr, "divquant-hip shadow: seq %llu record %d (len %u, tiles %d): %s\n",
+                   (unsigned long long)R.seq, r, b.len, b.tile_end - b.tile_begin, why);
+  }
+  std::fprintf(stderr, "divquant-hip shadow: seq %llu records %d checked %d mismatched %d\n",
+               (unsigned long long)R.seq, R.nr, checked, bad);
+}
+
 // Wait for a round's split epilogue, run its 2-means iterations if any record
 // is still active (host-polled, `lookahead_` launched past the one awaited),
 // then take its results: children nodes, segments, the parents' tiles.
@@ -925,12 +1008,27 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   const NodeResult* res = h_res_ + (size_t)R.par * cap_res_;
   int launched = 0, known = 0;
   bool all_proven = false;
+  // Late rounds (small records): every 2-means iteration in one launch,
+  // waited for on the status word of iteration max_iters - 1
+  const bool shadow = fixed_point_ && kloop_shadow_ && loop_ok(R);
+  const bool loop = fixed_point_ && !kloop_shadow_ && loop_ok(R);
+  bool shadowed = false;
   // Nothing else queued behind this round (a frame's last rounds): its first
   // 2-means iterations go in before its split status is known -- a record
   // final at the split makes them exit at once (~4 us each); C3's last round
   // needs them and otherwise waited ~15 us for the host to see the status.
-  if (speculate && fixed_point_)
-    for (; launched < max_iters && launched <= lookahead_; ++launched) kmeans_iter(R, launched, max_iters, stream);
+  if (speculate && fixed_point_) {
+    if (shadow) {
+      shadow_launch(R, max_iters, stream);
+      shadowed = true;
+    }
+    if (loop) {
+      kmeans_loop(R, max_iters, stream);
+      launched = max_iters;
+    } else {
+      for (; launched < max_iters && launched <= lookahead_; ++launched) kmeans_iter(R, launched, max_iters, stream);
+    }
+  }
   if (fixed_point_) all_proven = wait_status(stat + max_iters, R.seq, stream) == 0;
   if (R.planned) {   // the plan's counts equal the host's mirror of its layout
     const uint32_t* hc = h_counts_ + 4 * R.par;
@@ -942,6 +1040,11 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   }
   debug_host_delay();
   R.kmeans = !all_proven;
+  const bool all_proven_split = all_proven;
+  if (shadow && !shadowed && !all_proven) {
+    shadow_launch(R, max_iters, stream);
+    shadowed = true;
+  }
   // A planned successor queued behind this round aborts when a record it
   // splits is still active after the split epilogue (nearly always so when
   // 2-means runs).  Then every remaining iteration goes in now (a record final
@@ -951,10 +1054,22 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   // itself if the first plan ran after all; run() keeps whichever is live.
   int replan = -1;
   if (!all_proven && successor >= 0 && eager_replan_) {
+    if (loop && launched == 0) {
+      kmeans_loop(R, max_iters, stream);
+      launched = max_iters;
+    }
     for (; launched < max_iters; ++launched) kmeans_iter(R, launched, max_iters, stream);
     const std::vector<int32_t> pl = rounds_[successor].plist;
     for (int32_t a : pl) frames_[nodes_[R.order[a]].frame].splits_queued -= 2;   // (re-counted below)
     replan = enqueue_planned_round(ri, pl, max_iters, stream, rounds_[successor].dcounts);
+  }
+  if (!all_proven && loop) {
+    if (launched == 0) {
+      kmeans_loop(R, max_iters, stream);
+      launched = max_iters;
+    }
+    DQ_CHECK(wait_status(stat + (max_iters - 1), R.seq, stream) == 0, "kloop_kernel left a record active");
+    all_proven = true;   // (every record final: the loop below has nothing to wait for)
   }
   while (!all_proven) {
     while (launched < max_iters && launched <= known + lookahead_) {
@@ -1025,9 +1140,14 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
       pending_[e.first].bytes = swept_bytes(e.second);
       pending_[e.first].units = (double)swept_in(e.second);
     }
+    if (R.loop_event >= 0) {   // kloop reads every active record's points once
+      pending_[R.loop_event].bytes = swept_bytes(0);
+      pending_[R.loop_event].units = (double)swept_in(0);
+    }
     collect_timing();
   }
 
+  if (shadowed && !all_proven_split) shadow_compare(R);
   if (R.stats_only)   // written by PS_LATE iff the node or its sibling was active after its split
     for (int a = 0; a + 1 < nl; a += 2) {
       const bool written = !(res[a * S].proven && res[(a + 1) * S].proven);
@@ -1319,6 +1439,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   const double t_run0 = trace_ ? host_us() : 0.0;
   tr_wait_us_ = tr_build_us_ = tr_replay_us_ = 0.0;
   last_planned = last_aborted = 0;
+  last_loop_rounds = 0;
   {   // this run's capacities (nothing in flight now)
     size_t rec_cap = 64, px = 0;
     for (int i = 0; i < nframes; ++i) {

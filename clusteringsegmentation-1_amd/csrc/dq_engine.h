@@ -108,7 +108,7 @@ struct KernelStat {
   double units = 0.0;   // points (pixels) the launches processed
 };
 enum StatKind { ST_INIT = 0, ST_SPLIT, ST_KMEANS, ST_KLAST, ST_EPILOGUE, ST_PARTITION,
-                ST_CELLS, ST_MAP, ST_PLAN, ST_COUNT };
+                ST_CELLS, ST_MAP, ST_PLAN, ST_KLOOP, ST_COUNT };
 
 class Engine {
  public:
@@ -178,6 +178,7 @@ class Engine {
   int last_rounds = 0;
   int last_planned = 0;               // rounds planned on the device (of last_rounds)
   int last_aborted = 0;               // planned rounds whose plan found a parent unfinished
+  int last_loop_rounds = 0;           // rounds whose 2-means iterations ran in one kloop_kernel launch
   uint64_t last_points_swept = 0;     // sum over passes of points read (all frames)
   uint64_t last_points_full = 0;      // the same without fixed-point finalisation
   uint64_t last_seq_tiles = 0;        // weighted: tiles folded one summand at a time
@@ -199,6 +200,8 @@ class Engine {
   void set_fixed_point(bool on) { fixed_point_ = on; }
   // Device-planned rounds (default on; DQ_HIP_PLAN=0 turns the default off).
   void set_plan(bool on) { plan_ = on; }
+  // kloop_kernel eligibility: records of at most n points (0: never)
+  void set_loop_max(uint32_t n) { kloop_max_ = std::min<uint32_t>(n, kLoopMaxLen); }
   bool plan() const { return plan_; }
   bool fixed_point() const { return fixed_point_; }
   void reset_stats();
@@ -250,6 +253,7 @@ class Engine {
     bool kmeans = false;              // its split epilogue left records active
     bool stats_only = false;          // planned, a frame's last: partsplit PS_STATS (+ PS_LATE)
     std::vector<std::pair<size_t, int>> km_events;
+    long loop_event = -1;             // kloop_kernel's timing event (pending_ index)
     double t_enq = 0;
   };
   std::deque<Round> rounds_;          // (a deque: references stay valid while rounds are added)
@@ -269,6 +273,17 @@ class Engine {
   // of a re-plan of it enqueued behind ri's 2-means iterations, or -1.
   int finish_round(int ri, int max_iters, hipStream_t stream, bool speculate = false, int successor = -1);
   void kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream);
+  // All 2-means iterations of round R in one launch (kloop_kernel): every
+  // record one shard, planar, at most kloop_max_ points and kLoopMaxTiles tiles.
+  bool loop_ok(const Round& R) const;
+  void kmeans_loop(Round& R, int max_iters, hipStream_t stream);
+  // DQ_HIP_KLOOP_SHADOW=1 (debugging): kloop_kernel runs beside the kpass
+  // iterations into scratch, and its records / cursors / results are compared
+  bool kloop_shadow_ = false;
+  void* d_shadow_ = nullptr;
+  size_t cap_shadow_ = 0;
+  void shadow_launch(Round& R, int max_iters, hipStream_t stream);
+  void shadow_compare(Round& R);
   uint64_t tile_len_of(uint64_t len, uint64_t tl) const;
   uint64_t round_tile_len(uint64_t total) const;
   void replay(FrameState& f);
@@ -352,6 +367,7 @@ class Engine {
   void sync_stream(hipStream_t stream);
   bool speculate_kmeans_ = true;      // a round with nothing queued behind it starts its
                                       //   2-means iterations before its split status (DQ_HIP_SPEC_KMEANS)
+  uint32_t kloop_max_ = 49152;        // a record's points at most for kloop_kernel (DQ_HIP_KLOOP_MAX; 0: off)
   int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TILES)
   int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_NODE_TILES)
   uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TILE_MAX)

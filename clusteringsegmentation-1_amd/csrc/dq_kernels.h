@@ -52,6 +52,11 @@ struct RoundArgs {
   uint64_t plane;           // bytes between the R, G and B planes of P0 / P1
   int32_t tot_mode;         // where a record's pass totals come from (TotMode)
   int32_t ps_mode;          // what partsplit_kernel does (PsMode)
+  // kloop_kernel debugging (DQ_HIP_KLOOP_SHADOW): its records, tiles and
+  // results go here instead, and it does not arrive (nullptr: production)
+  DevNode* shadow_nodes;
+  Tile* shadow_tiles;
+  NodeResult* shadow_res;
 };
 
 // partsplit_kernel's work (RoundArgs::ps_mode):
@@ -141,6 +146,13 @@ void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t strea
 // TOT_ALLREDUCE rounds: per logical node, the sums of the pass over all its
 // shard records' tiles into a.tot (to be allreduced across processes).
 void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stream);
+// All 2-means iterations of the round in one launch, one workgroup per
+// record (kloop_kernel): records of one shard (S == 1, TOT_OWN) with planar
+// segments of at most kLoopMaxLen points and at most kLoopMaxTiles tiles.
+// Every record arrives on the counter of iteration max_iters - 1.
+constexpr uint32_t kLoopMaxTiles = 1024;
+constexpr uint32_t kLoopMaxLen = 1u << 20;   // (a wave's u32 sums of squares stay exact)
+void launch_kloop(const RoundArgs& a, int nrec, int max_iters, hipStream_t stream);
 // Fused partition + split pass over the round's PartTiles: writes each
 // parent's points into its two children's segments (old half first, then new
 // half) of the child buffer, using the parent's final 2-means decision, and

@@ -1626,6 +1626,240 @@ __global__ __launch_bounds__(kBlock, 4) void partsplit_kernel(RoundArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// All 2-means iterations of a round in ONE launch, one workgroup per record
+// (kloop_kernel).  Late rounds split nodes of ~10^4-10^5
+// points, and their 2-means loop (:613-811) is a chain of up to max_iters
+// dependent passes: as kpass launches each costs a kernel boundary, a sweep
+// over 8+ tiles and the last arriver's hand-off (~11 us at C3, ~13 at C2),
+// almost none of it moving bytes.  Here the record's points are loaded ONCE
+// into the workgroup's registers (kLoopRegChunks 16-point chunks per lane;
+// a longer record streams the rest from memory every iteration) and every
+// iteration is a sweep over registers, a workgroup reduction and the
+// reference's FP64 update (node_update, the same function as kpass's
+// epilogue, on the same exact integer sums), with no other workgroup
+// involved.  After the final iteration the record's per-(tile, wave) counts
+// under its final decision give the partition cursors (block_cursors), the
+// results go to the host as from kpass, and every record arrives once on
+// the launch counter of iteration max_iters - 1 (the status word the host
+// waits for).  One shard per record (S == 1, TOT_OWN), planar segments.
+constexpr int kLoopBlock = 1024;
+constexpr int kLoopRegChunks = 4;          // 4 x 16 points per sweeping lane in registers: 61440 points
+constexpr int kLoopMaxBuckets = 4096;      // (tile, wave) buckets: 1024 tiles per record
+
+// Valid slots of the 16-point chunk at absolute index c16 for the segment [lo, hi).
+__device__ __forceinline__ uint32_t chunk_valid(uint32_t c16, uint32_t lo, uint32_t hi) {
+  const int a = (int)lo - (int)c16, b = (int)hi - (int)c16;
+  uint32_t m = b >= 16 ? 0xFFFFu : (b <= 0 ? 0u : (1u << b) - 1u);
+  if (a > 0) m &= a >= 16 ? 0u : ~((1u << a) - 1u);
+  return m;
+}
+
+__device__ __forceinline__ Sweep chunk_sweep_of(const u32x4& r, const u32x4& g, const u32x4& b) {
+  Sweep w;
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) {
+    w.r[j] = r[j];
+    w.g[j] = g[j];
+    w.b[j] = b[j];
+  }
+  return w;
+}
+
+// (tile, wave) bucket of absolute point p of a record: tile k = [off + k tl,
+// ...), its waves per wave_range.
+__device__ __forceinline__ uint32_t loop_bucket(uint32_t p, uint32_t off, uint32_t len, uint32_t tl) {
+  const uint32_t k = (p - off) / tl;
+  const uint32_t ts = off + k * tl, te = min(off + len, ts + tl);
+  const uint32_t q = ((te - ts + kSweep - 1) / kSweep) * kWaveSweep;
+  return 4u * k + (p - ts) / q;
+}
+
+// Waves 0 .. kLoopDataWaves-1 hold the points and sweep them; the last wave
+// runs the FP64 update between the two barriers of every iteration.  (Two
+// loops, one per role: the sweepers' registers are not live across the
+// update, whose FP64 temporaries would otherwise spill them.)
+constexpr int kLoopDataWaves = kLoopBlock / 64 - 1;
+constexpr uint32_t kLoopDataLanes = 64u * kLoopDataWaves;
+__global__ __launch_bounds__(kLoopBlock) void kloop_kernel(RoundArgs a, int32_t max_iters) {
+  if (a.counts && a.counts[2] != 0) return;   // planned round aborted by its plan
+  typedef __attribute__((address_space(1))) u32x4 g_u4;
+  const uint32_t rec = blockIdx.x;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  DevNode* gw = a.nodes + rec;
+  const bool shadow = a.shadow_nodes != nullptr;
+  __shared__ __attribute__((aligned(16))) DevNode sw;
+  __shared__ NodeResult sres;
+  __shared__ uint32_t s_red[kLoopDataWaves][8];
+  __shared__ uint64_t s_tot[kLoopBlock / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t s_b[kLoopMaxBuckets];
+  __shared__ int s_fin;
+  constexpr int kW16 = (int)(sizeof(DevNode) / 16);
+  if (tid < (uint32_t)kW16) reinterpret_cast<u32x4*>(&sw)[tid] = ((const g_cu4*)gw)[tid];
+  for (uint32_t i = tid; i < (uint32_t)kLoopMaxBuckets; i += kLoopBlock) s_b[i] = 0u;
+  __syncthreads();
+  const int tb = sw.tile_begin, te = sw.tile_end;
+  // (the host's eligibility rules, checked again: a record outside them is
+  // left untouched and arrives active, which the host reports)
+  const bool bad = sw.done_it == 0 && (sw.planar != SRC_PLANAR || sw.len > kLoopMaxLen || tb < 0 ||
+                                       te - tb > (int)kLoopMaxTiles || te <= tb || sw.tile_len == 0);
+  const bool skip = sw.done_it != 0 || bad;   // final at its split (or in an earlier launch)
+  if (!skip) {
+    if (wv < (uint32_t)kLoopDataWaves) {
+      // (wave-uniform values read from LDS: readfirstlane keeps them, and the
+      // buffer resources built from them, in scalar registers)
+      const uint32_t off = __builtin_amdgcn_readfirstlane(sw.off);
+      const uint32_t len = __builtin_amdgcn_readfirstlane(sw.len), end = off + len;
+      const uint32_t base = off & ~15u;
+      const uint32_t nch = (end - base + 15u) >> 4;   // 16-point chunks of the segment
+      const uint64_t srcu = reinterpret_cast<uint64_t>(sw.src);
+      // (readfirstlane returns int: each half goes through uint32_t, or the
+      // low half's bit 31 would sign-extend over the high half)
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(srcu >> 32)) << 32) |
+          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)srcu));
+      PlaneRsrc s;
+      {
+        const int nb = (int)(end + 16u);   // (16 B of slack after every shard)
+        s.r = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, nb, 0x00020000);
+        s.g = __builtin_amdgcn_make_buffer_rsrc((void*)(src + a.plane), (short)0, nb, 0x00020000);
+        s.b = __builtin_amdgcn_make_buffer_rsrc((void*)(src + 2 * a.plane), (short)0, nb, 0x00020000);
+      }
+      auto load = [&](uint32_t c, u32x4& r, u32x4& g, u32x4& b) {
+        const int o = (int)(c < nch ? base + 16u * c : kOOB);
+        r = __builtin_amdgcn_raw_buffer_load_b128(s.r, o, 0, 0);
+        g = __builtin_amdgcn_raw_buffer_load_b128(s.g, o, 0, 0);
+        b = __builtin_amdgcn_raw_buffer_load_b128(s.b, o, 0, 0);
+      };
+      u32x4 rr[kLoopRegChunks], gg[kLoopRegChunks], bb[kLoopRegChunks];
+#pragma unroll
+      for (int k = 0; k < kLoopRegChunks; ++k) load(tid + k * kLoopDataLanes, rr[k], gg[k], bb[k]);
+      const uint32_t tail0 = kLoopRegChunks * kLoopDataLanes;   // first streamed chunk row
+      auto valid = [&](uint32_t c) { return c < nch ? chunk_valid(base + 16u * c, off, end) : 0u; };
+      for (;;) {
+        const Params q = sw.prm;
+        const bool exact_all = !(q.eps < __builtin_inff());
+        SplitSums ls;
+        // (the points are loop-invariant: without this the compiler hoists
+        // their per-slot conversions out of the loop and spills)
+#pragma unroll
+        for (int k = 0; k < kLoopRegChunks; ++k) asm volatile("" : "+v"(rr[k]), "+v"(gg[k]), "+v"(bb[k]));
+#pragma unroll
+        for (int k = 0; k < kLoopRegChunks; ++k) {
+          if (wv * 64u + k * kLoopDataLanes >= nch) break;   // (wave-uniform: the wave's chunks are past the segment)
+          const uint32_t vm = valid(tid + k * kLoopDataLanes);
+          const Sweep w = chunk_sweep_of(rr[k], gg[k], bb[k]);
+          add_sums(w, vm & ~old_mask(w, vm, q, exact_all), ls);
+        }
+        for (uint32_t c = tail0 + tid; c - tid < nch; c += kLoopDataLanes) {   // (wave-uniform trip count)
+          u32x4 r, g, b;
+          load(c, r, g, b);
+          const uint32_t vm = valid(c);
+          const Sweep w = chunk_sweep_of(r, g, b);
+          add_sums(w, vm & ~old_mask(w, vm, q, exact_all), ls);
+        }
+        // (a wave holds at most 2^16 points of a record below kLoopMaxLen:
+        // its u32 sums of squares are exact)
+        uint32_t f[F_NUM] = {ls.cnt, ls.sr, ls.sg, ls.sb, ls.qr, ls.qg, ls.qb};
+#pragma unroll
+        for (int k = 0; k < F_NUM; ++k) f[k] = wave_sum_u32(f[k]);
+        if (lane == 0) {
+#pragma unroll
+          for (int k = 0; k < F_NUM; ++k) s_red[wv][k] = f[k];
+        }
+        __syncthreads();   // (A) partial sums in
+        __syncthreads();   // (B) the update out
+        if (s_fin) break;
+      }
+      // per-(tile, wave) old | new << 16 counts under the final decision (the
+      // one that produced the final halves: node_update leaves prm unchanged
+      // when it finalises)
+      const Params q = sw.prm;
+      const bool exact_all = !(q.eps < __builtin_inff());
+      const uint32_t tl = __builtin_amdgcn_readfirstlane(sw.tile_len);
+      // (the register chunks' masks first, so their points are dead before
+      // the bucket arithmetic)
+      auto count = [&](uint32_t c, uint32_t om, uint32_t vm) {
+        const uint32_t nm = vm & ~om;
+        if (vm == 0u) return;
+        const uint32_t p0 = base + 16u * c + (uint32_t)__builtin_ctz(vm);
+        const uint32_t p1 = base + 16u * c + 31u - (uint32_t)__builtin_clz(vm);
+        const uint32_t b0 = loop_bucket(p0, off, len, tl);
+        if (b0 == loop_bucket(p1, off, len, tl)) {
+          atomicAdd(&s_b[b0], (uint32_t)__builtin_popcount(om) | ((uint32_t)__builtin_popcount(nm) << 16));
+        } else {
+          for (int e = 0; e < 16; ++e)
+            if ((vm >> e) & 1u)
+              atomicAdd(&s_b[loop_bucket(base + 16u * c + (uint32_t)e, off, len, tl)],
+                        ((om >> e) & 1u) ? 1u : 0x10000u);
+        }
+      };
+      uint32_t omk[kLoopRegChunks];
+#pragma unroll
+      for (int k = 0; k < kLoopRegChunks; ++k) asm volatile("" : "+v"(rr[k]), "+v"(gg[k]), "+v"(bb[k]));
+#pragma unroll
+      for (int k = 0; k < kLoopRegChunks; ++k) {
+        omk[k] = 0u;
+        if (wv * 64u + k * kLoopDataLanes >= nch) continue;   // (wave-uniform)
+        const uint32_t vm = valid(tid + k * kLoopDataLanes);
+        omk[k] = old_mask(chunk_sweep_of(rr[k], gg[k], bb[k]), vm, q, exact_all) | (vm << 16);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int k = 0; k < kLoopRegChunks; ++k) count(tid + k * kLoopDataLanes, omk[k] & 0xFFFFu, omk[k] >> 16);
+      for (uint32_t c = tail0 + tid; c - tid < nch; c += kLoopDataLanes) {
+        u32x4 r, g, b;
+        load(c, r, g, b);
+        const uint32_t vm = valid(c);
+        count(c, old_mask(chunk_sweep_of(r, g, b), vm, q, exact_all), vm);
+      }
+    } else {
+      // the update wave: iteration it's totals -> node_update (lane 0)
+      for (int it = sw.iter;; ++it) {
+        __syncthreads();   // (A)
+        if (lane == 0) {
+          uint64_t t[F_NUM];
+#pragma unroll
+          for (int k = 0; k < F_NUM; ++k) {
+            t[k] = 0;
+            for (int v = 0; v < kLoopDataWaves; ++v) t[k] += s_red[v][k];
+          }
+          const bool fin = it == max_iters - 1 ? node_update<PASS_KLAST>(&sw, &sres, t, a.fixed_point != 0)
+                                               : node_update<PASS_KMEANS>(&sw, &sres, t, a.fixed_point != 0);
+          if (fin) {
+            for (int c = 0; c < 3; ++c) { sres.tm[c] = sw.tm[c]; sres.tv[c] = sw.tv[c]; }
+            sw.n_new_local = (uint32_t)t[F_CNT];
+            sres.n_new_local = (uint32_t)t[F_CNT];
+            sres.done_it = sw.done_it;
+          }
+          s_fin = fin ? 1 : 0;
+        }
+        __syncthreads();   // (B)
+        if (s_fin) break;
+      }
+    }
+    __syncthreads();   // counts in
+    block_cursors<kLoopBlock>(shadow ? a.shadow_tiles : a.tiles, s_b, tb, te, s_tot, tb);
+    if (tid < (uint32_t)kW16)   // the final record back (later launches read it)
+      ((g_u4*)(shadow ? a.shadow_nodes + rec : gw))[tid] = reinterpret_cast<const u32x4*>(&sw)[tid];
+  }
+  // every wave's cursor / record stores complete before the results and the
+  // arrival (the host and later launches read them after the status word /
+  // the kernel boundary)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wv != 0) return;
+  if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x)) debug_sleep_us(10);
+  if (shadow) {
+    if (!skip && lane == 0) a.shadow_res[rec] = sres;
+    return;
+  }
+  if (!skip) store_result(a.hres + rec, a.dres ? a.dres + rec : nullptr, sres, lane, sw.len, a.seq);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0)
+    arrive(a.ctr + (max_iters - 1), rec, (uint32_t)a.nn, bad, a.hstat + (max_iters - 1), a.seq);
+}
+
+// ---------------------------------------------------------------------------
 // Device-planned rounds (PlanArgs, dq_kernels.h).  The tables a host-built
 // round gets from Engine::run_round -- records, tiles, part tiles, cleared
 // counters -- built on the device from the previous round's records and
@@ -2531,6 +2765,11 @@ void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stre
 void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream) {
   if (nptiles <= 0) return;
   partsplit_kernel<<<dim3(nptiles), dim3(kBlock), 0, stream>>>(a);
+}
+
+void launch_kloop(const RoundArgs& a, int nrec, int max_iters, hipStream_t stream) {
+  if (nrec <= 0) return;
+  kloop_kernel<<<dim3(nrec), dim3(kLoopBlock), 0, stream>>>(a, max_iters);
 }
 
 void launch_plan(const PlanArgs& a, hipStream_t stream) {

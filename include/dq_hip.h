@@ -225,6 +225,14 @@ void dq_hip_set_fixed_point(int device, int on);
  * dq_hip_last_planned_rounds: how many rounds of the last run were planned. */
 void dq_hip_set_planned_rounds(int device, int on);
 int dq_hip_last_planned_rounds(int device);
+/* One-launch 2-means loops: a round whose records all hold at
+ * most max_points points (default 49152; DQ_HIP_KLOOP_MAX) and that has at
+ * most one record per CU runs all its 2-means iterations in one
+ * kloop_kernel launch, one workgroup per record.  0 turns it off.  Outputs
+ * are identical either way.  dq_hip_last_loop_rounds: how many rounds of the
+ * last run did so. */
+void dq_hip_set_loop_max(int device, uint32_t max_points);
+int dq_hip_last_loop_rounds(int device);
 
 /* Engine lanes a batch of frames is split over (each: own stream, own host
  * thread; DQ_HIP_LANES, default 3).  lanes = 0 restores the default. */

@@ -337,6 +337,40 @@ def test_fixed_point_finalisation_is_exact(gpu):
         gpu.set_planned_rounds(True)
 
 
+@pytest.mark.parametrize("key", ["1920x1080_k256", "512x512_k64"])
+def test_one_launch_kmeans_loops(gpu, key):
+    """Rounds of small records run every 2-means iteration in one
+    kloop_kernel launch per round: same exact integer sums and
+    the same FP64 update as the kpass_kernel chain, so the colortable, output,
+    split trace, centroid doubles -- and the records, partition cursors and
+    results later rounds read -- are the reference's either way.  C2's last
+    rounds and the batman PNG (a later host round partitions nodes the loop
+    finalised) must take the loop."""
+    big = fx.load_json("big.json")
+    if key not in big:
+        pytest.skip("fixture not generated")
+    c = big[key]
+    arrs = fx.load_npz("big.npz")
+    px = fx.xorshift(c["w"] * c["h"])
+    bat = fx.load_png_u32(fx.os.path.join(fx.GOLDEN, "png", "batman.png"))[0]
+    fix = fx.load_json("png.json")["batman"]
+    try:
+        for lmax in (49152, 0):
+            gpu.set_loop_max(lmax)
+            out, ct = _quant_dev(gpu, px, c["k"])
+            assert (gpu.last_loop_rounds() > 0) == (lmax > 0)
+            assert [int(v) for v in ct] == c["ct"]
+            assert "%016x" % fx.fnv(out) == c["out_fnv"]
+            assert np.array_equal(gpu.last_trace(c["k"]), arrs["trace_" + key])
+            _check_centroids(gpu, c["k"], arrs["means_" + key])
+            for k in (16, 125, 256):
+                out, ct = _quant_dev(gpu, bat, k)
+                assert [int(v) for v in ct] == fix["k%d" % k]["ct"], (lmax, k)
+                assert "%016x" % fx.fnv(out) == fix["k%d" % k]["out_fnv"], (lmax, k)
+    finally:
+        gpu.set_loop_max(49152)
+
+
 def test_repeated_runs_identical(gpu):
     """Run-to-run determinism under many fused 2-means launches (fixed points
     off: every node runs all its iterations through kpass_kernel's
