@@ -611,8 +611,6 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   const double tb1 = trace_ ? host_us() : 0.0;
   // one upload kernel on the round's stream (no copy-engine hop)
   launch_upload(dblk, d_stage_view_, bytes, stream);
-  DQ_HIP(hipEventRecord(stage_ev_, stream));
-  stage_pending_ = true;
   if (trace_) tr_build_us_ += host_us() - tb0;
 
   R.seq = ++seq_;
@@ -679,6 +677,11 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     timed_end(ST_PARTITION, part_bytes, stream, (double)parent_total);
   }
   epilogue(PASS_SPLIT, max_iters);
+  // the staging's reuse waits for this event; recorded behind the round's
+  // kernels (stream order: after the upload) so that the host submits the
+  // first kernels without it in between (~6-15 us of GPU idle at a call's start)
+  DQ_HIP(hipEventRecord(stage_ev_, stream));
+  stage_pending_ = true;
   R.t_enq = tb1;
   return ri;
 }
@@ -2061,12 +2064,11 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     if (trace_) tr_mapprep_us_ = host_us() - tm1;
     if (staged.empty()) {
       launch_upload(d_mapstage_, d_mapstage_view_, bytes, stream);
-      DQ_HIP(hipEventRecord(map_ev_, stream));
-      map_pending_ = true;
       const MapTask* dt = reinterpret_cast<const MapTask*>(d_mapstage_);
       timed_begin(stream);
       launch_build_cells(dt, nt, kmax, stream);
       timed_end(ST_CELLS, 0.0, stream);
+      // (the staging-reuse event behind the map's kernels, as for round tables)
       double px = 0, mb = 0;   // pixels; bytes: 4 (BGR24: 3) read + 4 written per pixel
       for (int t = 0; t < nt; ++t) {
         px += ht[t].n;
@@ -2076,6 +2078,8 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       if (lds_map) launch_map_lds(dt, nt, kmax, nblocks, ht[0].bgr != 0, stream);
       else launch_map(dt, nt, kmax, nblocks, stream);
       timed_end(ST_MAP, mb, stream, px);
+      DQ_HIP(hipEventRecord(map_ev_, stream));
+      map_pending_ = true;
     } else {
       // rare path: run the chunk task by task, staging misaligned buffers
       for (int t = 0; t < nt; ++t) {
