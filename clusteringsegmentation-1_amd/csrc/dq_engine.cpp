@@ -27,6 +27,7 @@ void die(const char* what, const char* file, int line, const char* detail) {
 }
 
 namespace {
+constexpr uint64_t kFusePlanMaxPoints = 12u << 20;   // plansplit_kernel: rounds of <= ~one 4K frame
 
 inline double host_us() {
   return std::chrono::duration<double, std::micro>(
@@ -70,6 +71,7 @@ Engine::Engine(int device) : device_(device) {
   if (const char* v = getenv("DQ_HIP_EAGER_REPLAN")) eager_replan_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_STATS_ONLY")) stats_only_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_KLOOP_SHADOW")) kloop_shadow_ = v[0] == '1';
+  if (const char* v = getenv("DQ_HIP_FUSE_PLAN")) fuse_plan_ = v[0] != '0';
   if (const char* v = getenv("DQ_HIP_KLOOP_MAX"))
     kloop_max_ = (uint32_t)std::max<long>(0, std::min<long>((long)kLoopMaxLen, atol(v)));
   DQ_HIP(hipSetDevice(device_));
@@ -186,6 +188,7 @@ char* Engine::arena_alloc(size_t bytes) {
       if (arena_used_ + bytes <= c.second) {
         char* p = c.first + arena_used_;
         arena_used_ += bytes;
+        arena_hw_[arena_chunk_] = std::max(arena_hw_[arena_chunk_], arena_used_);
         return p;
       }
       ++arena_chunk_;
@@ -195,7 +198,9 @@ char* Engine::arena_alloc(size_t bytes) {
     const size_t sz = std::max<size_t>(bytes, (size_t)16 << 20);
     char* p = nullptr;
     DQ_HIP(hipMalloc((void**)&p, sz));
+    DQ_HIP(hipMemset(p, 0, sz));   // (synchronous: zero before any launch uses it)
     arena_.push_back({p, sz});
+    arena_hw_.push_back(0);
   }
 }
 
@@ -833,12 +838,31 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   ra.plane = cap_px_;
   ra.tot_mode = mode;
   ra.ps_mode = R.stats_only ? PS_STATS : PS_FULL;
-  timed_begin(stream);
-  launch_plan(pa, stream);
-  timed_end(ST_PLAN, 0.0, stream);
-  timed_begin(stream);
-  launch_partsplit(ra, (int)R.ptiles_cap, stream);
-  timed_end(ST_PARTITION, part_bytes, stream, (double)total);
+  // the plan and the partition in one launch (arena block zero) for rounds of
+  // about one wave of partition workgroups (4 per CU) over at most one 4K
+  // frame's points: there the plan's launch and round trips are on the
+  // critical path (C3 median 0.557-0.585 -> 0.537-0.544 ms); in the lanes of
+  // a batch (2-3 frames per round) the workgroups' repeated parent scans cost
+  // more than the plan launch they save (8 x 4K: 1.35 -> 1.40-1.42 ms)
+  size_t ptiles = 0;   // the part tiles (the listed records' tiles; prev is assigned)
+  if (P.tbeg.size() == (size_t)P.nr && P.tend.size() == (size_t)P.nr) {
+    for (int32_t a : plist)
+      for (int sh = 0; sh < S; ++sh) ptiles += (size_t)(P.tend[a * S + sh] - P.tbeg[a * S + sh]);
+  } else {
+    ptiles = R.ptiles_cap;
+  }
+  if (fuse_plan_ && S == 1 && ptiles <= (size_t)(6 * num_cus_) && total <= kFusePlanMaxPoints) {
+    timed_begin(stream);
+    launch_plansplit(pa, ra, (int)R.ptiles_cap, stream);
+    timed_end(ST_PARTITION, part_bytes, stream, (double)total);
+  } else {
+    timed_begin(stream);
+    launch_plan(pa, stream);
+    timed_end(ST_PLAN, 0.0, stream);
+    timed_begin(stream);
+    launch_partsplit(ra, (int)R.ptiles_cap, stream);
+    timed_end(ST_PARTITION, part_bytes, stream, (double)total);
+  }
   timed_begin(stream);
   if (mode == TOT_ALLREDUCE) {   // (an aborted round's nodesum writes nothing; every rank
     launch_nodesum(PASS_SPLIT, ra, R.nl, stream);   //  aborts the same rounds: same totals)
@@ -1339,6 +1363,11 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   segs_.clear();
   arena_chunk_ = 0;   // the previous run's tables are dead (its launches were drained)
   arena_used_ = 0;
+  for (size_t c = 0; c < arena_.size(); ++c)   // planned rounds find their block zero
+    if (arena_hw_[c] > 0) {
+      DQ_HIP(hipMemsetAsync(arena_[c].first, 0, arena_hw_[c], stream));
+      arena_hw_[c] = 0;
+    }
   last_rounds = 0;
   last_points_swept = 0;
   last_points_full = 0;

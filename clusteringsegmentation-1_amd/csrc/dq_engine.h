@@ -329,6 +329,11 @@ class Engine {
   // written with ONE copy from the pinned staging buffer.
   std::vector<std::pair<char*, size_t>> arena_;   // chunks
   size_t arena_chunk_ = 0, arena_used_ = 0;
+  // bytes of each chunk the last run used: cleared when the next run starts
+  // (a planned round's counters and counts must be zero on entry to the
+  // fused plan + partition launch, plansplit_kernel)
+  std::vector<size_t> arena_hw_;
+  bool fuse_plan_ = true;             // plansplit_kernel for one-shard planned rounds (DQ_HIP_FUSE_PLAN)
   char* h_stage_ = nullptr;           // pinned
   size_t cap_stage_tab_ = 0;
   TilePartial* d_parts_ = nullptr;    // per tile of the round

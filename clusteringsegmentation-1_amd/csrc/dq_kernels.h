@@ -127,6 +127,11 @@ constexpr int kPlanMaxParents = 6144;
 //                    publishing the plan's counts.
 constexpr int32_t kDebugPrewarm = 1, kDebugUneven = 2, kDebugHostDelay = 4, kDebugPlanStall = 8;   // parents per planned round (LDS scans)
 void launch_plan(const PlanArgs& a, hipStream_t stream);
+// plan_kernel's work and the planned round's partition (PS_FULL / PS_STATS)
+// in one launch of `grid` (= the part tiles' upper bound) workgroups; one
+// shard per node only.  The round block's [LaunchCtr | wparts | rdone] must
+// already be zero.
+void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, hipStream_t stream);
 // Host-built round tables: copy `bytes` from host-coherent pinned staging
 // (device view) into the round's device block on the round's stream (no
 // copy-engine hop between the host and the round's first kernel).

@@ -1100,17 +1100,33 @@ __device__ __forceinline__ void chunk_tile(ChunkAcc& c) {
   c.q = ((c.tend - c.t0 + kSweep - 1) / kSweep) * kWaveSweep;
 }
 
-// (plain pointers: a `const RoundArgs&` parameter made the kernel argument
-// addressable and cost partsplit ~80 VGPRs).  Enters the chunk holding p,
-// the wave's first position in the child.
-__device__ __forceinline__ void chunk_init(ChunkAcc& c, const DevNode* nodes, uint32_t* wparts, int rec,
-                                           uint32_t p) {
-  c.on = rec >= 0;
+// A child's segment and tiling (its record's off, len, tile_len and
+// tile_begin): what the partition's per-(tile, wave) counts need of it.
+struct ChildInfo {
+  uint32_t off, len, tl, tb;
+  int32_t on;               // the child is split this round
+};
+
+__device__ __forceinline__ ChildInfo child_info(const DevNode* nodes, int rec) {
   const DevNode* ch = nodes + (rec >= 0 ? rec : 0);
+  ChildInfo c;
+  c.on = rec >= 0;
   c.off = ch->off;
   c.len = ch->len;
   c.tl = ch->tile_len;
-  c.w0 = wparts + (size_t)ch->tile_begin * kTileWaves;
+  c.tb = (uint32_t)ch->tile_begin;
+  return c;
+}
+
+// (plain values: a `const RoundArgs&` parameter made the kernel argument
+// addressable and cost partsplit ~80 VGPRs).  Enters the chunk holding p,
+// the wave's first position in the child.
+__device__ __forceinline__ void chunk_init(ChunkAcc& c, const ChildInfo& ci, uint32_t* wparts, uint32_t p) {
+  c.on = ci.on != 0;
+  c.off = ci.off;
+  c.len = ci.len;
+  c.tl = ci.tl;
+  c.w0 = wparts + (size_t)ci.tb * kTileWaves;
   c.acc = c.lnew = 0;
   c.k = c.w = 0;
   if (c.on && p < c.off + c.len) {
@@ -1443,8 +1459,8 @@ typedef const __attribute__((address_space(1))) DevNode g_cnode;
 typedef const __attribute__((address_space(1))) Tile g_ctile;
 template <bool PLANAR, bool BGR, int MODE>
 __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g_ctile* tp,
-                                              const DevNode* nodes, uint32_t* wparts, uint64_t plane,
-                                              StageMem* st, SplitSums& so, SplitSums& sn) {
+                                              const ChildInfo& ci0, const ChildInfo& ci1, uint32_t* wparts,
+                                              uint64_t plane, StageMem* st, SplitSums& so, SplitSums& sn) {
   const uint32_t w = wave_id(), l = lane_id();
   uint32_t start, end;   // this wave's range of the parent tile (wave-uniform)
   wave_range(__builtin_amdgcn_readfirstlane(tp->start), __builtin_amdgcn_readfirstlane(tp->end), w, start, end);
@@ -1476,8 +1492,9 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
   constexpr bool kStore = MODE != PS_STATS, kSums = MODE == PS_FULL || MODE == PS_STATS;
   ChunkAcc cx, cy;   // (the children's per-(tile, wave) counts: PS_FULL and PS_STATS)
-  chunk_init(cx, nodes, wparts, kSums ? pt.child[0] : -1, oc0);
-  chunk_init(cy, nodes, wparts, kSums ? pt.child[1] : -1, nc0);
+  ChildInfo off{0u, 0u, 1u, 0u, 0};
+  chunk_init(cx, kSums ? ci0 : off, wparts, oc0);
+  chunk_init(cy, kSums ? ci1 : off, wparts, nc0);
   Stage g;
   constexpr uint32_t kPnOff = kStageRun;
   g.cbo = oc0 & ~15u;
@@ -1576,21 +1593,18 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   chunk_finish(cy);
 }
 
+// One part tile's partition + children's split pass (pt: the parent's tile,
+// record and children; ci0 / ci1: the children's segments and tiling).
 template <int MODE>
-__device__ __forceinline__ void partsplit_body(const RoundArgs& a, uint8_t* stage, uint32_t (*red)[16]) {
-  const PartTile pt = a.ptiles[blockIdx.x];
+__device__ __forceinline__ void partsplit_tile(const RoundArgs& a, const PartTile& pt, const ChildInfo& ci0,
+                                               const ChildInfo& ci1, uint8_t* stage, uint32_t (*red)[16]) {
   g_cnode& nd = *(g_cnode*)pt.parent;
   g_ctile* tp = (g_ctile*)pt.tile;
-  if (MODE == PS_LATE) {   // only parents with a child still active after its split epilogue
-    const bool a0 = pt.child[0] >= 0 && a.nodes[pt.child[0]].done_it == 0;
-    const bool a1 = pt.child[1] >= 0 && a.nodes[pt.child[1]].done_it == 0;
-    if (!a0 && !a1) return;
-  }
   SplitSums so, sn;
   StageMem* st = stage + wave_id() * kStageWave;
-  if (nd.planar == SRC_PLANAR) partsplit_run<true, false, MODE>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
-  else if (nd.planar == SRC_BGR24) partsplit_run<true, true, MODE>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
-  else partsplit_run<false, false, MODE>(pt, nd, tp, a.nodes, a.wparts, a.plane, st, so, sn);
+  if (nd.planar == SRC_PLANAR) partsplit_run<true, false, MODE>(pt, nd, tp, ci0, ci1, a.wparts, a.plane, st, so, sn);
+  else if (nd.planar == SRC_BGR24) partsplit_run<true, true, MODE>(pt, nd, tp, ci0, ci1, a.wparts, a.plane, st, so, sn);
+  else partsplit_run<false, false, MODE>(pt, nd, tp, ci0, ci1, a.wparts, a.plane, st, so, sn);
   if (MODE == PS_WRITE || MODE == PS_LATE) return;   // (no sums: the round's sparts stay)
 
   if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x)) debug_sleep_us(10);
@@ -1611,6 +1625,18 @@ __device__ __forceinline__ void partsplit_body(const RoundArgs& a, uint8_t* stag
     // (2 TilePartials: 16 words)
     __hip_atomic_store(a.sparts[2 * blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+template <int MODE>
+__device__ __forceinline__ void partsplit_body(const RoundArgs& a, uint8_t* stage, uint32_t (*red)[16]) {
+  const PartTile pt = a.ptiles[blockIdx.x];
+  if (MODE == PS_LATE) {   // only parents with a child still active after its split epilogue
+    const bool a0 = pt.child[0] >= 0 && a.nodes[pt.child[0]].done_it == 0;
+    const bool a1 = pt.child[1] >= 0 && a.nodes[pt.child[1]].done_it == 0;
+    if (!a0 && !a1) return;
+  }
+  const ChildInfo ci0 = child_info(a.nodes, pt.child[0]), ci1 = child_info(a.nodes, pt.child[1]);
+  partsplit_tile<MODE>(a, pt, ci0, ci1, stage, red);
 }
 
 __global__ __launch_bounds__(kBlock, 4) void partsplit_kernel(RoundArgs a) {
@@ -1960,6 +1986,145 @@ __device__ void plan_child(const PlanArgs& a, const DevNode& P, const NodeResult
     d->box_hi[c] = hi[c];
   }
 }
+
+// Plan + partition in one launch (one shard per node): the
+// planned round's part tile j is partitioned by workgroup j right after
+// plan_kernel's bookkeeping, restated per workgroup -- every workgroup scans
+// all parents (abort check, the tile counts' exclusive bases), finds the
+// parent of part tile j, and the workgroup of a parent's FIRST part tile
+// writes the parent's two child records and their tiles (read by the next
+// launches only).  The partition itself reads nothing this launch writes:
+// its part tile and the children's segments and tilings are computed here
+// (ChildInfo), so no workgroup waits for another.  Saves plan_kernel's
+// launch and its dependent round trips (~8-10 us per round at C3).  The
+// round's counters, per-(tile, wave) counts and arrival words must be zero
+// on entry (Engine: the run's round arena is cleared when the run starts).
+template <int MODE>
+__device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundArgs& a, uint8_t* stage,
+                                               uint32_t (*red)[16]) {
+  __shared__ uint32_t s_w[kBlock / 64][2];
+  __shared__ uint32_t s_abort;
+  __shared__ int32_t s_par;
+  __shared__ uint32_t s_cb, s_pb;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int32_t np = pa.np;
+  const uint32_t j = blockIdx.x;
+  auto parent = [&](int32_t i) -> int32_t { return pa.plist ? pa.plist[i] : i; };
+  auto ntl = [&](uint32_t len) { return plan_ntiles(len, pa.tl, pa.node_tiles); };
+  if (tid == 0) {
+    s_abort = 0;
+    s_par = -1;
+  }
+  __syncthreads();
+  constexpr int kPer = 4;
+  uint32_t run_t = 0, run_p = 0;
+  bool bad = false;
+  for (int32_t c0 = 0; c0 < np; c0 += kBlock * kPer) {
+    const int32_t i0 = c0 + (int32_t)tid * kPer;
+    uint32_t t[kPer], q[kPer];
+    uint32_t lt = 0, lp = 0;
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+      t[e] = q[e] = 0;
+      if (i0 + e < np) {
+        const DevNode& P = pa.pn[parent(i0 + e)];
+        bad |= P.done_it == 0;
+        const uint32_t nn = P.n_new_local;
+        t[e] = ntl(P.len - nn) + ntl(nn);
+        q[e] = (uint32_t)(P.tile_end - P.tile_begin);
+      }
+      lt += t[e];
+      lp += q[e];
+    }
+    uint32_t it = lt, ip = lp;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(it, o, 64), v = __shfl_up(ip, o, 64);
+      if (lane >= (uint32_t)o) { it += u; ip += v; }
+    }
+    if (lane == 63) { s_w[wv][0] = it; s_w[wv][1] = ip; }
+    __syncthreads();
+    uint32_t bt = run_t + it - lt, bp = run_p + ip - lp;
+    for (uint32_t w = 0; w < wv; ++w) { bt += s_w[w][0]; bp += s_w[w][1]; }
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+      if (i0 + e < np && j >= bp && j < bp + q[e]) {   // (one lane of the grid's chunk owns part tile j)
+        s_par = i0 + e;
+        s_cb = bt;
+        s_pb = bp;
+      }
+      bt += t[e];
+      bp += q[e];
+    }
+    for (int w = 0; w < kBlock / 64; ++w) { run_t += s_w[w][0]; run_p += s_w[w][1]; }
+    __syncthreads();   // (s_w reuse)
+  }
+  if (__any(bad) && lane == 0) s_abort = 1;
+  const bool cancelled = pa.cancel && pa.cancel[2] == 0;
+  __syncthreads();
+  const bool overflow = run_t > pa.tiles_cap || run_p > pa.ptiles_cap;
+  if (j == 0 && tid == 0) {
+    if (pa.debug & kDebugPlanStall) debug_sleep_us(20);
+    const uint32_t ab = cancelled ? 3u : (s_abort ? 1u : (overflow ? 2u : 0u));
+    const uint32_t c[3] = {ab ? 0u : run_t, ab ? 0u : run_p, ab};
+    for (int k = 0; k < 3; ++k) {
+      pa.counts[k] = c[k];
+      __hip_atomic_store(pa.hcounts + k, c[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (cancelled || s_abort || overflow || j >= run_p) return;   // (uniform)
+  const int32_t i = s_par;
+  const uint32_t cb = s_cb, pb = s_pb;
+  const int32_t ai = parent(i);
+  const DevNode* Pp = pa.pn + ai;
+  const NodeResult* rp = pa.pres + ai;
+  const uint32_t nn = Pp->n_new_local, lo = Pp->len - nn, off = Pp->off;
+  const uint32_t nto = ntl(lo), ntn = ntl(nn);
+  const int32_t pe = (int32_t)pb + (Pp->tile_end - Pp->tile_begin);
+  if (j == pb) {   // the parent's first part tile: its children's records and tiles
+    if (tid == 0) plan_child(pa, *Pp, *rp, 0, 2 * i, off, lo, (int32_t)cb, (int32_t)pb, pe);
+    if (tid == 64) plan_child(pa, *Pp, *rp, 1, 2 * i + 1, off + lo, nn, (int32_t)(cb + nto), (int32_t)pb, pe);
+    const uint32_t tlo = plan_tile_len(lo, pa.tl, pa.node_tiles), tln = plan_tile_len(nn, pa.tl, pa.node_tiles);
+    for (uint32_t k = tid; k < nto + ntn; k += kBlock) {
+      const int side = k < nto ? 0 : 1;
+      const uint32_t kk = side ? k - nto : k;
+      const uint32_t coff = side ? off + lo : off, clen = side ? nn : lo, ctl = side ? tln : tlo;
+      Tile* tt = pa.ct + cb + k;
+      tt->node = 2 * i + side;
+      tt->start = coff + kk * ctl;
+      tt->end = coff + min(clen, (kk + 1) * ctl);
+      tt->pad = 0;
+      for (int w = 0; w < kTileWaves; ++w) { tt->old_base[w] = 0; tt->new_base[w] = 0; }
+    }
+  }
+  PartTile pt;
+  pt.tile = pa.ptiles + Pp->tile_begin + (j - pb);
+  pt.parent = Pp;
+  plan_cut(*rp, 0, &pt.thr[0], &pt.shift[0]);
+  plan_cut(*rp, 1, &pt.thr[1], &pt.shift[1]);
+  pt.child[0] = 2 * i;
+  pt.child[1] = 2 * i + 1;
+  if (tid == 0) pa.cpt[j] = pt;   // (for the round's PS_LATE partition)
+  ChildInfo ci0, ci1;
+  ci0.on = ci1.on = 1;
+  ci0.off = off;
+  ci0.len = lo;
+  ci0.tl = plan_tile_len(lo, pa.tl, pa.node_tiles);
+  ci0.tb = cb;
+  ci1.off = off + lo;
+  ci1.len = nn;
+  ci1.tl = plan_tile_len(nn, pa.tl, pa.node_tiles);
+  ci1.tb = cb + nto;
+  partsplit_tile<MODE>(a, pt, ci0, ci1, stage, red);
+}
+
+__global__ __launch_bounds__(kBlock, 4) void plansplit_kernel(PlanArgs pa, RoundArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
+  __shared__ uint32_t red[kTileWaves][16];
+  if (a.ps_mode == PS_STATS) plansplit_body<PS_STATS>(pa, a, stage, red);
+  else plansplit_body<PS_FULL>(pa, a, stage, red);
+}
+
 
 // grid: nb_rec + nb_tile workgroups.  Every workgroup checks that all listed
 // parents are final (else the round aborts) and scans all parents' tile
@@ -2770,6 +2935,11 @@ void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream) {
 void launch_kloop(const RoundArgs& a, int nrec, int max_iters, hipStream_t stream) {
   if (nrec <= 0) return;
   kloop_kernel<<<dim3(nrec), dim3(kLoopBlock), 0, stream>>>(a, max_iters);
+}
+
+void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, hipStream_t stream) {
+  if (grid <= 0) return;
+  plansplit_kernel<<<dim3(grid), dim3(kBlock), 0, stream>>>(pa, a);
 }
 
 void launch_plan(const PlanArgs& a, hipStream_t stream) {
