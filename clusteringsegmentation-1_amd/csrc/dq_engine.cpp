@@ -1363,11 +1363,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   segs_.clear();
   arena_chunk_ = 0;   // the previous run's tables are dead (its launches were drained)
   arena_used_ = 0;
-  for (size_t c = 0; c < arena_.size(); ++c)   // planned rounds find their block zero
-    if (arena_hw_[c] > 0) {
-      DQ_HIP(hipMemsetAsync(arena_[c].first, 0, arena_hw_[c], stream));
-      arena_hw_[c] = 0;
-    }
+  // (the arena is zero here: cleared behind the previous run's last kernel)
   last_rounds = 0;
   last_points_swept = 0;
   last_points_full = 0;
@@ -1564,6 +1560,14 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     }
     if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream);
   }
+  // The next run's planned rounds find their blocks zero: clear what this run
+  // used, behind its last kernel (at the next run's start it delayed the
+  // first round by ~8 us).
+  for (size_t c = 0; c < arena_.size(); ++c)
+    if (arena_hw_[c] > 0) {
+      DQ_HIP(hipMemsetAsync(arena_[c].first, 0, arena_hw_[c], stream));
+      arena_hw_[c] = 0;
+    }
   // Synchronous on return: lookahead launches of the last round may still be
   // queued, and they read the caller's input.
   sync_stream(stream);
