@@ -1565,7 +1565,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   // first round by ~8 us).
   for (size_t c = 0; c < arena_.size(); ++c)
     if (arena_hw_[c] > 0) {
-      DQ_HIP(hipMemsetAsync(arena_[c].first, 0, arena_hw_[c], stream));
+      launch_zero(arena_[c].first, arena_hw_[c], stream);   // (chunks and allocations: 256-B multiples)
       arena_hw_[c] = 0;
     }
   // Synchronous on return: lookahead launches of the last round may still be

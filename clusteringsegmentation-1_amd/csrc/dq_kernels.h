@@ -136,6 +136,9 @@ void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, hipStrea
 // (device view) into the round's device block on the round's stream (no
 // copy-engine hop between the host and the round's first kernel).
 void launch_upload(void* dst, const void* src_dev_view, size_t bytes, hipStream_t stream);
+// Zero `bytes` (a multiple of 16, 16-B aligned) on the stream (hipMemsetAsync
+// cost ~20 us of host time at the end of a call).
+void launch_zero(void* dst, size_t bytes, hipStream_t stream);
 
 // One statistics pass over tiles [0, ntiles) of the round (one workgroup per tile).
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);

@@ -2312,6 +2312,10 @@ __global__ __launch_bounds__(256) void upload_kernel(u32x4* __restrict__ dst, co
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n16; i += gridDim.x * 256u) dst[i] = src[i];
 }
 
+__global__ __launch_bounds__(256) void zero_kernel(u32x4* __restrict__ dst, uint32_t n16) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n16; i += gridDim.x * 256u) dst[i] = (u32x4){0u, 0u, 0u, 0u};
+}
+
 // Map, step 1: per colour cell (8x8x8 values), the palette entries that can
 // be the nearest entry of some colour of the cell.  Two exact filters:
 //   (a) min distance of e to the cell <= the smallest max distance of any
@@ -2946,6 +2950,13 @@ void launch_plan(const PlanArgs& a, hipStream_t stream) {
   const uint32_t nb_rec = (uint32_t)max(1, (a.np * a.nshard + kPlanBlock - 1) / kPlanBlock);
   const uint32_t nb_tile = (max(a.tiles_cap, a.ptiles_cap) + kPlanBlock - 1) / kPlanBlock;
   plan_kernel<<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
+}
+
+void launch_zero(void* dst, size_t bytes, hipStream_t stream) {
+  const uint32_t n16 = (uint32_t)(bytes / 16);
+  if (n16 == 0) return;
+  const uint32_t nb = min(1024u, (n16 + 255u) / 256u);
+  zero_kernel<<<dim3(nb), dim3(256), 0, stream>>>((u32x4*)dst, n16);
 }
 
 void launch_upload(void* dst, const void* src, size_t bytes, hipStream_t stream) {
