@@ -2051,26 +2051,58 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
     }
     // K <= 1024: the LDS-table map, one workgroup per CU over all tasks
     const bool lds_map = kmax <= 1024 && use_lds_map_;
+    auto misaligned = [](const MapJob& j) {
+      return !j.bgr && (((uintptr_t)j.d_in & 15) != 0 || ((uintptr_t)j.d_out & 15) != 0);
+    };
+    // Tasks with the same colortable (a frame's row shards) share one palette
+    // block and one cell table: the table lists the first of each colortable
+    // first (the cell build covers those only), the others after them (block
+    // ranges follow table order).  Not with misaligned buffers (task by task).
+    bool any_mis = false;
+    for (int t = 0; t < nt; ++t) any_mis |= misaligned(jobs[c0 + t]);
+    std::vector<int> order, first(nt, -1), slot(nt);
+    for (int t = 0; t < nt && !any_mis; ++t)
+      for (int u = 0; u < t; ++u)
+        if (first[u] < 0 && jobs[c0 + u].ct == jobs[c0 + t].ct && jobs[c0 + u].k == jobs[c0 + t].k) {
+          first[t] = u;
+          break;
+        }
+    for (int t = 0; t < nt; ++t) if (first[t] < 0) order.push_back(t);
+    const int nbuild = (int)order.size();
+    for (int t = 0; t < nt; ++t) if (first[t] >= 0) order.push_back(t);
+    for (int x = 0; x < nt; ++x) slot[order[x]] = x;
     size_t woff = 0;   // packed blocks
     std::vector<size_t> blk_off(nt), blk_words(nt);
-    for (int t = 0; t < nt; ++t) {
+    for (int x = 0; x < nt; ++x) {
+      const int t = order[x];
       const MapJob& j = jobs[c0 + t];
-      blk_off[t] = woff;
-      blk_words[t] = 768 / 2 + (((size_t)j.k + 3) & ~(size_t)3);
-      woff += blk_words[t];
-      uint32_t* hb = hblk0 + blk_off[t];
-      const uint32_t* db = dblk0 + blk_off[t];
-      sorted_palette(j.ct, j.k, hb + 768 / 2, reinterpret_cast<uint16_t*>(hb));
-      MapTask& m = ht[t];
+      MapTask& m = ht[x];
+      if (first[t] >= 0) {
+        const MapTask& f = ht[slot[first[t]]];
+        blk_off[x] = blk_off[slot[first[t]]];
+        blk_words[x] = blk_words[slot[first[t]]];
+        m.pal = f.pal;
+        m.lut = f.lut;
+        m.cell_rec = f.cell_rec;
+        m.cell_idx = f.cell_idx;
+        m.cell_c32 = f.cell_c32;
+      } else {
+        blk_off[x] = woff;
+        blk_words[x] = 768 / 2 + (((size_t)j.k + 3) & ~(size_t)3);
+        woff += blk_words[x];
+        uint32_t* hb = hblk0 + blk_off[x];
+        const uint32_t* db = dblk0 + blk_off[x];
+        sorted_palette(j.ct, j.k, hb + 768 / 2, reinterpret_cast<uint16_t*>(hb));
+        m.pal = db + 768 / 2;
+        m.lut = reinterpret_cast<const uint16_t*>(db);
+        m.cell_rec = d_cell_rec_ + (size_t)x * kCells * kCellRecWords;
+        m.cell_idx = d_cell_idx_ + (size_t)x * kCells * kCellCap;
+        m.cell_c32 = d_cell_c32_ + (size_t)x * kCells;
+      }
       m.in = j.d_in;
       m.out = j.d_out;
       m.bgr = j.bgr ? 1 : 0;   // (aligned and K <= 1024: never staged)
-      if (!j.bgr && (((uintptr_t)j.d_in & 15) != 0 || ((uintptr_t)j.d_out & 15) != 0)) staged.push_back(t);
-      m.pal = db + 768 / 2;
-      m.lut = reinterpret_cast<const uint16_t*>(db);
-      m.cell_rec = d_cell_rec_ + (size_t)t * kCells * kCellRecWords;
-      m.cell_idx = d_cell_idx_ + (size_t)t * kCells * kCellCap;
-      m.cell_c32 = d_cell_c32_ + (size_t)t * kCells;
+      if (misaligned(j)) staged.push_back(x);   // (identity order)
       m.n = j.n;
       m.k = j.k;
       const uint32_t groups = j.n / 8;
@@ -2099,7 +2131,7 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       launch_upload(d_mapstage_, d_mapstage_view_, bytes, stream);
       const MapTask* dt = reinterpret_cast<const MapTask*>(d_mapstage_);
       timed_begin(stream);
-      launch_build_cells(dt, nt, kmax, stream);
+      launch_build_cells(dt, nbuild, kmax, stream);
       timed_end(ST_CELLS, 0.0, stream);
       // (the staging-reuse event behind the map's kernels, as for round tables)
       double px = 0, mb = 0;   // pixels; bytes: 4 (BGR24: 3) read + 4 written per pixel

@@ -2138,8 +2138,11 @@ __global__ __launch_bounds__(kBlock, 4) void plansplit_kernel(PlanArgs pa, Round
 // are logical nodes 2i (old half) and 2i+1 (new half) with records
 // (2i+side)*S + s, tiles in record order (old half's shards, then the new
 // half's), part tiles in the parent's record order -- Engine::enqueue_host_
-// round's layout.
+// round's layout.  SH (S > 1): each node's S records are read as kMaxShard
+// clamped loads issued together (then masked by shard < S), not a walk of
+// dependent loads: with 8 shards the walks made the plan ~35 us per round.
 constexpr int kPlanBlock = 256;
+template <bool SH>
 __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t nb_rec) {
   __shared__ uint32_t s_cb[kPlanMaxParents + 1];   // children's tiles before parent i
   __shared__ uint32_t s_pb[kPlanMaxParents + 1];   // part tiles before parent i
@@ -2156,7 +2159,9 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
   // (1) every parent final? exclusive scans of the tile counts, chunk by
   //     chunk; a lane takes kPlanPer consecutive parents of a chunk (all their
   //     loads in flight together)
-  constexpr int kPlanPer = 4;
+  constexpr int kPlanPer = SH ? 2 : 4;
+  constexpr int SM = SH ? kMaxShard : 1;   // shard records read per node
+  auto shard = [&](int x) -> int { return SH ? min(x, S - 1) : 0; };
   uint32_t run_t = 0, run_p = 0;
   bool bad = false;
   for (int32_t c0 = 0; c0 < np; c0 += kPlanBlock * kPlanPer) {
@@ -2169,11 +2174,13 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
       if (i0 + e < np) {
         const DevNode* P0 = a.pn + (size_t)parent(i0 + e) * S;
         bad |= P0->done_it == 0;   // (every shard record of a node agrees)
-        for (int sh = 0; sh < S; ++sh) {
-          const DevNode& P = P0[sh];
+#pragma unroll
+        for (int sh = 0; sh < SM; ++sh) {
+          const DevNode& P = P0[shard(sh)];
           const uint32_t nn = P.n_new_local;
-          t[e] += ntl(P.len - nn) + ntl(nn);
-          q[e] += (uint32_t)(P.tile_end - P.tile_begin);
+          const bool on = !SH || sh < S;
+          t[e] += on ? ntl(P.len - nn) + ntl(nn) : 0u;
+          q[e] += on ? (uint32_t)(P.tile_end - P.tile_begin) : 0u;
         }
       }
       lt += t[e];
@@ -2225,15 +2232,18 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     const int32_t i = u / S, sh = u - i * S;
     const int32_t ai = parent(i) * S;
     uint32_t told = 0, tnew_all = 0, tnew = 0, pbo = 0;   // tiles / part tiles before this shard's
-    for (int x = 0; x < S; ++x) {
-      const DevNode& Q = a.pn[ai + x];
+#pragma unroll
+    for (int x = 0; x < SM; ++x) {
+      const DevNode& Q = a.pn[ai + shard(x)];
+      const bool on = !SH || x < S;
       const uint32_t nn = Q.n_new_local;
-      if (x < sh) {
-        told += ntl(Q.len - nn);
-        tnew += ntl(nn);
-        pbo += (uint32_t)(Q.tile_end - Q.tile_begin);
+      const uint32_t to = ntl(Q.len - nn), tn = ntl(nn), pq = (uint32_t)(Q.tile_end - Q.tile_begin);
+      if (on && x < sh) {
+        told += to;
+        tnew += tn;
+        pbo += pq;
       }
-      tnew_all += ntl(Q.len - nn);
+      tnew_all += on ? to : 0u;
     }
     const DevNode& P = a.pn[ai + sh];
     const NodeResult& r = a.pres[ai + sh];
@@ -2258,18 +2268,31 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     const int32_t ai = parent(i) * S;
     uint32_t k = j - s_cb[i];
     // the child record holding slot k: old half's shards, then the new half's
+    uint32_t qlo[SM], qnn[SM], qoff[SM];
+#pragma unroll
+    for (int x = 0; x < SM; ++x) {
+      const DevNode& Q = a.pn[ai + shard(x)];
+      qnn[x] = Q.n_new_local;
+      qlo[x] = Q.len - qnn[x];
+      qoff[x] = Q.off;
+    }
     int side = 0, sh = 0;
     uint32_t off = 0, len = 0;
-    for (int v = 0; v < 2 * S; ++v) {
-      const DevNode& Q = a.pn[ai + (v % S)];
-      const uint32_t nn = Q.n_new_local, lo = Q.len - nn;
-      const uint32_t l = v < S ? lo : nn, nt = ntl(l);
-      side = v < S ? 0 : 1;
-      sh = v % S;
-      off = v < S ? Q.off : Q.off + lo;
-      len = l;
-      if (k < nt) break;
-      k -= nt;
+    bool found = false;
+#pragma unroll
+    for (int v = 0; v < 2 * SM; ++v) {
+      const int nw = v >= SM ? 1 : 0, x = nw ? v - SM : v;
+      if (found || (SH && x >= S)) continue;
+      const uint32_t l = nw ? qnn[x] : qlo[x], nt = ntl(l);
+      if (k < nt) {
+        found = true;
+        side = nw;
+        sh = x;
+        off = nw ? qoff[x] + qlo[x] : qoff[x];
+        len = l;
+      } else {
+        k -= nt;
+      }
     }
     const uint32_t tln = plan_tile_len(len, a.tl, a.node_tiles);
     Tile* tt = a.ct + j;
@@ -2283,11 +2306,16 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     const int32_t i = find(s_pb, j);
     const int32_t ai = parent(i) * S;
     uint32_t k = j - s_pb[i];
+    uint32_t qnt[SM];
+#pragma unroll
+    for (int x = 0; x < SM; ++x) qnt[x] = (uint32_t)(a.pn[ai + shard(x)].tile_end - a.pn[ai + shard(x)].tile_begin);
     int sh = 0;
-    for (; sh < S - 1; ++sh) {
-      const uint32_t nt = (uint32_t)(a.pn[ai + sh].tile_end - a.pn[ai + sh].tile_begin);
-      if (k < nt) break;
-      k -= nt;
+    bool stop = false;
+#pragma unroll
+    for (int x = 0; x < SM - 1; ++x) {
+      if (stop || x >= S - 1) continue;
+      if (k < qnt[x]) stop = true;
+      else { k -= qnt[x]; sh = x + 1; }
     }
     const DevNode& P = a.pn[ai + sh];
     const NodeResult& r = a.pres[ai + sh];
@@ -2949,7 +2977,8 @@ void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, hipStrea
 void launch_plan(const PlanArgs& a, hipStream_t stream) {
   const uint32_t nb_rec = (uint32_t)max(1, (a.np * a.nshard + kPlanBlock - 1) / kPlanBlock);
   const uint32_t nb_tile = (max(a.tiles_cap, a.ptiles_cap) + kPlanBlock - 1) / kPlanBlock;
-  plan_kernel<<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
+  if (a.nshard > 1) plan_kernel<true><<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
+  else plan_kernel<false><<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
 }
 
 void launch_zero(void* dst, size_t bytes, hipStream_t stream) {
