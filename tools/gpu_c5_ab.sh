@@ -1,6 +1,6 @@
 set -e -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/c5ab; mkdir -p $O
+O=gpurun_out/${C5AB_TAG:-c5ab}; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_rows.py tests/test_gpu_atsize.py tests/test_gpu_handoff.py -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 for i in 1 2; do
