@@ -16,7 +16,8 @@ Reference-named entry points (same argument meaning, host numpy arrays):
 Device-resident entry points (torch tensors / raw device pointers on HBM):
     quant_device, quant_batch_device, cluster_device, map_device
 Row-tile sharding (one frame over shards / GPUs, RCCL allreduce per pass):
-    quant_rows_device, comm_init_torch (comm_unique_id, comm_init, comm_destroy)
+    quant_rows_device, comm_init_torch (comm_unique_id, comm_init, comm_destroy);
+    loopback_rows_device (tests: N ranks in one process, loopback collective)
 Full-frame block histograms (genHistogramsForBlocks):
     get_subdivided_colors, gen_histograms_for_blocks, block_hist_device
 BGR24 (OpenCV CV_8UC3) ingestion / output on the GPU (Vec3BToUID / PixelToVec3b):
@@ -118,6 +119,8 @@ def lib():
         "quant_recurse": ([c.c_uint32, vp, vp, u32p, vp, c.c_int], None),
         "dq_hip_build_id": ([], c.c_uint64),
         "dq_hip_set_debug": ([c.c_int, c.c_int], None),
+        "dq_hip_loopback_rows_dev": ([c.c_int, c.c_int, c.c_int, vp, c.c_uint32, c.c_uint32, vp, c.c_uint32,
+                                      vp, vp, c.c_int, vp, c.c_int, vp], c.c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -327,6 +330,35 @@ def quant_rows_device(t_ins, t_outs, num_clusters, widths=None, n_globals=None, 
     if r < 0:
         raise DivQuantError("dq_hip_quant_rows_dev: bad arguments")
     return [ct[i, :kout[i]].copy() for i in range(nf)], r
+
+
+def loopback_rows_device(t_ins, t_outs, width, height, num_clusters, nranks, max_iters=10, device=0,
+                         log_cap=8192):
+    """Test-only: row-tile sharding of `nranks` processes, run as nranks
+    engines of this process on `device` (own stream and host thread each)
+    joined by the in-process loopback collective instead of RCCL -- the
+    TOT_ALLREDUCE path with every rank's local counts != the global totals.
+    t_ins / t_outs: whole width x height frames; rank r maps its rows
+    [r*H/N, (r+1)*H/N) into t_outs.  Returns (cts, logs, empty): cts[r][i] =
+    rank r's colortable of frame i, logs[r] = the element counts of the
+    collectives rank r enqueued, in order."""
+    nf = len(t_ins)
+    ins = (ctypes.c_void_p * nf)(*[_dptr(t).value for t in t_ins])
+    outs = (ctypes.c_void_p * nf)(*[_dptr(t).value for t in t_outs])
+    ct = np.zeros((nranks, nf, num_clusters), np.uint32)
+    kout = np.zeros((nranks, nf), np.uint32)
+    log = np.zeros((nranks, log_cap), np.uint64)
+    nlog = np.zeros(nranks, np.int32)
+    r = lib().dq_hip_loopback_rows_dev(device, nranks, nf, ctypes.cast(ins, ctypes.c_void_p), width, height,
+                                       ctypes.cast(outs, ctypes.c_void_p), num_clusters, _ptr(ct), _ptr(kout),
+                                       max_iters, _ptr(log), log_cap, _ptr(nlog))
+    if r < 0:
+        raise DivQuantError("dq_hip_loopback_rows_dev: bad arguments")
+    if nlog.max() > log_cap:
+        raise DivQuantError("collective log longer than log_cap")
+    cts = [[ct[q, i, :kout[q, i]].copy() for i in range(nf)] for q in range(nranks)]
+    logs = [log[q, :nlog[q]].tolist() for q in range(nranks)]
+    return cts, logs, r
 
 
 def comm_unique_id():
@@ -567,7 +599,8 @@ def build_id():
 def set_debug(flags, device=0):
     """Test-only interleaving knobs (dq_hip.h dq_hip_set_debug; 0 in production):
     1 prewarm the 2-means hand-off lines, 2 uneven workgroup stalls, 4 host
-    delays between a round's status and its results, 8 plan-kernel stall."""
+    delays between a round's status and its results, 8 plan-kernel stall,
+    16 check that the round arena is all zero when a run starts."""
     lib().dq_hip_set_debug(device, int(flags))
 
 

@@ -29,6 +29,7 @@
 
 #include <rccl/rccl.h>
 #include <map>
+#include <tuple>
 
 using dq::Engine;
 using dq::engine_for;
@@ -558,6 +559,84 @@ int dq_hip_quant_rows_dev(int device, int nframes, const uint32_t* const* d_in,
     empty += jobs[i].num_empty;
   }
   return empty;
+}
+
+// Test-only (dq_hip.h): row-tile sharding over nranks in-process ranks of
+// one device, joined by the loopback collective (dq_engine.h Loopback).
+// Rank r holds rows [r*H/N, (r+1)*H/N) of every frame (bench.py row_range),
+// runs them on its own engine, stream and host thread with n_global = W*H,
+// and maps them into its rows of d_out.
+int dq_hip_loopback_rows_dev(int device, int nranks, int nframes, const uint32_t* const* d_in,
+                             uint32_t width, uint32_t height, uint32_t* const* d_out, uint32_t k,
+                             uint32_t* ct, uint32_t* k_out, int max_iters, uint64_t* coll_log,
+                             int log_cap, int* log_len) {
+  if (nranks < 1 || nranks > dq::kMaxShard || nframes <= 0 || !d_in || !d_out || !ct || !k_out || k == 0 ||
+      max_iters < 1 || width == 0 || height < (uint32_t)nranks || (uint64_t)width * height >= (1ull << 32))
+    return -1;
+  for (int i = 0; i < nframes; ++i)
+    if (!d_in[i] || !d_out[i]) return -1;
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int>, Engine*> engines;
+  static std::map<std::pair<int, int>, dq::Loopback*> groups;
+  std::lock_guard<std::mutex> call(mu);
+  DQ_HIP(hipSetDevice(device));
+  dq::Loopback*& grp = groups[{device, nranks}];
+  if (!grp) grp = new dq::Loopback(nranks, device);
+  grp->reset_log();
+  std::vector<Engine*> es(nranks);
+  for (int r = 0; r < nranks; ++r) {
+    Engine*& e = engines[std::make_tuple(device, nranks, r)];
+    if (!e) e = new Engine(device);
+    es[r] = e;
+  }
+  // inputs may still be in flight on the legacy default stream
+  hipEvent_t ready = events().get();
+  DQ_HIP(hipEventRecord(ready, nullptr));
+  for (Engine* e : es) DQ_HIP(hipStreamWaitEvent(e->stream(), ready, 0));
+  events().put(ready);
+  const uint64_t ng = (uint64_t)width * height;
+  std::vector<int> empty(nranks, 0);
+  auto work = [&](int r) {
+    Engine& e = *es[r];
+    DQ_HIP(hipSetDevice(device));
+    std::lock_guard<std::mutex> g(e.mutex());
+    const uint32_t r0 = (uint32_t)((uint64_t)height * r / nranks), r1 = (uint32_t)((uint64_t)height * (r + 1) / nranks);
+    std::vector<dq::FrameJob> jobs(nframes);
+    for (int i = 0; i < nframes; ++i) {
+      jobs[i].d_in = d_in[i] + (size_t)r0 * width;
+      jobs[i].n = (r1 - r0) * width;
+      jobs[i].d_out = d_out[i] + (size_t)r0 * width;
+      jobs[i].k = (int)k;
+      jobs[i].ct = ct + ((size_t)r * nframes + i) * k;
+      jobs[i].width = width;
+      jobs[i].n_global = ng;
+    }
+    e.set_loopback(grp, r);
+    e.run(jobs.data(), nframes, max_iters, true, e.stream());
+    e.set_loopback(nullptr, 0);
+    for (int i = 0; i < nframes; ++i) {
+      k_out[(size_t)r * nframes + i] = (uint32_t)jobs[i].k_out;
+      empty[r] += jobs[i].num_empty;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int r = 1; r < nranks; ++r) th.emplace_back(work, r);
+  work(0);
+  for (auto& t : th) t.join();
+  for (int r = 0; r < nranks; ++r) {
+    if (log_len) log_len[r] = (int)grp->log[r].size();
+    if (coll_log)
+      for (int c = 0; c < log_cap && c < (int)grp->log[r].size(); ++c) coll_log[(size_t)r * log_cap + c] = grp->log[r][c];
+  }
+  {   // rank 0's diagnostics of its last frame on the device's lane-0 engine (dq_hip_last_*)
+    Engine& e0 = engine_for(device);
+    std::lock_guard<std::mutex> g(e0.mutex());
+    e0.last_means = es[0]->last_means;
+    e0.last_sizes = es[0]->last_sizes;
+    e0.last_trace = es[0]->last_trace;
+    e0.last_rounds = es[0]->last_rounds;
+  }
+  return empty[0];
 }
 
 int dq_hip_comm_unique_id(void* id128) {

@@ -15,14 +15,24 @@
 #include <chrono>
 #include <deque>
 #include <functional>
+#include <string>
 #include <unordered_set>
 
 namespace dq {
 
+// The message also goes to the file DQ_HIP_DIE_LOG names (appended, flushed
+// before the abort): a test runner that captures stderr loses it otherwise.
 void die(const char* what, const char* file, int line, const char* detail) {
   std::fprintf(stderr, "divquant-hip: fatal: %s (%s:%d): %s\n", what, file, line,
                detail ? detail : "");
   std::fflush(stderr);
+  if (const char* path = getenv("DQ_HIP_DIE_LOG")) {
+    if (FILE* f = std::fopen(path, "a")) {
+      std::fprintf(f, "divquant-hip: fatal: %s (%s:%d): %s\n", what, file, line, detail ? detail : "");
+      std::fflush(f);
+      std::fclose(f);
+    }
+  }
   std::abort();
 }
 
@@ -52,28 +62,47 @@ int32_t split_threshold(double cut) {
 
 }  // namespace
 
+// Experiment switches, all behind ONE entry point: DQ_HIP_TUNE is a list of
+// key=value pairs ("tiles=768,lookahead=1").  Every setting leaves the
+// outputs identical (they move work between launches, not arithmetic); the
+// defaults are the measured best.  Unknown keys abort, so a
+// misspelt experiment cannot silently measure the default.
+void Engine::apply_tune(const char* spec) {
+  std::string all(spec);
+  size_t pos = 0;
+  while (pos < all.size()) {
+    size_t end = all.find(',', pos);
+    if (end == std::string::npos) end = all.size();
+    const std::string kv = all.substr(pos, end - pos);
+    pos = end + 1;
+    if (kv.empty()) continue;
+    const size_t eq = kv.find('=');
+    DQ_CHECK(eq != std::string::npos, "DQ_HIP_TUNE entries are key=value");
+    const std::string k = kv.substr(0, eq);
+    const long v = atol(kv.c_str() + eq + 1);
+    if (k == "full_iters") fixed_point_ = v == 0;                       // every 2-means iteration runs
+    else if (k == "plan") plan_ = v != 0;                               // device-planned rounds
+    else if (k == "tiles") tiles_target_ = std::max<long>(64, v);      // tiles per big round
+    else if (k == "node_tiles") node_tiles_ = std::max<long>(1, v);    // tiles per record at least
+    else if (k == "tile_max")                                           // points per tile at most
+      tile_max_ = (uint32_t)std::max<long>(kSweep, std::min<long>(kMaxTilePx, v)) / kSweep * kSweep;
+    else if (k == "lds_map") use_lds_map_ = v != 0;                     // 0: the L2-gather map kernel
+    else if (k == "lookahead") lookahead_ = (int)std::max<long>(0, std::min<long>(8, v));
+    else if (k == "spec_kmeans") speculate_kmeans_ = v != 0;
+    else if (k == "spin_sync") spin_sync_ = v != 0;
+    else if (k == "eager_replan") eager_replan_ = v != 0;
+    else if (k == "stats_only") stats_only_ = v != 0;
+    else if (k == "fuse_plan") fuse_plan_ = v != 0;
+    else if (k == "kloop_max") kloop_max_ = (uint32_t)std::max<long>(0, std::min<long>(kLoopMaxLen, v));
+    else die("DQ_HIP_TUNE", __FILE__, __LINE__, ("unknown key " + k).c_str());
+  }
+}
+
 Engine::Engine(int device) : device_(device) {
-  const char* full = getenv("DQ_HIP_FULL_ITERS");
-  fixed_point_ = !(full && full[0] == '1');
   const char* tr = getenv("DQ_HIP_TRACE");
   trace_ = tr && (tr[0] == '1' || tr[0] == '2');
   trace_rounds_ = tr && tr[0] == '2';
-  if (const char* v = getenv("DQ_HIP_TILES")) tiles_target_ = std::max(64, atoi(v));
-  if (const char* v = getenv("DQ_HIP_NODE_TILES")) node_tiles_ = std::max(1, atoi(v));
-  if (const char* v = getenv("DQ_HIP_TILE_MAX"))
-    tile_max_ = (uint32_t)std::max<int>(kSweep, std::min<int>((int)kMaxTilePx, atoi(v))) / kSweep * kSweep;
-  if (const char* v = getenv("DQ_HIP_LDS_MAP")) use_lds_map_ = v[0] != '0';
-  const char* la = getenv("DQ_HIP_LOOKAHEAD");
-  if (la && la[0]) lookahead_ = std::max(0, std::min(8, atoi(la)));
-  if (const char* v = getenv("DQ_HIP_SPEC_KMEANS")) speculate_kmeans_ = v[0] != '0';
-  if (const char* v = getenv("DQ_HIP_SPIN_SYNC")) spin_sync_ = v[0] != '0';
-  if (const char* v = getenv("DQ_HIP_PLAN")) plan_ = v[0] != '0';
-  if (const char* v = getenv("DQ_HIP_EAGER_REPLAN")) eager_replan_ = v[0] != '0';
-  if (const char* v = getenv("DQ_HIP_STATS_ONLY")) stats_only_ = v[0] != '0';
-  if (const char* v = getenv("DQ_HIP_KLOOP_SHADOW")) kloop_shadow_ = v[0] == '1';
-  if (const char* v = getenv("DQ_HIP_FUSE_PLAN")) fuse_plan_ = v[0] != '0';
-  if (const char* v = getenv("DQ_HIP_KLOOP_MAX"))
-    kloop_max_ = (uint32_t)std::max<long>(0, std::min<long>((long)kLoopMaxLen, atol(v)));
+  if (const char* t = getenv("DQ_HIP_TUNE")) apply_tune(t);
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   DQ_HIP(hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_));
@@ -135,6 +164,27 @@ void Engine::debug_host_delay() const {
   if (!(debug_ & kDebugHostDelay)) return;
   const double t0 = host_us();
   while (host_us() - t0 < 200.0) __builtin_ia32_pause();
+}
+
+// kDebugArenaCheck (tests): the round arena must be all zero when a run
+// starts -- every byte a planned round's fused plan + partition expects to
+// find cleared (its counters, per-(tile, wave) counts, arrival words) lies
+// in it, and nothing but the previous run's end-of-run clear restores it.
+void Engine::check_arena_zero(hipStream_t stream) {
+  DQ_HIP(hipStreamSynchronize(stream));
+  DQ_HIP(hipDeviceSynchronize());   // (the previous run's clear may be on another stream)
+  std::vector<uint64_t> h;
+  for (size_t c = 0; c < arena_.size(); ++c) {
+    h.resize(arena_[c].second / 8);
+    DQ_HIP(hipMemcpy(h.data(), arena_[c].first, h.size() * 8, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < h.size(); ++i)
+      if (h[i] != 0) {
+        char msg[200];
+        std::snprintf(msg, sizeof msg, "chunk %zu of %zu (%zu B): non-zero word 0x%016llx at byte %zu", c,
+                      arena_.size(), arena_[c].second, (unsigned long long)h[i], i * 8);
+        die("round arena not zero at run entry", __FILE__, __LINE__, msg);
+      }
+  }
 }
 
 void Engine::reset_stats() {
@@ -290,7 +340,7 @@ void Engine::ensure_totals(size_t nlogical, hipStream_t stream) {
 // active.  Bounded: once the stream has drained the word must be there.
 // The end of a call: an event on the stream, polled with pause (the host's
 // status-word waits spin the same way); hipStreamSynchronize's blocking wait
-// woke the host tens of microseconds after the last kernel (DQ_HIP_SPIN_SYNC=0:
+// woke the host tens of microseconds after the last kernel (DQ_HIP_TUNE spin_sync=0:
 // hipStreamSynchronize).
 void Engine::sync_stream(hipStream_t stream) {
   if (!spin_sync_) {
@@ -949,7 +999,7 @@ bool Engine::loop_ok(const Round& R) const {
   // (one workgroup per record on one CU: a 2-means pass costs it ~0.1 us per
   // 1000 points of VALU work, so only small records in rounds of at most one
   // record per CU beat the ~11 us of a kpass launch per iteration)
-  if (kloop_max_ == 0 || nshard_ != 1 || comm_ || R.root || R.nr > num_cus_) return false;
+  if (kloop_max_ == 0 || nshard_ != 1 || cross_process() || R.root || R.nr > num_cus_) return false;
   for (int a = 0; a < R.nl; ++a) {
     const int id = R.order[a];
     if (nodes_[id].buf == BUF_IN) return false;   // (a root's packed / BGR24 frame)
@@ -966,63 +1016,6 @@ void Engine::kmeans_loop(Round& R, int max_iters, hipStream_t stream) {
   if (timing_) R.loop_event = (long)pending_.size() - 1;
 }
 
-void Engine::shadow_launch(Round& R, int max_iters, hipStream_t stream) {
-  const size_t need = R.nr * sizeof(DevNode) + R.ntiles * sizeof(Tile) + R.nr * sizeof(NodeResult) + 256;
-  if (need > cap_shadow_) {
-    DQ_HIP(hipStreamSynchronize(stream));
-    if (d_shadow_) DQ_HIP(hipFree(d_shadow_));
-    DQ_HIP(hipMalloc(&d_shadow_, 2 * need));
-    cap_shadow_ = 2 * need;
-  }
-  RoundArgs sa = R.ra;
-  char* p = static_cast<char*>(d_shadow_);
-  sa.shadow_nodes = reinterpret_cast<DevNode*>(p);
-  sa.shadow_tiles = reinterpret_cast<Tile*>(p + ((R.nr * sizeof(DevNode) + 63) & ~(size_t)63));
-  sa.shadow_res = reinterpret_cast<NodeResult*>(reinterpret_cast<char*>(sa.shadow_tiles) +
-                                                ((R.ntiles * sizeof(Tile) + 63) & ~(size_t)63));
-  DQ_HIP(hipMemsetAsync(d_shadow_, 0, need, stream));
-  launch_kloop(sa, R.nr, max_iters, stream);
-}
-
-void Engine::shadow_compare(Round& R) {
-  DQ_HIP(hipDeviceSynchronize());
-  std::vector<DevNode> sn(R.nr), rn(R.nr);
-  std::vector<Tile> st(R.ntiles), rt(R.ntiles);
-  std::vector<NodeResult> sr(R.nr);
-  char* p = static_cast<char*>(d_shadow_);
-  const size_t ot = (R.nr * sizeof(DevNode) + 63) & ~(size_t)63;
-  const size_t orr = ot + ((R.ntiles * sizeof(Tile) + 63) & ~(size_t)63);
-  DQ_HIP(hipMemcpy(sn.data(), p, R.nr * sizeof(DevNode), hipMemcpyDeviceToHost));
-  DQ_HIP(hipMemcpy(st.data(), p + ot, R.ntiles * sizeof(Tile), hipMemcpyDeviceToHost));
-  DQ_HIP(hipMemcpy(sr.data(), p + orr, R.nr * sizeof(NodeResult), hipMemcpyDeviceToHost));
-  DQ_HIP(hipMemcpy(rn.data(), R.dn, R.nr * sizeof(DevNode), hipMemcpyDeviceToHost));
-  DQ_HIP(hipMemcpy(rt.data(), R.dt, R.ntiles * sizeof(Tile), hipMemcpyDeviceToHost));
-  const NodeResult* res = h_res_ + (size_t)R.par * cap_res_;
-  int bad = 0, checked = 0;
-  for (int r = 0; r < R.nr; ++r) {
-    if (res[r].proven) continue;   // final at the split: kloop skipped it
-    ++checked;
-    const DevNode& a = sn[r];
-    const DevNode& b = rn[r];
-    char why[256] = "";
-    if (a.n_new_local != b.n_new_local) std::snprintf(why, sizeof why, "n_new_local %u vs %u", a.n_new_local, b.n_new_local);
-    else if (a.done_it != b.done_it) std::snprintf(why, sizeof why, "done_it %d vs %d", a.done_it, b.done_it);
-    else if (std::memcmp(&a.prm, &b.prm, sizeof(Params)) != 0) std::snprintf(why, sizeof why, "prm");
-    else if (std::memcmp(&sr[r], &res[r], offsetof(NodeResult, pad)) != 0) std::snprintf(why, sizeof why, "result");
-    else
-      for (int i = b.tile_begin; i < b.tile_end && !why[0]; ++i)
-        if (std::memcmp(st[i].old_base, rt[i].old_base, sizeof rt[i].old_base) != 0 ||
-            std::memcmp(st[i].new_base, rt[i].new_base, sizeof rt[i].new_base) != 0)
-          std::snprintf(why, sizeof why, "tile %d cursors (old_base[0] %u vs %u, new_base[0] %u vs %u)", i,
-                        st[i].old_base[0], rt[i].old_base[0], st[i].new_base[0], rt[i].new_base[0]);
-    if (why[0] && bad++ < 8)
-      std::fprintf(stderr, "divquant-hip shadow: seq %llu record %d (len %u, tiles %d): %s\n",
-                   (unsigned long long)R.seq, r, b.len, b.tile_end - b.tile_begin, why);
-  }
-  std::fprintf(stderr, "divquant-hip shadow: seq %llu records %d checked %d mismatched %d\n",
-               (unsigned long long)R.seq, R.nr, checked, bad);
-}
-
 // Wait for a round's split epilogue, run its 2-means iterations if any record
 // is still active (host-polled, `lookahead_` launched past the one awaited),
 // then take its results: children nodes, segments, the parents' tiles.
@@ -1037,18 +1030,12 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   bool all_proven = false;
   // Late rounds (small records): every 2-means iteration in one launch,
   // waited for on the status word of iteration max_iters - 1
-  const bool shadow = fixed_point_ && kloop_shadow_ && loop_ok(R);
-  const bool loop = fixed_point_ && !kloop_shadow_ && loop_ok(R);
-  bool shadowed = false;
+  const bool loop = fixed_point_ && loop_ok(R);
   // Nothing else queued behind this round (a frame's last rounds): its first
   // 2-means iterations go in before its split status is known -- a record
   // final at the split makes them exit at once (~4 us each); C3's last round
   // needs them and otherwise waited ~15 us for the host to see the status.
   if (speculate && fixed_point_) {
-    if (shadow) {
-      shadow_launch(R, max_iters, stream);
-      shadowed = true;
-    }
     if (loop) {
       kmeans_loop(R, max_iters, stream);
       launched = max_iters;
@@ -1067,11 +1054,6 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   }
   debug_host_delay();
   R.kmeans = !all_proven;
-  const bool all_proven_split = all_proven;
-  if (shadow && !shadowed && !all_proven) {
-    shadow_launch(R, max_iters, stream);
-    shadowed = true;
-  }
   // A planned successor queued behind this round aborts when a record it
   // splits is still active after the split epilogue (nearly always so when
   // 2-means runs).  Then every remaining iteration goes in now (a record final
@@ -1174,7 +1156,6 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
     collect_timing();
   }
 
-  if (shadowed && !all_proven_split) shadow_compare(R);
   if (R.stats_only)   // written by PS_LATE iff the node or its sibling was active after its split
     for (int a = 0; a + 1 < nl; a += 2) {
       const bool written = !(res[a * S].proven && res[(a + 1) * S].proven);
@@ -1357,6 +1338,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   DQ_HIP(hipSetDevice(device_));
   if (!stream) stream = stream_;
   debug_ = debug_flags();
+  if (debug_ & kDebugArenaCheck) check_arena_zero(stream);
 
   frames_.assign(nframes, FrameState());
   nodes_.clear();
@@ -1378,7 +1360,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     DQ_CHECK(j.d_in && j.ct, "null buffer");
     DQ_CHECK(j.nshard == S, "every frame of a batch must have the same shard count");
     DQ_CHECK(j.n_global == 0 || j.n_global >= j.n, "n_global < n");
-    DQ_CHECK(j.n_global == 0 || j.n_global == j.n || comm_ != nullptr,
+    DQ_CHECK(j.n_global == 0 || j.n_global == j.n || cross_process(),
              "n_global > n needs a communicator (dq_hip_comm_init)");
     DQ_CHECK(!j.bgr || (S == 1 && (j.n_global == 0 || j.n_global == j.n)), "BGR24 frames are one shard");
     FrameState& f = frames_[i];
@@ -1896,9 +1878,96 @@ void Engine::comm_destroy() {
 // The per-pass exchange of row-tile sharding: the logical nodes' 8 u64
 // totals summed over all processes, in place, on the round's stream.
 void Engine::allreduce_totals(int nlogical, hipStream_t stream) {
+  if (loop_) {
+    loop_->allreduce(loop_rank_, d_tot_, (size_t)nlogical * 8, stream);
+    return;
+  }
   const ncclResult_t r = ncclAllReduce(d_tot_, d_tot_, (size_t)nlogical * 8, ncclUint64, ncclSum,
                                        (ncclComm_t)comm_, stream);
   if (r != ncclSuccess) die("ncclAllReduce", __FILE__, __LINE__, ncclGetErrorString(r));
+}
+
+// ---------------------------------------------------------------------------
+// Loopback collective (tests; dq_engine.h).  One allreduce, per rank r:
+//   1. record in_ev[r] behind r's producers (nodesum / kpass) on r's stream;
+//   2. barrier: every rank has recorded its in_ev and published its buffer;
+//   3. r's stream waits for every in_ev, sums all ranks' buffers into its own
+//      scratch, records rd_ev[r];
+//   4. barrier: every rank has enqueued its reads (and waits on in_ev);
+//   5. r's stream waits for every rd_ev, copies its scratch into its buffer.
+// Every stream wait refers to an event recorded before a barrier the waiting
+// host thread passed after it, so all dependencies point back in enqueue
+// order (no cycle, whichever hardware queues the streams share), and an
+// event is re-recorded only after every wait on its previous record was
+// enqueued (in_ev before barrier 4 of the previous collective, rd_ev before
+// barrier 2 of the next).
+Loopback::Loopback(int nranks, int device) : n_(nranks) {
+  DQ_CHECK(nranks >= 1 && nranks <= kMaxShard, "loopback ranks must be in [1, 8]");
+  DQ_HIP(hipSetDevice(device));
+  log.assign(n_, {});
+  in_ev_.resize(n_);
+  rd_ev_.resize(n_);
+  bufs_.assign(n_, nullptr);
+  scratch_.assign(n_, nullptr);
+  counts_.assign(n_, 0);
+  cap_.assign(n_, 0);
+  for (int r = 0; r < n_; ++r) {
+    DQ_HIP(hipEventCreateWithFlags(&in_ev_[r], hipEventDisableTiming));
+    DQ_HIP(hipEventCreateWithFlags(&rd_ev_[r], hipEventDisableTiming));
+  }
+}
+
+void Loopback::reset_log() {
+  for (auto& l : log) l.clear();
+}
+
+void Loopback::barrier(int rank, const char* where) {
+  std::unique_lock<std::mutex> l(mu_);
+  const uint64_t g = gen_;
+  if (++arrived_ == n_) {
+    arrived_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    return;
+  }
+  const auto limit = std::chrono::duration<double>(kLoopbackTimeoutS);
+  if (!cv_.wait_for(l, limit, [&] { return gen_ != g; })) {
+    char msg[200];
+    std::snprintf(msg, sizeof msg, "rank %d waited %.0f s at %s of collective #%zu (%d of %d ranks there)",
+                  rank, kLoopbackTimeoutS, where, log[rank].size(), arrived_, n_);
+    die("loopback collective", __FILE__, __LINE__, msg);
+  }
+}
+
+void Loopback::allreduce(int rank, uint64_t* buf, size_t count, hipStream_t stream) {
+  log[rank].push_back(count);
+  if (count > cap_[rank]) {   // (first use: a sized scratch, no stream is waiting on it yet)
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (scratch_[rank]) DQ_HIP(hipFree(scratch_[rank]));
+    cap_[rank] = std::max<size_t>(count, (size_t)1 << 16);
+    DQ_HIP(hipMalloc((void**)&scratch_[rank], cap_[rank] * sizeof(uint64_t)));
+  }
+  bufs_[rank] = buf;
+  counts_[rank] = count;
+  DQ_HIP(hipEventRecord(in_ev_[rank], stream));
+  barrier(rank, "entry");
+  SumSrcs src{};
+  for (int q = 0; q < n_; ++q) {
+    if (counts_[q] != count) {
+      char msg[160];
+      std::snprintf(msg, sizeof msg, "collective #%zu: rank %d has %zu elements, rank %d %zu", log[rank].size(),
+                    rank, count, q, counts_[q]);
+      die("loopback collective", __FILE__, __LINE__, msg);
+    }
+    src.p[q] = bufs_[q];
+    if (q != rank) DQ_HIP(hipStreamWaitEvent(stream, in_ev_[q], 0));
+  }
+  launch_sum_u64(src, n_, scratch_[rank], count, stream);
+  DQ_HIP(hipEventRecord(rd_ev_[rank], stream));
+  barrier(rank, "reads");
+  for (int q = 0; q < n_; ++q)
+    if (q != rank) DQ_HIP(hipStreamWaitEvent(stream, rd_ev_[q], 0));
+  DQ_HIP(hipMemcpyAsync(buf, scratch_[rank], count * sizeof(uint64_t), hipMemcpyDeviceToDevice, stream));
 }
 
 // ---------------------------------------------------------------------------

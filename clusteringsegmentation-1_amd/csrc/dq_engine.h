@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <condition_variable>
 #include <mutex>
 #include <queue>
 #include <deque>
@@ -110,6 +111,38 @@ struct KernelStat {
 enum StatKind { ST_INIT = 0, ST_SPLIT, ST_KMEANS, ST_KLAST, ST_EPILOGUE, ST_PARTITION,
                 ST_CELLS, ST_MAP, ST_PLAN, ST_KLOOP, ST_COUNT };
 
+// Test-only stand-in for the RCCL communicator of row-tile sharding: N
+// engines of ONE process on one device, each driven by its own host thread
+// and stream (rank r = the engine holding rows row_range(h, r, N)), sum their
+// node totals with a reduction kernel ordered by cross-stream events.  The
+// engines run the TOT_ALLREDUCE path exactly as N processes would (local
+// counts != global totals), which a 1-rank RCCL communicator cannot show.
+// Every rank must enqueue the same collective sequence (RCCL's contract): the
+// loopback checks the element counts of each collective against each other
+// and records them per rank (`log`), and a rank left waiting at a collective
+// for kLoopbackTimeoutS aborts with the sequence number instead of hanging.
+class Loopback {
+ public:
+  explicit Loopback(int nranks, int device);
+  int ranks() const { return n_; }
+  // rank's part of one in-place u64 sum allreduce of `count` words on `stream`
+  void allreduce(int rank, uint64_t* buf, size_t count, hipStream_t stream);
+  void reset_log();
+  std::vector<std::vector<uint64_t>> log;   // per rank: element count of each collective
+  static constexpr double kLoopbackTimeoutS = 120.0;
+
+ private:
+  void barrier(int rank, const char* where);
+  int n_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int arrived_ = 0;
+  uint64_t gen_ = 0;
+  std::vector<hipEvent_t> in_ev_, rd_ev_;   // per rank: its inputs ready / its reads done
+  std::vector<uint64_t*> bufs_, scratch_;
+  std::vector<size_t> counts_, cap_;
+};
+
 class Engine {
  public:
   explicit Engine(int device);
@@ -166,7 +199,12 @@ class Engine {
     comm_rank_ = c.rank;
     return old;
   }
-  int comm_ranks() const { return comm_ranks_; }
+  int comm_ranks() const { return loop_ ? loop_->ranks() : comm_ranks_; }
+  // Tests: join the in-process loopback group `l` as `rank` (nullptr: leave).
+  void set_loopback(Loopback* l, int rank) {
+    loop_ = l;
+    loop_rank_ = rank;
+  }
   void allreduce_totals(int nlogical, hipStream_t stream);
   int device() const { return device_; }
   std::mutex& mutex() { return mu_; }
@@ -198,7 +236,7 @@ class Engine {
   // Finalise a split when its 2-means reaches an exact fixed point (default
   // on; results are identical either way -- dq_kernels.hip, node_update).
   void set_fixed_point(bool on) { fixed_point_ = on; }
-  // Device-planned rounds (default on; DQ_HIP_PLAN=0 turns the default off).
+  // Device-planned rounds (default on; DQ_HIP_TUNE plan=0 turns the default off).
   void set_plan(bool on) { plan_ = on; }
   // kloop_kernel eligibility: records of at most n points (0: never)
   void set_loop_max(uint32_t n) { kloop_max_ = std::min<uint32_t>(n, kLoopMaxLen); }
@@ -277,13 +315,8 @@ class Engine {
   // record one shard, planar, at most kloop_max_ points and kLoopMaxTiles tiles.
   bool loop_ok(const Round& R) const;
   void kmeans_loop(Round& R, int max_iters, hipStream_t stream);
-  // DQ_HIP_KLOOP_SHADOW=1 (debugging): kloop_kernel runs beside the kpass
-  // iterations into scratch, and its records / cursors / results are compared
-  bool kloop_shadow_ = false;
-  void* d_shadow_ = nullptr;
-  size_t cap_shadow_ = 0;
-  void shadow_launch(Round& R, int max_iters, hipStream_t stream);
-  void shadow_compare(Round& R);
+  void apply_tune(const char* spec);
+  void check_arena_zero(hipStream_t stream);
   uint64_t tile_len_of(uint64_t len, uint64_t tl) const;
   uint64_t round_tile_len(uint64_t total) const;
   void replay(FrameState& f);
@@ -333,7 +366,7 @@ class Engine {
   // (a planned round's counters and counts must be zero on entry to the
   // fused plan + partition launch, plansplit_kernel)
   std::vector<size_t> arena_hw_;
-  bool fuse_plan_ = true;             // plansplit_kernel for one-shard planned rounds (DQ_HIP_FUSE_PLAN)
+  bool fuse_plan_ = true;             // plansplit_kernel for one-shard planned rounds (DQ_HIP_TUNE fuse_plan)
   char* h_stage_ = nullptr;           // pinned
   size_t cap_stage_tab_ = 0;
   TilePartial* d_parts_ = nullptr;    // per tile of the round
@@ -360,22 +393,22 @@ class Engine {
   char* d_stage_view_ = nullptr;      // device view of h_stage_ (host-coherent)
   hipEvent_t stage_ev_ = nullptr;     // the last upload of h_stage_
   bool stage_pending_ = false;
-  bool plan_ = true;                  // device-planned rounds (DQ_HIP_PLAN=0: host only)
-  bool stats_only_ = true;            // a frame's last planned round: PS_STATS + PS_LATE (DQ_HIP_STATS_ONLY)
+  bool plan_ = true;                  // device-planned rounds (DQ_HIP_TUNE plan=0: host only)
+  bool stats_only_ = true;            // a frame's last planned round: PS_STATS + PS_LATE (DQ_HIP_TUNE stats_only)
   bool eager_replan_ = true;          // finish_round: all 2-means iterations + the re-plan at
-                                      //   once when a planned successor waits (DQ_HIP_EAGER_REPLAN)
+                                      //   once when a planned successor waits (DQ_HIP_TUNE eager_replan)
   uint64_t seq_ = 0;                  // round sequence number
   int lookahead_ = 2;                 // 2-means iterations queued past the one awaited
                                       //   (1: C3 0.543-0.554 ms, 2: 0.518-0.525, 4: 0.520-0.532)
-  bool spin_sync_ = true;             // sync_stream polls an event (DQ_HIP_SPIN_SYNC)
+  bool spin_sync_ = true;             // sync_stream polls an event (DQ_HIP_TUNE spin_sync)
   hipEvent_t sync_ev_ = nullptr;
   void sync_stream(hipStream_t stream);
   bool speculate_kmeans_ = true;      // a round with nothing queued behind it starts its
-                                      //   2-means iterations before its split status (DQ_HIP_SPEC_KMEANS)
-  uint32_t kloop_max_ = 49152;        // a record's points at most for kloop_kernel (DQ_HIP_KLOOP_MAX; 0: off)
-  int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TILES)
-  int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_NODE_TILES)
-  uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TILE_MAX)
+                                      //   2-means iterations before its split status (DQ_HIP_TUNE spec_kmeans)
+  uint32_t kloop_max_ = 49152;        // a record's points at most for kloop_kernel (DQ_HIP_TUNE kloop_max; 0: off)
+  int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TUNE tiles)
+  int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_TUNE node_tiles)
+  uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TUNE tile_max)
   // host-side trace (DQ_HIP_TRACE=1): per-run phase times on stderr
   bool trace_ = false, trace_rounds_ = false;   // DQ_HIP_TRACE=1 / 2 (per round)
   double tr_wait_us_ = 0, tr_build_us_ = 0, tr_replay_us_ = 0;
@@ -384,7 +417,7 @@ class Engine {
   // map tables
   uint32_t* d_cell_c32_ = nullptr;    // compact records per map task of a chunk
   int num_cus_ = 0;
-  bool use_lds_map_ = true;           // DQ_HIP_LDS_MAP=0: the L2-gather map kernel
+  bool use_lds_map_ = true;           // DQ_HIP_TUNE lds_map=0: the L2-gather map kernel
   uint32_t* d_cell_rec_ = nullptr;    // per map task of a chunk
   size_t cap_cells_ = 0;
   uint16_t* d_cell_idx_ = nullptr;
@@ -411,12 +444,15 @@ class Engine {
   int nshard_ = 1;                    // shard records per logical node in this run
   // where a pass's node totals come from (TotMode): own record, the node's
   // shard records in this process, or an allreduce across processes
-  int tot_mode() const { return comm_ ? TOT_ALLREDUCE : (nshard_ > 1 ? TOT_NODE : TOT_OWN); }
+  bool cross_process() const { return comm_ != nullptr || loop_ != nullptr; }
+  int tot_mode() const { return cross_process() ? TOT_ALLREDUCE : (nshard_ > 1 ? TOT_NODE : TOT_OWN); }
   void ensure_totals(size_t nlogical, hipStream_t stream);
   uint64_t* d_tot_ = nullptr;         // sharded rounds: per logical node totals
   size_t cap_tot_ = 0;
   void* comm_ = nullptr;              // ncclComm_t across processes (row-tile sharding)
   int comm_ranks_ = 1, comm_rank_ = 0;
+  Loopback* loop_ = nullptr;          // tests: in-process ranks instead of comm_
+  int loop_rank_ = 0;
   std::vector<int> slot_of_, parent_pos_;   // enqueue_host_round scratch, indexed by node id
   std::vector<FrameState> frames_;
   struct PendingEvent { hipEvent_t a, b; int kind; double bytes, units; };

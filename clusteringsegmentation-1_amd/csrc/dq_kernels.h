@@ -52,11 +52,6 @@ struct RoundArgs {
   uint64_t plane;           // bytes between the R, G and B planes of P0 / P1
   int32_t tot_mode;         // where a record's pass totals come from (TotMode)
   int32_t ps_mode;          // what partsplit_kernel does (PsMode)
-  // kloop_kernel debugging (DQ_HIP_KLOOP_SHADOW): its records, tiles and
-  // results go here instead, and it does not arrive (nullptr: production)
-  DevNode* shadow_nodes;
-  Tile* shadow_tiles;
-  NodeResult* shadow_res;
 };
 
 // partsplit_kernel's work (RoundArgs::ps_mode):
@@ -110,7 +105,7 @@ struct PlanArgs {
   int32_t debug;            // kDebug* flags
   int32_t nshard;           // records per logical node (record = node * nshard + shard)
 };
-constexpr int kPlanMaxParents = 6144;
+constexpr int kPlanMaxParents = 6144;   // parents per planned round (LDS scans)
 
 // Test-only interleaving knobs (dq_hip_set_debug): each forces a timing or
 // cache state the production path must tolerate, with identical outputs.
@@ -125,7 +120,11 @@ constexpr int kPlanMaxParents = 6144;
 //                    GPU runs ahead into the other parity slot);
 //   kDebugPlanStall: the plan kernel's first workgroup stalls ~20 us before
 //                    publishing the plan's counts.
-constexpr int32_t kDebugPrewarm = 1, kDebugUneven = 2, kDebugHostDelay = 4, kDebugPlanStall = 8;   // parents per planned round (LDS scans)
+//   kDebugArenaCheck: every run first checks on the host that the round
+//                    arena is all zero (the planned rounds' invariant) and
+//                    aborts naming the first non-zero byte.
+constexpr int32_t kDebugPrewarm = 1, kDebugUneven = 2, kDebugHostDelay = 4, kDebugPlanStall = 8,
+                  kDebugArenaCheck = 16;
 void launch_plan(const PlanArgs& a, hipStream_t stream);
 // plan_kernel's work and the planned round's partition (PS_FULL / PS_STATS)
 // in one launch of `grid` (= the part tiles' upper bound) workgroups; one
@@ -139,6 +138,10 @@ void launch_upload(void* dst, const void* src_dev_view, size_t bytes, hipStream_
 // Zero `bytes` (a multiple of 16, 16-B aligned) on the stream (hipMemsetAsync
 // cost ~20 us of host time at the end of a call).
 void launch_zero(void* dst, size_t bytes, hipStream_t stream);
+// dst[i] = sum of src.p[r][i] over r < nsrc (u64; the test-only loopback
+// collective of Engine, dq_engine.cpp).  dst must not alias a source.
+struct SumSrcs { const uint64_t* p[kMaxShard]; };
+void launch_sum_u64(const SumSrcs& src, int nsrc, uint64_t* dst, size_t count, hipStream_t stream);
 
 // One statistics pass over tiles [0, ntiles) of the round (one workgroup per tile).
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
@@ -159,7 +162,11 @@ void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stre
 // segments of at most kLoopMaxLen points and at most kLoopMaxTiles tiles.
 // Every record arrives on the counter of iteration max_iters - 1.
 constexpr uint32_t kLoopMaxTiles = 1024;
-constexpr uint32_t kLoopMaxLen = 1u << 20;   // (a wave's u32 sums of squares stay exact)
+// A data wave of kloop_kernel sweeps 64 of every 960 16-point chunks: with
+// at most 64 chunk rows (61440 chunks, less the 16-B alignment slack of the
+// segment's first chunk) it sums at most 65536 points, and 65536 * 255^2 <
+// 2^32 keeps its u32 sums of squares exact.
+constexpr uint32_t kLoopMaxLen = 61440u * 16u - 32u;
 void launch_kloop(const RoundArgs& a, int nrec, int max_iters, hipStream_t stream);
 // Fused partition + split pass over the round's PartTiles: writes each
 // parent's points into its two children's segments (old half first, then new

@@ -1712,7 +1712,6 @@ __global__ __launch_bounds__(kLoopBlock) void kloop_kernel(RoundArgs a, int32_t 
   const uint32_t rec = blockIdx.x;
   const uint32_t tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   DevNode* gw = a.nodes + rec;
-  const bool shadow = a.shadow_nodes != nullptr;
   __shared__ __attribute__((aligned(16))) DevNode sw;
   __shared__ NodeResult sres;
   __shared__ uint32_t s_red[kLoopDataWaves][8];
@@ -1783,8 +1782,8 @@ __global__ __launch_bounds__(kLoopBlock) void kloop_kernel(RoundArgs a, int32_t 
           const Sweep w = chunk_sweep_of(r, g, b);
           add_sums(w, vm & ~old_mask(w, vm, q, exact_all), ls);
         }
-        // (a wave holds at most 2^16 points of a record below kLoopMaxLen:
-        // its u32 sums of squares are exact)
+        // (a wave holds at most 64 chunk rows = 65536 points of a record of
+        // at most kLoopMaxLen points: its u32 sums of squares are exact)
         uint32_t f[F_NUM] = {ls.cnt, ls.sr, ls.sg, ls.sb, ls.qr, ls.qg, ls.qb};
 #pragma unroll
         for (int k = 0; k < F_NUM; ++k) f[k] = wave_sum_u32(f[k]);
@@ -1864,9 +1863,9 @@ __global__ __launch_bounds__(kLoopBlock) void kloop_kernel(RoundArgs a, int32_t 
       }
     }
     __syncthreads();   // counts in
-    block_cursors<kLoopBlock>(shadow ? a.shadow_tiles : a.tiles, s_b, tb, te, s_tot, tb);
+    block_cursors<kLoopBlock>(a.tiles, s_b, tb, te, s_tot, tb);
     if (tid < (uint32_t)kW16)   // the final record back (later launches read it)
-      ((g_u4*)(shadow ? a.shadow_nodes + rec : gw))[tid] = reinterpret_cast<const u32x4*>(&sw)[tid];
+      ((g_u4*)gw)[tid] = reinterpret_cast<const u32x4*>(&sw)[tid];
   }
   // every wave's cursor / record stores complete before the results and the
   // arrival (the host and later launches read them after the status word /
@@ -1875,10 +1874,6 @@ __global__ __launch_bounds__(kLoopBlock) void kloop_kernel(RoundArgs a, int32_t 
   __syncthreads();
   if (wv != 0) return;
   if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x)) debug_sleep_us(10);
-  if (shadow) {
-    if (!skip && lane == 0) a.shadow_res[rec] = sres;
-    return;
-  }
   if (!skip) store_result(a.hres + rec, a.dres ? a.dres + rec : nullptr, sres, lane, sw.len, a.seq);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0)
@@ -1998,7 +1993,10 @@ __device__ void plan_child(const PlanArgs& a, const DevNode& P, const NodeResult
 // (ChildInfo), so no workgroup waits for another.  Saves plan_kernel's
 // launch and its dependent round trips (~8-10 us per round at C3).  The
 // round's counters, per-(tile, wave) counts and arrival words must be zero
-// on entry (Engine: the run's round arena is cleared when the run starts).
+// on entry: the invariant's owner is Engine::run, which zeroes every byte of
+// the arena a run used with one launch behind that run's last kernel (and a
+// new chunk is zeroed when allocated); kDebugArenaCheck verifies it at the
+// next run's entry.
 template <int MODE>
 __device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundArgs& a, uint8_t* stage,
                                                uint32_t (*red)[16]) {
@@ -2342,6 +2340,17 @@ __global__ __launch_bounds__(256) void upload_kernel(u32x4* __restrict__ dst, co
 
 __global__ __launch_bounds__(256) void zero_kernel(u32x4* __restrict__ dst, uint32_t n16) {
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n16; i += gridDim.x * 256u) dst[i] = (u32x4){0u, 0u, 0u, 0u};
+}
+
+// The in-process loopback collective's reduction (tests): dst[i] = sum over
+// the ranks' buffers of src[r][i] (u64, exact).
+__global__ __launch_bounds__(256) void sum_u64_kernel(SumSrcs s, int nsrc, uint64_t* __restrict__ dst,
+                                                      uint32_t count) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < count; i += gridDim.x * 256u) {
+    uint64_t v = 0;
+    for (int r = 0; r < nsrc; ++r) v += s.p[r][i];
+    dst[i] = v;
+  }
 }
 
 // Map, step 1: per colour cell (8x8x8 values), the palette entries that can
@@ -2986,6 +2995,12 @@ void launch_zero(void* dst, size_t bytes, hipStream_t stream) {
   if (n16 == 0) return;
   const uint32_t nb = min(1024u, (n16 + 255u) / 256u);
   zero_kernel<<<dim3(nb), dim3(256), 0, stream>>>((u32x4*)dst, n16);
+}
+
+void launch_sum_u64(const SumSrcs& s, int nsrc, uint64_t* dst, size_t count, hipStream_t stream) {
+  if (count == 0) return;
+  const uint32_t nb = (uint32_t)std::min<size_t>(256, (count + 255) / 256);
+  sum_u64_kernel<<<dim3(nb), dim3(256), 0, stream>>>(s, nsrc, dst, (uint32_t)count);
 }
 
 void launch_upload(void* dst, const void* src, size_t bytes, hipStream_t stream) {

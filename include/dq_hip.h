@@ -258,10 +258,25 @@ const char *dq_hip_stat_name(int kind);
  * dq_hip_set_debug: interleaving knobs for the hand-off tests (flags of
  * dq_kernels.h kDebug*: 1 prewarm the 2-means hand-off lines, 2 uneven
  * workgroup stalls, 4 host delays between status and results, 8 plan-kernel
- * stall); every lane of `device`; 0 (the default) in production.  Outputs are
- * identical under every flag. */
+ * stall, 16 abort unless the round arena is all zero when a run starts); every
+ * lane of `device`; 0 (the default) in production.  Outputs are identical
+ * under every flag. */
 uint64_t dq_hip_build_id(void);
 void dq_hip_set_debug(int device, int flags);
+/* Test-only: the row-tile sharding of nranks (1..8) processes, run by
+ * nranks engines of THIS process on `device`, each with its own stream and
+ * host thread, joined by an in-process loopback collective instead of RCCL
+ * (the TOT_ALLREDUCE path with every rank's local counts != the global
+ * totals).  Rank r holds rows [r*height/nranks, (r+1)*height/nranks) of every
+ * frame (width x height, d_in / d_out whole frames), maps them into the same
+ * rows of d_out and writes its colortables to ct + (r*nframes + i)*k, its
+ * counts to k_out[r*nframes + i].  coll_log (nranks x log_cap, may be NULL)
+ * gets the element count of each collective rank r enqueued, log_len[r] how
+ * many it enqueued.  Synchronous; returns rank 0's empty clusters or -1. */
+int dq_hip_loopback_rows_dev(int device, int nranks, int nframes, const uint32_t *const *d_in,
+                             uint32_t width, uint32_t height, uint32_t *const *d_out,
+                             uint32_t k, uint32_t *ct, uint32_t *k_out, int max_iters,
+                             uint64_t *coll_log, int log_cap, int *log_len);
 
 #ifdef __cplusplus
 }

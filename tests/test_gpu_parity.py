@@ -371,6 +371,44 @@ def test_one_launch_kmeans_loops(gpu, key):
         gpu.set_loop_max(49152)
 
 
+def test_kmeans_loop_at_max_len_near_white(gpu):
+    """kloop_kernel at its largest record (kLoopMaxLen = 983008 points): a
+    data wave then sums 65536 points, and near-white points (255^2-sized
+    squares) bring its u32 sums of squares to within 5 % of 2^32.  The root
+    splits this frame exactly in half (R < 248 | R >= 248), so the next round
+    holds two records of exactly kLoopMaxLen points, unproven at their split
+    (G, B and R-within-half spread alike), which the loop must run.  Parity
+    against the oracle's exact sums."""
+    import ctypes
+    lmax = 61440 * 16 - 32
+    rng = np.random.default_rng(2024)
+    n2 = lmax
+    lo = (rng.integers(240, 248, n2, dtype=np.uint32) << 16)
+    hi = (rng.integers(248, 256, n2, dtype=np.uint32) << 16)
+    r = np.concatenate([lo, hi])
+    gb = (rng.integers(248, 256, 2 * n2, dtype=np.uint32) << 8) | rng.integers(248, 256, 2 * n2, dtype=np.uint32)
+    px = r | gb
+    px = px[rng.permutation(px.size)].astype(np.uint32)
+    k = 8
+    ref_out = np.zeros(px.size, np.uint32)
+    ref_ct = np.zeros(k, np.uint32)
+    kk = ctypes.c_uint32(k)
+    fx.oracle().dqo_quant_recurse(ctypes.c_uint32(px.size), fx.vp(px), fx.vp(ref_out), ctypes.byref(kk),
+                                  fx.vp(ref_ct))
+    try:
+        gpu.set_loop_max(lmax)
+        out, ct = _quant_dev(gpu, px, k)
+        loops = gpu.last_loop_rounds()
+        assert np.array_equal(ct, ref_ct[:kk.value])
+        assert np.array_equal(out, ref_out)
+        assert loops > 0
+        gpu.set_loop_max(lmax + 1000)   # (clamped to kLoopMaxLen)
+        out, ct = _quant_dev(gpu, px, k)
+        assert np.array_equal(ct, ref_ct[:kk.value]) and np.array_equal(out, ref_out)
+    finally:
+        gpu.set_loop_max(49152)
+
+
 def test_repeated_runs_identical(gpu):
     """Run-to-run determinism under many fused 2-means launches (fixed points
     off: every node runs all its iterations through kpass_kernel's
