@@ -408,6 +408,20 @@ uint64_t Engine::tile_len_of(uint64_t len, uint64_t tl) const {
   return std::max<uint64_t>(kSweep, std::min<uint64_t>(tl, t));
 }
 
+// The source format of every node in `ids` (a partition launch's parents):
+// planar working buffers, or a root's caller frame (packed / BGR24); mixed:
+// FMT_ANY.
+int Engine::src_fmt(const std::vector<int>& ids) const {
+  int f = -1;
+  for (int id : ids) {
+    const Node& n = nodes_[id];
+    const int g = n.buf != BUF_IN ? FMT_PLANAR : (frames_[n.frame].job->bgr ? FMT_BGR : FMT_PACKED);
+    if (f >= 0 && g != f) return FMT_ANY;
+    f = g;
+  }
+  return f < 0 ? FMT_ANY : f;
+}
+
 // ---------------------------------------------------------------------------
 // Host-built round: split every node in `active` (one launch per pass for
 // all), launched up to its split epilogue; finish_round waits for it.
@@ -698,7 +712,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     ma.ptiles = reinterpret_cast<const PartTile*>(dblk + o_mpt);
     ma.ps_mode = PS_WRITE;
     timed_begin(stream);
-    launch_partsplit(ma, (int)nmat, stream);
+    launch_partsplit(ma, (int)nmat, src_fmt(mat), stream);
     timed_end(ST_PARTITION, 0.0, stream);
   }
   const double bytes_all = 4.0 * (double)total;
@@ -728,7 +742,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   pass(PASS_SPLIT, ST_SPLIT, (int)nt_own, own_bytes, (double)own_total);
   if (nptiles > 0) {
     timed_begin(stream);
-    launch_partsplit(ra, (int)nptiles, stream);
+    launch_partsplit(ra, (int)nptiles, src_fmt(parents), stream);
     timed_end(ST_PARTITION, part_bytes, stream, (double)parent_total);
   }
   epilogue(PASS_SPLIT, max_iters);
@@ -903,14 +917,14 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   }
   if (fuse_plan_ && S == 1 && ptiles <= (size_t)(6 * num_cus_) && total <= kFusePlanMaxPoints) {
     timed_begin(stream);
-    launch_plansplit(pa, ra, (int)R.ptiles_cap, stream);
+    launch_plansplit(pa, ra, (int)R.ptiles_cap, src_fmt(R.parents), stream);
     timed_end(ST_PARTITION, part_bytes, stream, (double)total);
   } else {
     timed_begin(stream);
     launch_plan(pa, stream);
     timed_end(ST_PLAN, 0.0, stream);
     timed_begin(stream);
-    launch_partsplit(ra, (int)R.ptiles_cap, stream);
+    launch_partsplit(ra, (int)R.ptiles_cap, src_fmt(R.parents), stream);
     timed_end(ST_PARTITION, part_bytes, stream, (double)total);
   }
   timed_begin(stream);
@@ -924,7 +938,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
     RoundArgs la = ra;
     la.ps_mode = PS_LATE;
     timed_begin(stream);
-    launch_partsplit(la, (int)R.ptiles_cap, stream);
+    launch_partsplit(la, (int)R.ptiles_cap, src_fmt(R.parents), stream);
     timed_end(ST_PARTITION, 0.0, stream);
   }
   if (trace_) tr_build_us_ += host_us() - tb0;
@@ -1540,7 +1554,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
         for (int sh = 0; sh < S; ++sh)
           if (f.n[sh] > 0) mj.push_back(MapJob{f.in[sh], f.n[sh], j.d_out + f.first[sh], j.ct, m, j.bgr});
     }
-    if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream);
+    if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream, false);
   }
   // The next run's planned rounds find their blocks zero: clear what this run
   // used, behind its last kernel (at the next run's start it delayed the
@@ -1552,7 +1566,10 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     }
   // Synchronous on return: lookahead launches of the last round may still be
   // queued, and they read the caller's input.
+  const double ts0 = trace_ ? host_us() : 0.0;
   sync_stream(stream);
+  if (trace_) tr_mapsync_us_ = host_us() - ts0;
+  collect_timing();
   if (trace_) {
     const double t_end = host_us();
     std::fprintf(stderr, "divquant-hip trace: map prep %.1fus, map launch+sync %.1fus\n",
@@ -2031,7 +2048,7 @@ void Engine::ensure_map_stage(size_t nmaps) {
 // colortable) triples: host palettes for all of them, ONE upload, then ONE
 // cell-build launch and ONE map launch per chunk of up to kMapChunk tasks,
 // ONE synchronisation at the end.
-void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
+void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream, bool sync) {
   DQ_HIP(hipSetDevice(device_));
   if (!stream) stream = stream_;
   for (int i = 0; i < njobs; ++i) {
@@ -2252,6 +2269,7 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream) {
       }
     }
   }
+  if (!sync) return;   // (run(): its end-of-run clear goes in first, then one sync)
   const double tm2 = trace_ ? host_us() : 0.0;
   sync_stream(stream);
   if (trace_) {

@@ -171,7 +171,8 @@ class Engine {
     int k;
     bool bgr = false;     // d_in is a BGR24 frame (3 B per pixel)
   };
-  void map_many(const MapJob* jobs, int njobs, hipStream_t stream);
+  // sync = false: enqueue only (the caller synchronises and collects the timing)
+  void map_many(const MapJob* jobs, int njobs, hipStream_t stream, bool sync = true);
 
   // Host-pointer convenience (copies in and out through the engine's buffers).
   void stage_in(const uint32_t* h_in, uint32_t n, hipStream_t stream);
@@ -316,6 +317,7 @@ class Engine {
   bool loop_ok(const Round& R) const;
   void kmeans_loop(Round& R, int max_iters, hipStream_t stream);
   void apply_tune(const char* spec);
+  int src_fmt(const std::vector<int>& ids) const;
   void check_arena_zero(hipStream_t stream);
   uint64_t tile_len_of(uint64_t len, uint64_t tl) const;
   uint64_t round_tile_len(uint64_t total) const;

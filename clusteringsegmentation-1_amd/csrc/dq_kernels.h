@@ -24,6 +24,11 @@ constexpr int kCellRecWords = 4;                // 16-B record per cell
 constexpr int kCellCap = 32;                    // candidates in the overflow list
 constexpr uint32_t kCellBrute = 0xFFFF;         // count marker: scan the whole palette
 
+// The source format of every parent of a partition launch (launch_partsplit,
+// launch_plansplit), or FMT_ANY (mixed: each record's own, in a kernel
+// compiled for all of them).
+enum SrcFmt : int { FMT_PLANAR = 0, FMT_BGR = 1, FMT_PACKED = 2, FMT_ANY = 3 };
+
 // Tables of one round (device pointers unless noted).
 struct RoundArgs {
   Tile* tiles;              // the round's tiles (kept: a later round partitions through them)
@@ -130,7 +135,7 @@ void launch_plan(const PlanArgs& a, hipStream_t stream);
 // in one launch of `grid` (= the part tiles' upper bound) workgroups; one
 // shard per node only.  The round block's [LaunchCtr | wparts | rdone] must
 // already be zero.
-void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, hipStream_t stream);
+void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, int fmt, hipStream_t stream);
 // Host-built round tables: copy `bytes` from host-coherent pinned staging
 // (device view) into the round's device block on the round's stream (no
 // copy-engine hop between the host and the round's first kernel).
@@ -172,7 +177,7 @@ void launch_kloop(const RoundArgs& a, int nrec, int max_iters, hipStream_t strea
 // parent's points into its two children's segments (old half first, then new
 // half) of the child buffer, using the parent's final 2-means decision, and
 // accumulates the children's split-pass statistics.
-void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream);
+void launch_partsplit(const RoundArgs& a, int nptiles, int fmt, hipStream_t stream);
 
 // One map_colors_mps job of a batched map launch (device-resident table).
 struct alignas(16) MapTask {

@@ -1418,11 +1418,15 @@ __device__ __forceinline__ void stage_flush(uint8_t* st, const PlaneRsrc& d, Sta
   const uint32_t nfo = g.po >> 4, nfn = (g.pn - kStageRun) >> 4;
   const uint32_t nf = nfo + nfn;
   flush_chunk(st, d, g, l, nfo, nf);
-  if (nf > 64u) flush_chunk(st, d, g, 64u + l, nfo, nf);   // (wave-uniform, rare)
+  // (the rare second chunk row and the first chunks' bytes below are stored
+  // unconditionally -- at kOOB when there is nothing to store -- so every
+  // sweep issues the same count of vector-memory operations and the next
+  // sweep's wait for its loads need not drain these stores)
+  flush_chunk(st, d, g, 64u + l, nfo, nf);
   // a completed first chunk that starts below the wave's first position
   const uint32_t ho = (nfo > 0u && g.cbo < g.loo) ? g.cbo + 16u : 0u;
   const uint32_t hn = (nfn > 0u && g.cbn < g.lon) ? g.cbn + 16u : 0u;
-  if (ho | hn) stage_bytes(st, d, g, ho, hn, l);
+  stage_bytes(st, d, g, ho, hn, l);
   if (nfo | nfn) {   // the partial chunks to the front
     const uint32_t run = (l >> 4) & 1u, i = l & 15u;
     const uint32_t nf = run ? nfn : nfo;
@@ -1527,11 +1531,28 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
       s.g = s.b = s.r;
     }
   }
-  RawSweep x, xn;
+  RawSweep xn;
   uint32_t vs = start & ~15u;
   bool full = vs >= start && vs + kWaveSweep <= end;
-  fetch_sweep_rs<PLANAR, BGR>(s, vs, end, x);
+  fetch_sweep_rs<PLANAR, BGR>(s, vs, end, xn);
+  // the vector-memory operations a sweep issues after its loads, here as
+  // no-ops (kOOB): the loop's top then waits for the previous loads only,
+  // entered from here or from the previous sweep alike
+  if (kStore) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){0u, 0u, 0u, 0u}, d.r, (int)kOOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){0u, 0u, 0u, 0u}, d.g, (int)kOOB, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){0u, 0u, 0u, 0u}, d.b, (int)kOOB, 0, 0);
+    }
+  }
   while (vs < end) {
+    // this sweep's points: a copy of the loads issued one sweep ago, made
+    // HERE (the asm makes x a value of its own): left to the compiler, the
+    // loop-carried copy sat at the end of the sweep and waited there for the
+    // loads the sweep had just issued, exposing the memory latency per sweep
+    RawSweep x = xn;
+    asm volatile("" : "+v"(x.v[0]), "+v"(x.v[1]), "+v"(x.v[2]), "+v"(x.v[3]));
     const uint32_t nvs = vs + kWaveSweep;
     const bool nfull = nvs + kWaveSweep <= end;
     // the next sweep's loads in flight during this one (past the end: kOOB,
@@ -1584,7 +1605,6 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     chunk_sweep(cx, oc, g.cbo + g.po, mask_count(xm), ax);
     chunk_sweep(cy, nc, g.cbn + g.pn - kPnOff, mask_count(ym), ay);
     if (kStore) stage_flush(st, d, g, l);
-    x = xn;
     vs = nvs;
     full = nfull;
   }
@@ -1595,15 +1615,20 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
 
 // One part tile's partition + children's split pass (pt: the parent's tile,
 // record and children; ci0 / ci1: the children's segments and tiling).
-template <int MODE>
+// FMT: the source format of every parent of the launch (FMT_ANY: read from
+// each record -- every path compiled into one kernel, whose register
+// allocation is then the largest path's).
+template <int MODE, int FMT>
 __device__ __forceinline__ void partsplit_tile(const RoundArgs& a, const PartTile& pt, const ChildInfo& ci0,
                                                const ChildInfo& ci1, uint8_t* stage, uint32_t (*red)[16]) {
   g_cnode& nd = *(g_cnode*)pt.parent;
   g_ctile* tp = (g_ctile*)pt.tile;
   SplitSums so, sn;
-  StageMem* st = stage + wave_id() * kStageWave;
-  if (nd.planar == SRC_PLANAR) partsplit_run<true, false, MODE>(pt, nd, tp, ci0, ci1, a.wparts, a.plane, st, so, sn);
-  else if (nd.planar == SRC_BGR24) partsplit_run<true, true, MODE>(pt, nd, tp, ci0, ci1, a.wparts, a.plane, st, so, sn);
+  StageMem* st = stage ? stage + wave_id() * kStageWave : nullptr;
+  if (FMT == FMT_PLANAR || (FMT == FMT_ANY && nd.planar == SRC_PLANAR))
+    partsplit_run<true, false, MODE>(pt, nd, tp, ci0, ci1, a.wparts, a.plane, st, so, sn);
+  else if (FMT == FMT_BGR || (FMT == FMT_ANY && nd.planar == SRC_BGR24))
+    partsplit_run<true, true, MODE>(pt, nd, tp, ci0, ci1, a.wparts, a.plane, st, so, sn);
   else partsplit_run<false, false, MODE>(pt, nd, tp, ci0, ci1, a.wparts, a.plane, st, so, sn);
   if (MODE == PS_WRITE || MODE == PS_LATE) return;   // (no sums: the round's sparts stay)
 
@@ -1627,7 +1652,7 @@ __device__ __forceinline__ void partsplit_tile(const RoundArgs& a, const PartTil
   }
 }
 
-template <int MODE>
+template <int MODE, int FMT>
 __device__ __forceinline__ void partsplit_body(const RoundArgs& a, uint8_t* stage, uint32_t (*red)[16]) {
   const PartTile pt = a.ptiles[blockIdx.x];
   if (MODE == PS_LATE) {   // only parents with a child still active after its split epilogue
@@ -1636,18 +1661,20 @@ __device__ __forceinline__ void partsplit_body(const RoundArgs& a, uint8_t* stag
     if (!a0 && !a1) return;
   }
   const ChildInfo ci0 = child_info(a.nodes, pt.child[0]), ci1 = child_info(a.nodes, pt.child[1]);
-  partsplit_tile<MODE>(a, pt, ci0, ci1, stage, red);
+  partsplit_tile<MODE, FMT>(a, pt, ci0, ci1, stage, red);
 }
 
+// One kernel per (mode, parent format): each gets the registers its own path
+// needs, and PS_STATS (no stores) no LDS staging at all.
+template <int MODE, int FMT>
 __global__ __launch_bounds__(kBlock, 4) void partsplit_kernel(RoundArgs a) {
   if (a.counts && blockIdx.x >= a.counts[1]) return;   // planned round: grid is an upper bound
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
   __shared__ uint32_t red[kTileWaves][16];
-  switch (a.ps_mode) {
-    case PS_STATS: partsplit_body<PS_STATS>(a, stage, red); break;
-    case PS_LATE: partsplit_body<PS_LATE>(a, stage, red); break;
-    case PS_WRITE: partsplit_body<PS_WRITE>(a, stage, red); break;
-    default: partsplit_body<PS_FULL>(a, stage, red); break;
+  if constexpr (MODE == PS_STATS) {
+    partsplit_body<MODE, FMT>(a, nullptr, red);
+  } else {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
+    partsplit_body<MODE, FMT>(a, stage, red);
   }
 }
 
@@ -1997,7 +2024,7 @@ __device__ void plan_child(const PlanArgs& a, const DevNode& P, const NodeResult
 // the arena a run used with one launch behind that run's last kernel (and a
 // new chunk is zeroed when allocated); kDebugArenaCheck verifies it at the
 // next run's entry.
-template <int MODE>
+template <int MODE, int FMT>
 __device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundArgs& a, uint8_t* stage,
                                                uint32_t (*red)[16]) {
   __shared__ uint32_t s_w[kBlock / 64][2];
@@ -2113,14 +2140,18 @@ __device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundAr
   ci1.len = nn;
   ci1.tl = plan_tile_len(nn, pa.tl, pa.node_tiles);
   ci1.tb = cb + nto;
-  partsplit_tile<MODE>(a, pt, ci0, ci1, stage, red);
+  partsplit_tile<MODE, FMT>(a, pt, ci0, ci1, stage, red);
 }
 
+template <int MODE, int FMT>
 __global__ __launch_bounds__(kBlock, 4) void plansplit_kernel(PlanArgs pa, RoundArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
   __shared__ uint32_t red[kTileWaves][16];
-  if (a.ps_mode == PS_STATS) plansplit_body<PS_STATS>(pa, a, stage, red);
-  else plansplit_body<PS_FULL>(pa, a, stage, red);
+  if constexpr (MODE == PS_STATS) {
+    plansplit_body<MODE, FMT>(pa, a, nullptr, red);
+  } else {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kTileWaves * kStageWave];
+    plansplit_body<MODE, FMT>(pa, a, stage, red);
+  }
 }
 
 
@@ -2756,8 +2787,11 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
       b = in4[2 * gi + 1];
     }
   };
-  typedef __attribute__((address_space(1))) u32x4 g_u4;
-  g_u4* out4 = (g_u4*)as_gw(tk.out);
+  // the output through a buffer resource: a lane past the task's groups
+  // stores at kOOB (dropped), so every iteration issues the same count of
+  // vector-memory operations after its loads (see the loop's top)
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)tk.out, (short)0, (int)min(4u * n, 0x7FFFFFF0u), 0x00020000);
 
   // (c2 - 2 dot) << 12 | sad, as (c2 << 12) - (dot << 13) + sad: the low 12
   // bits of the first two terms are zero and sad < 4096, so the OR is an add
@@ -2822,12 +2856,21 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   // the next iteration's pixels are loaded before this one's are mapped
   u32x4 na = (u32x4){0u, 0u, 0u, 0u}, nb = na;
   if (g0 + threadIdx.x < g1) load_group(g0 + threadIdx.x, na, nb);
+  // an iteration's two stores, here as no-ops: the loop's top waits for the
+  // previous loads only, entered from here or from the previous iteration
+  __builtin_amdgcn_raw_buffer_store_b128(na, orsrc, (int)kOOB, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(na, orsrc, (int)kOOB, 0, 0);
   for (uint32_t gb = g0; gb < g1; gb += kMapLdsBlock) {
     const uint32_t g = gb + threadIdx.x;
     const bool have = g < g1;
     uint32_t px[kMapPx];
     {
-      const u32x4 a = na, b = nb;
+      // a copy of the loads issued one iteration ago, made HERE (the asm makes
+      // it a value of its own): left to the compiler, the loop-carried copy
+      // sat at the end of the iteration and waited there for the loads the
+      // iteration had just issued
+      u32x4 a = na, b = nb;
+      asm volatile("" : "+v"(a), "+v"(b));
       const uint32_t gn = g + kMapLdsBlock;
       if (gn < g1) load_group(gn, na, nb);
       if (bgr) {
@@ -2900,11 +2943,12 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
       }
       wave_lds_sync();
     }
-    if (have) {
-      // (nontemporal: streamed past the caches -- the next call's root pass
-      // found its frame in L2 / MALL instead of the map's output)
-      __builtin_nontemporal_store((u32x4){res[0], res[1], res[2], res[3]}, out4 + 2 * g);
-      __builtin_nontemporal_store((u32x4){res[4], res[5], res[6], res[7]}, out4 + 2 * g + 1);
+    {
+      // (nontemporal, aux bit 1: streamed past the caches -- the next call's
+      // root pass found its frame in L2 / MALL instead of the map's output)
+      const int o = (int)(have ? 32u * g : kOOB);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){res[0], res[1], res[2], res[3]}, orsrc, o, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){res[4], res[5], res[6], res[7]}, orsrc, o + 16, 0, 2);
     }
   }
   // tail (n % kMapPx points): the task's first workgroup, whole palette
@@ -2968,9 +3012,25 @@ void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stre
   }
 }
 
-void launch_partsplit(const RoundArgs& a, int nptiles, hipStream_t stream) {
+template <int MODE>
+static void partsplit_fmt(const RoundArgs& a, int nptiles, int fmt, hipStream_t stream) {
+  const dim3 g(nptiles), b(kBlock);
+  switch (fmt) {
+    case FMT_PLANAR: partsplit_kernel<MODE, FMT_PLANAR><<<g, b, 0, stream>>>(a); break;
+    case FMT_BGR: partsplit_kernel<MODE, FMT_BGR><<<g, b, 0, stream>>>(a); break;
+    case FMT_PACKED: partsplit_kernel<MODE, FMT_PACKED><<<g, b, 0, stream>>>(a); break;
+    default: partsplit_kernel<MODE, FMT_ANY><<<g, b, 0, stream>>>(a); break;
+  }
+}
+
+void launch_partsplit(const RoundArgs& a, int nptiles, int fmt, hipStream_t stream) {
   if (nptiles <= 0) return;
-  partsplit_kernel<<<dim3(nptiles), dim3(kBlock), 0, stream>>>(a);
+  switch (a.ps_mode) {
+    case PS_STATS: partsplit_fmt<PS_STATS>(a, nptiles, fmt, stream); break;
+    case PS_LATE: partsplit_fmt<PS_LATE>(a, nptiles, fmt, stream); break;
+    case PS_WRITE: partsplit_fmt<PS_WRITE>(a, nptiles, fmt, stream); break;
+    default: partsplit_fmt<PS_FULL>(a, nptiles, fmt, stream); break;
+  }
 }
 
 void launch_kloop(const RoundArgs& a, int nrec, int max_iters, hipStream_t stream) {
@@ -2978,9 +3038,21 @@ void launch_kloop(const RoundArgs& a, int nrec, int max_iters, hipStream_t strea
   kloop_kernel<<<dim3(nrec), dim3(kLoopBlock), 0, stream>>>(a, max_iters);
 }
 
-void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, hipStream_t stream) {
+template <int MODE>
+static void plansplit_fmt(const PlanArgs& pa, const RoundArgs& a, int grid, int fmt, hipStream_t stream) {
+  const dim3 g(grid), b(kBlock);
+  switch (fmt) {
+    case FMT_PLANAR: plansplit_kernel<MODE, FMT_PLANAR><<<g, b, 0, stream>>>(pa, a); break;
+    case FMT_BGR: plansplit_kernel<MODE, FMT_BGR><<<g, b, 0, stream>>>(pa, a); break;
+    case FMT_PACKED: plansplit_kernel<MODE, FMT_PACKED><<<g, b, 0, stream>>>(pa, a); break;
+    default: plansplit_kernel<MODE, FMT_ANY><<<g, b, 0, stream>>>(pa, a); break;
+  }
+}
+
+void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, int fmt, hipStream_t stream) {
   if (grid <= 0) return;
-  plansplit_kernel<<<dim3(grid), dim3(kBlock), 0, stream>>>(pa, a);
+  if (a.ps_mode == PS_STATS) plansplit_fmt<PS_STATS>(pa, a, grid, fmt, stream);
+  else plansplit_fmt<PS_FULL>(pa, a, grid, fmt, stream);
 }
 
 void launch_plan(const PlanArgs& a, hipStream_t stream) {

@@ -90,8 +90,12 @@ cut_bits ( const uint32_t *inPixels,
           const uchar num_bits_blue );
 
 /* DivQuantCluster.cpp:1099-1179 -- divisive clustering into <= *numClustersPtr
- * colours.  GPU for num_bits == 8 && dec_factor == 1 (the only combination
- * quant_recurse uses); other combinations abort with a message. */
+ * colours, on the GPU for every (num_bits, dec_factor, allPixelsUnique):
+ * the uniform-weight rounds for allPixelsUnique && num_bits == 8 &&
+ * dec_factor == 1 (the combination quant_recurse uses), else cut_bits + the
+ * decimated calc_color_table walk + the weighted rounds (:1130-1146).  A walk
+ * that would read past the input (numRows > numCols: the reference reads out
+ * of bounds there) aborts with a message. */
 void
 quant_varpart_fast (
                     const uint32_t numPixels,
