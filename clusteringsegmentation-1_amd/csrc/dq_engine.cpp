@@ -83,7 +83,7 @@ void Engine::apply_tune(const char* spec) {
     if (k == "full_iters") fixed_point_ = v == 0;                       // every 2-means iteration runs
     else if (k == "plan") plan_ = v != 0;                               // device-planned rounds
     else if (k == "tiles") tiles_target_ = std::max<long>(64, v);      // tiles per big round
-    else if (k == "node_tiles") node_tiles_ = std::max<long>(1, v);    // tiles per record at least
+    else if (k == "node_tiles") node_tiles_ = std::max<long>(1, std::min<long>(65536, v));   // tiles per record at least
     else if (k == "tile_max")                                           // points per tile at most
       tile_max_ = (uint32_t)std::max<long>(kSweep, std::min<long>(kMaxTilePx, v)) / kSweep * kSweep;
     else if (k == "lds_map") use_lds_map_ = v != 0;                     // 0: the L2-gather map kernel
@@ -230,7 +230,7 @@ uint32_t* Engine::scratch_words(size_t n) {
 
 // Device arena for the per-round tables.  Chunks are kept (and reused by the
 // next run); a round's block never moves once written.
-char* Engine::arena_alloc(size_t bytes) {
+char* Engine::arena_alloc(size_t bytes, hipStream_t stream) {
   bytes = (bytes + 255) & ~(size_t)255;
   while (true) {
     if (arena_chunk_ < arena_.size()) {
@@ -248,7 +248,12 @@ char* Engine::arena_alloc(size_t bytes) {
     const size_t sz = std::max<size_t>(bytes, (size_t)16 << 20);
     char* p = nullptr;
     DQ_HIP(hipMalloc((void**)&p, sz));
-    DQ_HIP(hipMemset(p, 0, sz));   // (synchronous: zero before any launch uses it)
+    // Zeroed on the round's stream, ahead of every launch that uses it.  (Not
+    // hipMemset: for device memory it is asynchronous to the host and runs on
+    // the null stream, which a non-blocking stream does not wait for -- behind
+    // other lanes' work it could clear a round block after its first kernels
+    // wrote it; see DESIGN.md 3c''.)
+    launch_zero(p, sz, stream);
     arena_.push_back({p, sz});
     arena_hw_.push_back(0);
   }
@@ -378,7 +383,19 @@ uint32_t Engine::wait_status(const uint64_t* slot, uint64_t seq, hipStream_t str
       const hipError_t e = hipStreamQuery(stream);
       if (e == hipSuccess) {
         if (ready(&act)) return act;
-        die("status word", __FILE__, __LINE__, "stream drained without the round's status");
+        char msg[384];
+        const uint64_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+        const long si = (long)(slot - h_stat_);
+        int n = snprintf(msg, sizeof msg, "stream drained without the round's status (slot %ld:%ld, seq %llu, word %016llx",
+                         si / (long)cap_stat_, si % (long)cap_stat_, (unsigned long long)seq, (unsigned long long)v);
+        if (wait_round_ >= 0 && wait_round_ < (int)rounds_.size()) {
+          const Round& R = rounds_[wait_round_];
+          const uint32_t* hc = h_counts_ + 4 * R.par;
+          n += snprintf(msg + n, sizeof msg - n, "; round %d planned %d prev %d nr %d tiles %zu ptiles %zu counts %u/%u/%u",
+                        wait_round_, (int)R.planned, R.prev, R.nr, R.ntiles, R.nptiles, hc[0], hc[1], hc[2]);
+        }
+        snprintf(msg + n, sizeof msg - n, ")");
+        die("status word", __FILE__, __LINE__, msg);
       }
       if (e != hipErrorNotReady) die("hipStreamQuery", __FILE__, __LINE__, hipGetErrorString(e));
     }
@@ -538,7 +555,9 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   const size_t o_wp = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
   // then the fused 2-means passes' arrival words, per (iteration, record)
   const size_t o_rd = o_wp + al(ntiles * kTileWaves * sizeof(uint32_t));
-  const size_t bytes = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
+  // then the records' summaries (written as each becomes final; the next plan's scan)
+  const size_t o_sum = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
+  const size_t bytes = o_sum + al((size_t)nr * sizeof(RecSummary));
   R.bytes = bytes;
   if (mode == TOT_ALLREDUCE) ensure_totals(nl, stream);
   // the staging is rewritten: its previous upload must have run
@@ -553,7 +572,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     DQ_HIP(hipHostGetDevicePointer((void**)&d_stage_view_, h_stage_, 0));
     cap_stage_tab_ = c;
   }
-  char* dblk = arena_alloc(bytes);
+  char* dblk = arena_alloc(bytes, stream);
   std::memset(h_stage_, 0, bytes);
   DevNode* hn = reinterpret_cast<DevNode*>(h_stage_);
   Tile* ht = reinterpret_cast<Tile*>(h_stage_ + o_tiles);
@@ -702,6 +721,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   ra.nshard = S;
   ra.debug = debug_;
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
+  ra.rsum = reinterpret_cast<RecSummary*>(dblk + o_sum);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = nullptr;
   ra.plane = cap_px_;
@@ -841,9 +861,10 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   const size_t o_ctr = o_cnt + 64;
   const size_t o_wp = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
   const size_t o_rd = o_wp + al(R.tiles_cap * kTileWaves * sizeof(uint32_t));
-  const size_t bytes = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
+  const size_t o_sum = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
+  const size_t bytes = o_sum + al(nr * sizeof(RecSummary));   // ([o_ctr, bytes): zero on entry)
   R.bytes = bytes;
-  char* dblk = arena_alloc(bytes);
+  char* dblk = arena_alloc(bytes, stream);
   R.dn = reinterpret_cast<DevNode*>(dblk);
   R.dt = reinterpret_cast<Tile*>(dblk + o_tiles);
   R.dcounts = reinterpret_cast<uint32_t*>(dblk + o_cnt);
@@ -857,6 +878,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
 
   PlanArgs pa;
   pa.pn = P.dn;
+  pa.psum = P.ra.rsum;
   pa.pres = d_dres_ + (size_t)P.par * cap_res_;
   pa.ptiles = P.dt;
   pa.plist = ident ? nullptr : d_plist_ + (size_t)R.par * cap_plist_;
@@ -868,8 +890,6 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   pa.cn = R.dn;
   pa.ct = R.dt;
   pa.cpt = reinterpret_cast<PartTile*>(dblk + o_pt);
-  pa.zero = reinterpret_cast<uint32_t*>(dblk + o_ctr);
-  pa.nzero = (uint32_t)((bytes - o_ctr) / 4);
   pa.counts = R.dcounts;
   pa.hcounts = d_counts_h_ + 4 * R.par;
   pa.p0 = reinterpret_cast<const uint8_t*>(d_p0_);
@@ -897,6 +917,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   ra.nshard = S;
   ra.debug = debug_;
   ra.rdone = reinterpret_cast<uint32_t*>(dblk + o_rd);
+  ra.rsum = reinterpret_cast<RecSummary*>(dblk + o_sum);
   ra.dres = d_dres_ + (size_t)R.par * cap_res_;
   ra.counts = R.dcounts;
   ra.plane = cap_px_;
@@ -1037,6 +1058,7 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   Round& R = rounds_[ri];   // (rounds_ is a deque: enqueueing below keeps R valid)
   const int S = nshard_;
   const double tw0 = tr_wait_us_;
+  wait_round_ = ri;   // (named by wait_status's diagnostics)
   const double tf0 = trace_ ? host_us() : 0.0;
   const uint64_t* stat = h_stat_ + (size_t)R.par * cap_stat_;
   const NodeResult* res = h_res_ + (size_t)R.par * cap_res_;

@@ -296,11 +296,12 @@ class Engine {
     double t_enq = 0;
   };
   std::deque<Round> rounds_;          // (a deque: references stay valid while rounds are added)
+  int wait_round_ = -1;               // the round finish_round waits on (diagnostics)
 
   void ensure_pixels(size_t total);
   void ensure_round(size_t nnodes, size_t ntiles, size_t nptiles, size_t staging_bytes,
                     int max_iters, hipStream_t stream);
-  char* arena_alloc(size_t bytes);
+  char* arena_alloc(size_t bytes, hipStream_t stream);
   uint32_t wait_status(const uint64_t* slot, uint64_t seq, hipStream_t stream);
   int enqueue_host_round(const std::vector<int>& active, bool root_round, int max_iters,
                          hipStream_t stream);

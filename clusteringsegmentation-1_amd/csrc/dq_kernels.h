@@ -29,6 +29,19 @@ constexpr uint32_t kCellBrute = 0xFFFF;         // count marker: scan the whole 
 // compiled for all of them).
 enum SrcFmt : int { FMT_PLANAR = 0, FMT_BGR = 1, FMT_PACKED = 2, FMT_ANY = 3 };
 
+// What a plan reads of each record of the round it is planned from, written
+// by whichever kernel finalises the record (store_result), 32 B contiguous
+// per record: the plan's scan over every parent's (shard) records reads these
+// instead of fields spread over 272-B DevNodes (with 8 shard records per
+// parent the scattered loads were most of a sharded plan's time).  Zero
+// (final = 0) until the record is final: the round arena is zero on entry.
+struct alignas(16) RecSummary {
+  uint32_t off, len, n_new_local, ntiles;   // local segment, final new half, the record's tiles
+  int32_t tile_begin;
+  uint32_t final;                           // 1 once the record's split is final
+  uint32_t pad[2];
+};
+
 // Tables of one round (device pointers unless noted).
 struct RoundArgs {
   Tile* tiles;              // the round's tiles (kept: a later round partitions through them)
@@ -57,6 +70,7 @@ struct RoundArgs {
   uint64_t plane;           // bytes between the R, G and B planes of P0 / P1
   int32_t tot_mode;         // where a record's pass totals come from (TotMode)
   int32_t ps_mode;          // what partsplit_kernel does (PsMode)
+  RecSummary* rsum;         // per record, written with its final results (the next plan's scan)
 };
 
 // partsplit_kernel's work (RoundArgs::ps_mode):
@@ -87,6 +101,7 @@ enum TotMode : int32_t { TOT_OWN = 0, TOT_NODE = 1, TOT_ALLREDUCE = 2 };
 // when a listed parent is not final after its split epilogue.
 struct PlanArgs {
   const DevNode* pn;        // previous round: records
+  const RecSummary* psum;   //                 their summaries (the scans)
   const NodeResult* pres;   //                 results (device copy)
   const Tile* ptiles;       //                 tiles (the part tiles point into them)
   const int32_t* plist;     // parent (logical) nodes to split (host-coherent pinned memory)
@@ -97,8 +112,6 @@ struct PlanArgs {
   DevNode* cn;              // this round: 2 np records
   Tile* ct;
   PartTile* cpt;
-  uint32_t* zero;           // [LaunchCtr | wparts | rdone] words to clear
-  uint32_t nzero;
   uint32_t* counts;         // device: tiles, part tiles, aborted (1: a listed parent not
                             //   final, 2: overflow, 3: cancelled -- see `cancel`)
   uint32_t* hcounts;        // host-coherent mirror of counts
@@ -130,11 +143,14 @@ constexpr int kPlanMaxParents = 6144;   // parents per planned round (LDS scans)
 //                    aborts naming the first non-zero byte.
 constexpr int32_t kDebugPrewarm = 1, kDebugUneven = 2, kDebugHostDelay = 4, kDebugPlanStall = 8,
                   kDebugArenaCheck = 16;
+// plan_kernel: the planned round's tables.  Like plansplit below, it relies on
+// the round block's [LaunchCtr | wparts | rdone | summaries] being zero on
+// entry (the round arena's invariant, Engine::run).
 void launch_plan(const PlanArgs& a, hipStream_t stream);
 // plan_kernel's work and the planned round's partition (PS_FULL / PS_STATS)
 // in one launch of `grid` (= the part tiles' upper bound) workgroups; one
-// shard per node only.  The round block's [LaunchCtr | wparts | rdone] must
-// already be zero.
+// shard per node only.  The round block's [LaunchCtr | wparts | rdone |
+// summaries] must already be zero.
 void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, int fmt, hipStream_t stream);
 // Host-built round tables: copy `bytes` from host-coherent pinned staging
 // (device view) into the round's device block on the round's stream (no

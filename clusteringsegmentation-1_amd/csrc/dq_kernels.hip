@@ -742,13 +742,21 @@ __device__ __forceinline__ void block_cursors(Tile* tiles, const uint32_t* wp, i
 // tag = round seq) is stored only after the others completed (vmcnt(0)), so
 // a host that sees the tag sees the record; the caller drains the tag store
 // before arriving.
+// sum (may be null): the record's RecSummary, from its final record w.
 __device__ __forceinline__ void store_result(NodeResult* dst, NodeResult* ddst, NodeResult& r,
-                                             uint32_t lane, uint32_t len_local, uint64_t seq) {
+                                             uint32_t lane, uint32_t len_local, uint64_t seq,
+                                             RecSummary* sum, const DevNode* w) {
   constexpr int kWords = (int)(sizeof(NodeResult) / 8);
   static_assert(kWords <= 64, "one wave stores the result");
   if (lane == 0) {
     r.len_local = len_local;
     r.tag = (uint32_t)seq;
+  }
+  if (sum && lane == 1) {
+    typedef __attribute__((address_space(1))) u32x4 g_u4;
+    g_u4* s4 = (g_u4*)sum;
+    s4[0] = (u32x4){w->off, w->len, r.n_new_local, (uint32_t)(w->tile_end - w->tile_begin)};
+    s4[1] = (u32x4){(uint32_t)w->tile_begin, 1u, 0u, 0u};
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -900,7 +908,8 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (final_results)
-      store_result(a.hres + blockIdx.x, a.dres ? a.dres + blockIdx.x : nullptr, sres, lane, w->len, a.seq);
+      store_result(a.hres + blockIdx.x, a.dres ? a.dres + blockIdx.x : nullptr, sres, lane, w->len, a.seq,
+                   a.rsum ? a.rsum + blockIdx.x : nullptr, w);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
       arrive(a.ctr + a.it, blockIdx.x, (uint32_t)a.nn, !skip && !final_results, a.hstat + a.it, a.seq);
@@ -968,7 +977,8 @@ __device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int nod
     for (int sh = 0; sh < S; ++sh) {
       const DevNode* w = a.nodes + r0 + sh;
       record_cursors<true>(a.tiles, a.wparts, w->tile_begin, w->tile_end, lane);
-      store_result(a.hres + r0 + sh, a.dres ? a.dres + r0 + sh : nullptr, sres[sh], lane, w->len, a.seq);
+      store_result(a.hres + r0 + sh, a.dres ? a.dres + r0 + sh : nullptr, sres[sh], lane, w->len, a.seq,
+                   a.rsum ? a.rsum + r0 + sh : nullptr, w);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1901,7 +1911,9 @@ __global__ __launch_bounds__(kLoopBlock) void kloop_kernel(RoundArgs a, int32_t 
   __syncthreads();
   if (wv != 0) return;
   if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x)) debug_sleep_us(10);
-  if (!skip) store_result(a.hres + rec, a.dres ? a.dres + rec : nullptr, sres, lane, sw.len, a.seq);
+  if (!skip)
+    store_result(a.hres + rec, a.dres ? a.dres + rec : nullptr, sres, lane, sw.len, a.seq,
+                 a.rsum ? a.rsum + rec : nullptr, &sw);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0)
     arrive(a.ctr + (max_iters - 1), rec, (uint32_t)a.nn, bad, a.hstat + (max_iters - 1), a.seq);
@@ -1915,16 +1927,39 @@ __global__ __launch_bounds__(kLoopBlock) void kloop_kernel(RoundArgs a, int32_t 
 // layout rules are Engine::tile_len and the record fill of run_round,
 // restated; the host mirrors them (Engine::mirror_planned) and checks the
 // counts.
-__device__ __forceinline__ uint32_t plan_tile_len(uint32_t len, uint32_t tl, int32_t nt) {
-  uint64_t t = ((uint64_t)len + (uint32_t)nt - 1) / (uint32_t)nt;
-  t = ((t + kSweep - 1) / kSweep) * kSweep;
-  return (uint32_t)max((uint64_t)kSweep, min((uint64_t)tl, t));
+// Exact a / b for a < 2^22, b >= 1: a float reciprocal (error < 0.75 on the
+// quotient) and one correction each way.  (A generic 32-bit division is ~4x
+// the code; the sharded plan inlines 30+ of them and outgrew the I-cache.)
+__device__ __forceinline__ uint32_t small_udiv(uint32_t a, uint32_t b) {
+  uint32_t q = (uint32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
+  int32_t r = (int32_t)(a - q * b);
+  if (r < 0) { q -= 1u; r += (int32_t)b; }
+  if ((uint32_t)r >= b) q += 1u;
+  return q;
 }
 
+// Tile length of a record of `len` points, in whole 4096-point sweeps:
+// Engine::tile_len_of (roundup_4096(ceil(len / nt)) clamped to [4096, tl])
+// restated on L = ceil(len / 4096) < 2^20 sweeps -- nested ceilings:
+// ceil(ceil(len / nt) / 4096) = ceil(L / nt).  tl is a whole number of sweeps
+// (round_tile_len, tile_max_), nt <= 65536 (apply_tune).
+static_assert(kSweep == 4096, "plan_tile_sweeps shifts by 12");
+__device__ __forceinline__ uint32_t plan_tile_sweeps(uint32_t len, uint32_t tl, int32_t nt) {
+  const uint32_t L = (len >> 12) + ((len & (kSweep - 1)) != 0 ? 1u : 0u);
+  const uint32_t m = small_udiv(L + (uint32_t)nt - 1u, (uint32_t)nt);
+  return max(1u, min(tl / kSweep, m));
+}
+
+__device__ __forceinline__ uint32_t plan_tile_len(uint32_t len, uint32_t tl, int32_t nt) {
+  return plan_tile_sweeps(len, tl, nt) * kSweep;
+}
+
+// ceil(len / tile length) = ceil(L / m) (nested ceilings again)
 __device__ __forceinline__ uint32_t plan_ntiles(uint32_t len, uint32_t tl, int32_t nt) {
   if (len == 0) return 1;   // an empty record still gets one (empty) tile
-  const uint32_t t = plan_tile_len(len, tl, nt);
-  return (len + t - 1) / t;
+  const uint32_t L = (len >> 12) + ((len & (kSweep - 1)) != 0 ? 1u : 0u);
+  const uint32_t m = plan_tile_sweeps(len, tl, nt);
+  return small_udiv(L + m - 1u, m);
 }
 
 // The split threshold / shift of a child (the cut of :388-403 from its mean
@@ -2052,11 +2087,11 @@ __device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundAr
     for (int e = 0; e < kPer; ++e) {
       t[e] = q[e] = 0;
       if (i0 + e < np) {
-        const DevNode& P = pa.pn[parent(i0 + e)];
-        bad |= P.done_it == 0;
+        const RecSummary& P = pa.psum[parent(i0 + e)];
+        bad |= P.final == 0;
         const uint32_t nn = P.n_new_local;
         t[e] = ntl(P.len - nn) + ntl(nn);
-        q[e] = (uint32_t)(P.tile_end - P.tile_begin);
+        q[e] = P.ntiles;
       }
       lt += t[e];
       lp += q[e];
@@ -2098,9 +2133,12 @@ __device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundAr
     }
   }
   if (cancelled || s_abort || overflow || j >= run_p) return;   // (uniform)
-  const int32_t i = s_par;
-  const uint32_t cb = s_cb, pb = s_pb;
-  const int32_t ai = parent(i);
+  // (workgroup-uniform values read from LDS: readfirstlane puts them, and
+  // every address and load derived from them, in SGPRs -- as VGPRs they
+  // pushed partsplit_tile's body over 128 VGPRs and into scratch)
+  const int32_t i = __builtin_amdgcn_readfirstlane(s_par);
+  const uint32_t cb = __builtin_amdgcn_readfirstlane(s_cb), pb = __builtin_amdgcn_readfirstlane(s_pb);
+  const int32_t ai = __builtin_amdgcn_readfirstlane(parent(i));
   const DevNode* Pp = pa.pn + ai;
   const NodeResult* rp = pa.pres + ai;
   const uint32_t nn = Pp->n_new_local, lo = Pp->len - nn, off = Pp->off;
@@ -2127,6 +2165,10 @@ __device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundAr
   pt.parent = Pp;
   plan_cut(*rp, 0, &pt.thr[0], &pt.shift[0]);
   plan_cut(*rp, 1, &pt.thr[1], &pt.shift[1]);
+  for (int s = 0; s < 2; ++s) {   // (FP64 compares run on the VALU: back to SGPRs)
+    pt.thr[s] = __builtin_amdgcn_readfirstlane(pt.thr[s]);
+    pt.shift[s] = __builtin_amdgcn_readfirstlane(pt.shift[s]);
+  }
   pt.child[0] = 2 * i;
   pt.child[1] = 2 * i + 1;
   if (tid == 0) pa.cpt[j] = pt;   // (for the round's PS_LATE partition)
@@ -2140,6 +2182,10 @@ __device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundAr
   ci1.len = nn;
   ci1.tl = plan_tile_len(nn, pa.tl, pa.node_tiles);
   ci1.tb = cb + nto;
+  for (ChildInfo* c : {&ci0, &ci1}) {   // (the tile lengths: VALU divisions)
+    c->tl = __builtin_amdgcn_readfirstlane(c->tl);
+    c->tb = __builtin_amdgcn_readfirstlane(c->tb);
+  }
   partsplit_tile<MODE, FMT>(a, pt, ci0, ci1, stage, red);
 }
 
@@ -2171,6 +2217,10 @@ __global__ __launch_bounds__(kBlock, 4) void plansplit_kernel(PlanArgs pa, Round
 // clamped loads issued together (then masked by shard < S), not a walk of
 // dependent loads: with 8 shards the walks made the plan ~35 us per round.
 constexpr int kPlanBlock = 256;
+#ifndef DQ_PLAN_SHARD_WGS
+#define DQ_PLAN_SHARD_WGS 64
+#endif
+constexpr int kPlanShardTileWgs = DQ_PLAN_SHARD_WGS;   // tile workgroups of a sharded plan
 template <bool SH>
 __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t nb_rec) {
   __shared__ uint32_t s_cb[kPlanMaxParents + 1];   // children's tiles before parent i
@@ -2182,9 +2232,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
   auto parent = [&](int32_t i) -> int32_t { return a.plist ? a.plist[i] : i; };   // logical, in prev
   auto ntl = [&](uint32_t len) { return plan_ntiles(len, a.tl, a.node_tiles); };
   if (tid == 0) s_abort = 0;
-  // clear [LaunchCtr | wparts | rdone] (grid-stride)
-  for (uint32_t i = blockIdx.x * kPlanBlock + tid; i < a.nzero; i += gridDim.x * kPlanBlock) a.zero[i] = 0u;
-  __syncthreads();
+  __syncthreads();   // (the round's [LaunchCtr | wparts | rdone | summaries] are zero on entry: plansplit_body)
   // (1) every parent final? exclusive scans of the tile counts, chunk by
   //     chunk; a lane takes kPlanPer consecutive parents of a chunk (all their
   //     loads in flight together)
@@ -2201,15 +2249,15 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     for (int e = 0; e < kPlanPer; ++e) {
       t[e] = q[e] = 0;
       if (i0 + e < np) {
-        const DevNode* P0 = a.pn + (size_t)parent(i0 + e) * S;
-        bad |= P0->done_it == 0;   // (every shard record of a node agrees)
+        const RecSummary* P0 = a.psum + (size_t)parent(i0 + e) * S;
+        bad |= P0->final == 0;   // (every shard record of a node agrees)
 #pragma unroll
         for (int sh = 0; sh < SM; ++sh) {
-          const DevNode& P = P0[shard(sh)];
+          const RecSummary& P = P0[shard(sh)];
           const uint32_t nn = P.n_new_local;
           const bool on = !SH || sh < S;
           t[e] += on ? ntl(P.len - nn) + ntl(nn) : 0u;
-          q[e] += on ? (uint32_t)(P.tile_end - P.tile_begin) : 0u;
+          q[e] += on ? P.ntiles : 0u;
         }
       }
       lt += t[e];
@@ -2263,10 +2311,10 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     uint32_t told = 0, tnew_all = 0, tnew = 0, pbo = 0;   // tiles / part tiles before this shard's
 #pragma unroll
     for (int x = 0; x < SM; ++x) {
-      const DevNode& Q = a.pn[ai + shard(x)];
+      const RecSummary& Q = a.psum[ai + shard(x)];
       const bool on = !SH || x < S;
       const uint32_t nn = Q.n_new_local;
-      const uint32_t to = ntl(Q.len - nn), tn = ntl(nn), pq = (uint32_t)(Q.tile_end - Q.tile_begin);
+      const uint32_t to = ntl(Q.len - nn), tn = ntl(nn), pq = Q.ntiles;
       if (on && x < sh) {
         told += to;
         tnew += tn;
@@ -2282,8 +2330,10 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     plan_child(a, P, r, 1, (2 * i + 1) * S + sh, P.off + lo, nn, (int32_t)(s_cb[i] + tnew_all + tnew), pb, pe);
     return;
   }
-  // (2b) one child tile and one part tile per lane
-  const uint32_t j = (blockIdx.x - nb_rec) * kPlanBlock + tid;
+  // (2b) child tiles and part tiles, one of each per lane per step, grid-
+  //      stride over the tile workgroups of the launch (S > 1 launches only
+  //      a few: every workgroup's scan of the parents' S records above costs
+  //      more than the tiles it then writes)
   auto find = [&](const uint32_t* base, uint32_t x) -> int32_t {   // last i with base[i] <= x
     int32_t lo = 0, hi = np - 1;
     while (lo < hi) {
@@ -2292,6 +2342,8 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     }
     return lo;
   };
+  const uint32_t nbt = gridDim.x - nb_rec;
+  for (uint32_t j = (blockIdx.x - nb_rec) * kPlanBlock + tid; j < max(run_t, run_p); j += nbt * kPlanBlock) {
   if (j < run_t) {
     const int32_t i = find(s_cb, j);
     const int32_t ai = parent(i) * S;
@@ -2300,7 +2352,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     uint32_t qlo[SM], qnn[SM], qoff[SM];
 #pragma unroll
     for (int x = 0; x < SM; ++x) {
-      const DevNode& Q = a.pn[ai + shard(x)];
+      const RecSummary& Q = a.psum[ai + shard(x)];
       qnn[x] = Q.n_new_local;
       qlo[x] = Q.len - qnn[x];
       qoff[x] = Q.off;
@@ -2337,7 +2389,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     uint32_t k = j - s_pb[i];
     uint32_t qnt[SM];
 #pragma unroll
-    for (int x = 0; x < SM; ++x) qnt[x] = (uint32_t)(a.pn[ai + shard(x)].tile_end - a.pn[ai + shard(x)].tile_begin);
+    for (int x = 0; x < SM; ++x) qnt[x] = a.psum[ai + shard(x)].ntiles;
     int sh = 0;
     bool stop = false;
 #pragma unroll
@@ -2346,10 +2398,9 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
       if (k < qnt[x]) stop = true;
       else { k -= qnt[x]; sh = x + 1; }
     }
-    const DevNode& P = a.pn[ai + sh];
     const NodeResult& r = a.pres[ai + sh];
     PartTile* pt = a.cpt + j;
-    pt->tile = a.ptiles + P.tile_begin + k;
+    pt->tile = a.ptiles + a.psum[ai + sh].tile_begin + k;
     pt->parent = a.pn + ai + sh;
     int32_t thr0, sh0, thr1, sh1;
     plan_cut(r, 0, &thr0, &sh0);
@@ -2360,6 +2411,7 @@ __global__ __launch_bounds__(kPlanBlock) void plan_kernel(PlanArgs a, uint32_t n
     pt->shift[1] = sh1;
     pt->child[0] = (2 * i) * S + sh;
     pt->child[1] = (2 * i + 1) * S + sh;
+  }
   }
 }
 
@@ -3057,9 +3109,13 @@ void launch_plansplit(const PlanArgs& pa, const RoundArgs& a, int grid, int fmt,
 
 void launch_plan(const PlanArgs& a, hipStream_t stream) {
   const uint32_t nb_rec = (uint32_t)max(1, (a.np * a.nshard + kPlanBlock - 1) / kPlanBlock);
-  const uint32_t nb_tile = (max(a.tiles_cap, a.ptiles_cap) + kPlanBlock - 1) / kPlanBlock;
-  if (a.nshard > 1) plan_kernel<true><<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
-  else plan_kernel<false><<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
+  uint32_t nb_tile = (max(a.tiles_cap, a.ptiles_cap) + kPlanBlock - 1) / kPlanBlock;
+  if (a.nshard > 1) {   // (grid-stride tile workgroups: see plan_kernel (2b))
+    nb_tile = min(nb_tile, (uint32_t)kPlanShardTileWgs);
+    plan_kernel<true><<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
+  } else {
+    plan_kernel<false><<<dim3(nb_rec + nb_tile), dim3(kPlanBlock), 0, stream>>>(a, nb_rec);
+  }
 }
 
 void launch_zero(void* dst, size_t bytes, hipStream_t stream) {
