@@ -1547,6 +1547,15 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     if (!active.empty()) q.push_back(enqueue_host_round(active, false, max_iters, stream));
   }
   const double t_clu = trace_ ? host_us() : 0.0;
+  // The next run's planned rounds find their blocks zero: clear what this run
+  // used, behind the last round's kernels -- here, before the host's colour
+  // table work, so the clear runs while the host dedups instead of behind the
+  // map (at the next run's start it delayed the first round by ~8 us).
+  for (size_t c = 0; c < arena_.size(); ++c)
+    if (arena_hw_[c] > 0) {
+      launch_zero(arena_[c].first, arena_hw_[c], stream);   // (chunks and allocations: 256-B multiples)
+      arena_hw_[c] = 0;
+    }
 
   for (int i = 0; i < nframes; ++i) finish_frame(frames_[i], i == nframes - 1);
 
@@ -1578,14 +1587,6 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     }
     if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream, false);
   }
-  // The next run's planned rounds find their blocks zero: clear what this run
-  // used, behind its last kernel (at the next run's start it delayed the
-  // first round by ~8 us).
-  for (size_t c = 0; c < arena_.size(); ++c)
-    if (arena_hw_[c] > 0) {
-      launch_zero(arena_[c].first, arena_hw_[c], stream);   // (chunks and allocations: 256-B multiples)
-      arena_hw_[c] = 0;
-    }
   // Synchronous on return: lookahead launches of the last round may still be
   // queued, and they read the caller's input.
   const double ts0 = trace_ ? host_us() : 0.0;

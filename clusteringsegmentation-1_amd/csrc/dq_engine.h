@@ -409,7 +409,7 @@ class Engine {
   bool speculate_kmeans_ = true;      // a round with nothing queued behind it starts its
                                       //   2-means iterations before its split status (DQ_HIP_TUNE spec_kmeans)
   uint32_t kloop_max_ = 49152;        // a record's points at most for kloop_kernel (DQ_HIP_TUNE kloop_max; 0: off)
-  int tiles_target_ = 1024;           // tiles per big round (DQ_HIP_TUNE tiles)
+  int tiles_target_ = 512;            // tiles per big round (DQ_HIP_TUNE tiles; 512 vs 1024: C3 -4 %)
   int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_TUNE node_tiles)
   uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TUNE tile_max)
   // host-side trace (DQ_HIP_TRACE=1): per-run phase times on stderr
