@@ -34,7 +34,19 @@ def per_kernel(path, counter):
             name = name.replace("<false>", "").replace("<true>", "")
             tot[name] += float(r["Counter_Value"])
             cnt[name] += 1
-    return {k: (tot[k] / cnt[k], cnt[k]) for k in tot}
+    out = {k: (tot[k] / cnt[k], cnt[k]) for k in tot}
+    # kernels specialised per (mode, format) (partsplit_kernel<0, 2>, ...): also
+    # the average over all their launches under the bare name, as bench.py's
+    # HIP events time them (one kind)
+    base = collections.defaultdict(lambda: [0.0, 0])
+    for k in tot:
+        if "<" in k and "," in k:
+            b = base[k.split("<")[0]]
+            b[0] += tot[k]
+            b[1] += cnt[k]
+    for k, (t, c) in base.items():
+        out.setdefault(k, (t / c, c))
+    return out
 
 
 def main():

@@ -27,6 +27,13 @@ def main():
     want = {"<PASS_KMEANS>": "<2>", "<PASS_KLAST>": "<3>"}.get(tmpl, tmpl)
     hit = [r for r in rows if ("dq::" + sym + want + "(") in r["Name"] or
            (not want and ("dq::" + sym + "(") in r["Name"])]
+    if not hit and not want:   # specialised per (mode, format): all of them, as the bench times them
+        hit = [r for r in rows if ("dq::" + sym + "<") in r["Name"]]
+        if hit:
+            calls = sum(int(r["Calls"]) for r in hit)
+            tot = sum(float(r["TotalDurationNs"]) for r in hit)
+            hit = [{"Name": " + ".join(r["Name"].split("(")[0] for r in hit), "Calls": calls,
+                    "AverageNs": tot / calls}]
     if not hit:
         raise SystemExit("kernel %s not in %s" % (roof["kernel"], stats[0]))
     r = hit[0]
