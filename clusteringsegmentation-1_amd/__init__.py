@@ -600,7 +600,8 @@ def set_debug(flags, device=0):
     """Test-only interleaving knobs (dq_hip.h dq_hip_set_debug; 0 in production):
     1 prewarm the 2-means hand-off lines, 2 uneven workgroup stalls, 4 host
     delays between a round's status and its results, 8 plan-kernel stall,
-    16 check that the round arena is all zero when a run starts."""
+    16 check that the round arena is all zero when a run starts, 32 release the
+    round arena at every run's start (its rounds allocate new chunks)."""
     lib().dq_hip_set_debug(device, int(flags))
 
 

@@ -1375,6 +1375,11 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   if (!stream) stream = stream_;
   debug_ = debug_flags();
   if (debug_ & kDebugArenaCheck) check_arena_zero(stream);
+  if (debug_ & kDebugFreshArena) {   // (nothing of this engine in flight: the previous run synced)
+    for (auto& c : arena_) DQ_HIP(hipFree(c.first));
+    arena_.clear();
+    arena_hw_.clear();
+  }
 
   frames_.assign(nframes, FrameState());
   nodes_.clear();

@@ -141,8 +141,12 @@ constexpr int kPlanMaxParents = 6144;   // parents per planned round (LDS scans)
 //   kDebugArenaCheck: every run first checks on the host that the round
 //                    arena is all zero (the planned rounds' invariant) and
 //                    aborts naming the first non-zero byte.
+//   kDebugFreshArena: every run first releases the round arena, so its
+//                    rounds allocate (and clear) new chunks while the other
+//                    lanes' runs are in flight -- the order in which a
+//                    null-stream clear once raced the round's kernels.
 constexpr int32_t kDebugPrewarm = 1, kDebugUneven = 2, kDebugHostDelay = 4, kDebugPlanStall = 8,
-                  kDebugArenaCheck = 16;
+                  kDebugArenaCheck = 16, kDebugFreshArena = 32;
 // plan_kernel: the planned round's tables.  Like plansplit below, it relies on
 // the round block's [LaunchCtr | wparts | rdone | summaries] being zero on
 // entry (the round arena's invariant, Engine::run).

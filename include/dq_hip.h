@@ -258,7 +258,8 @@ const char *dq_hip_stat_name(int kind);
  * dq_hip_set_debug: interleaving knobs for the hand-off tests (flags of
  * dq_kernels.h kDebug*: 1 prewarm the 2-means hand-off lines, 2 uneven
  * workgroup stalls, 4 host delays between status and results, 8 plan-kernel
- * stall, 16 abort unless the round arena is all zero when a run starts); every
+ * stall, 16 abort unless the round arena is all zero when a run starts, 32
+ * release the round arena at every run's start: new chunks); every
  * lane of `device`; 0 (the default) in production.  Outputs are identical
  * under every flag. */
 uint64_t dq_hip_build_id(void);

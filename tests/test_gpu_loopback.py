@@ -210,3 +210,33 @@ def test_arena_zero_after_sharded_runs(gpu):
                 assert "%016x" % fx.fnv(t_out[f].cpu().numpy().view(np.uint32)) == fix["f%02d" % f]["out_fnv"]
     finally:
         gpu.set_debug(0)
+
+
+def test_fresh_arena_chunks_under_concurrent_lanes(gpu):
+    """Regression for the round-4 abort (DESIGN.md 3c''): a new arena chunk
+    was cleared by a null-stream hipMemset that nothing ordered before the
+    round's kernels.  With kDebugFreshArena every run of every lane
+    allocates (and clears) new chunks while the other lanes run, each call
+    entered with the caller's stream busy; 4-frame batches over the default
+    lanes, checked against the reference's hashes.  (The buggy build did not
+    fail this test on three tries: the race needs the clear to queue behind
+    other work -- a guard, not a deterministic reproducer.)"""
+    import torch
+    fix = fx.load_json("c4.json")
+    t_in = [torch.from_numpy(fx.xorshift(W4 * H4, seed=fx.SEED + f).view(np.int32)).to("cuda:0")
+            for f in range(4)]
+    t_out = [torch.empty_like(t) for t in t_in]
+    busy = torch.empty(1 << 28, dtype=torch.int32, device="cuda:0")
+    try:
+        gpu.set_debug(32 | 16)
+        for _ in range(3):
+            # the caller's (null) stream busy when the call starts: the lanes
+            # join it, and so would a null-stream clear
+            busy.fill_(7)
+            cts, _ = gpu.quant_batch_device(t_in, t_out, 256)
+            torch.cuda.synchronize()
+            for f in range(4):
+                assert [int(v) for v in cts[f]] == fix["f%02d" % f]["ct"], f
+                assert "%016x" % fx.fnv(t_out[f].cpu().numpy().view(np.uint32)) == fix["f%02d" % f]["out_fnv"]
+    finally:
+        gpu.set_debug(0)
