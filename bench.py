@@ -54,6 +54,13 @@ import time
 
 import numpy as np
 
+# HIP's hardware queues per process (its default is 4): one per engine lane
+# plus the caller's stream, set before anything initialises HIP -- the
+# library then runs 4 lanes per batch (dq_engine.cpp batch_lanes)
+_HWQ = int(os.environ.get("DQ_BENCH_HW_QUEUES", "8"))   # (A/B: the queue count to run with)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) != _HWQ:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_HWQ)
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")

@@ -2332,7 +2332,11 @@ int batch_lanes() {
     // 3 lanes: 1.29 ms per 8 x 4K vs 1.33 with 2 (each lane's chain of
     // partition -> plan -> 2-means launches overlaps two others); 4 lanes
     // exceed HIP's default 4 hardware queues with the caller's stream (1.6 ms)
-    return v && v[0] ? std::max(1, std::min(kMaxLanes, atoi(v))) : 3;
+    // -- with GPU_MAX_HW_QUEUES >= 6 every lane's stream has a queue of its
+    // own and 4 lanes win (1.21 -> 1.18-1.19 ms; 5 or 6 lanes: 1.64-1.75)
+    const char* q = getenv("GPU_MAX_HW_QUEUES");
+    const int dflt = q && atoi(q) >= 6 ? 4 : 3;
+    return v && v[0] ? std::max(1, std::min(kMaxLanes, atoi(v))) : dflt;
   }();
   const int o = g_lanes_override.load();
   return o > 0 ? std::min(o, kMaxLanes) : lanes;
