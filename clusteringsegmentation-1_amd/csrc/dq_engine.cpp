@@ -698,6 +698,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   }
   const double tb1 = trace_ ? host_us() : 0.0;
   // one upload kernel on the round's stream (no copy-engine hop)
+  if (trace_ && root_round) tr_first_us_ = host_us() - tr_entry_t0_;
   launch_upload(dblk, d_stage_view_, bytes, stream);
   if (trace_) tr_build_us_ += host_us() - tb0;
 
@@ -1371,6 +1372,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
                  hipStream_t stream) {
   DQ_CHECK(nframes > 0, "empty batch");
   DQ_CHECK(max_iters >= 1, "max_iters < 1 is not supported (the reference never writes member[] then)");
+  tr_entry_t0_ = trace_ ? host_us() : 0.0;
   DQ_HIP(hipSetDevice(device_));
   if (!stream) stream = stream_;
   debug_ = debug_flags();
@@ -1603,10 +1605,10 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     std::fprintf(stderr, "divquant-hip trace: map prep %.1fus, map launch+sync %.1fus\n",
                  tr_mapprep_us_, tr_mapsync_us_);
     std::fprintf(stderr,
-                 "divquant-hip trace: frames=%d shards=%d rounds=%d cluster=%.1fus (build %.1f, "
-                 "wait %.1f, replay %.1f) map+sync=%.1fus total=%.1fus\n",
-                 nframes, S, last_rounds, t_clu - t_run0, tr_build_us_, tr_wait_us_,
-                 tr_replay_us_, t_end - t_clu, t_end - t_run0);
+                 "divquant-hip trace: frames=%d shards=%d rounds=%d entry->first launch %.1fus "
+                 "cluster=%.1fus (build %.1f, wait %.1f, replay %.1f) map+sync=%.1fus total=%.1fus\n",
+                 nframes, S, last_rounds, tr_first_us_, t_clu - t_run0, tr_build_us_, tr_wait_us_,
+                 tr_replay_us_, t_end - t_clu, t_end - tr_entry_t0_);
   }
 }
 

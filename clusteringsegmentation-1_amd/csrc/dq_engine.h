@@ -416,6 +416,7 @@ class Engine {
   bool trace_ = false, trace_rounds_ = false;   // DQ_HIP_TRACE=1 / 2 (per round)
   double tr_wait_us_ = 0, tr_build_us_ = 0, tr_replay_us_ = 0;
   double tr_mapprep_us_ = 0, tr_mapsync_us_ = 0;
+  double tr_entry_t0_ = 0, tr_first_us_ = 0;   // run() entry; entry -> the root round's first launch
 
   // map tables
   uint32_t* d_cell_c32_ = nullptr;    // compact records per map task of a chunk
