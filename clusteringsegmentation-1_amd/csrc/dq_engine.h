@@ -411,7 +411,7 @@ class Engine {
   uint32_t kloop_max_ = 49152;        // a record's points at most for kloop_kernel (DQ_HIP_TUNE kloop_max; 0: off)
   int tiles_target_ = 512;            // tiles per big round (DQ_HIP_TUNE tiles; 512 vs 1024: C3 -4 %)
   int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_TUNE node_tiles)
-  uint32_t tile_max_ = kMaxTilePx;    // points per tile at most (DQ_HIP_TUNE tile_max)
+  uint32_t tile_max_ = kMaxTilePx / 2;   // points per tile at most (DQ_HIP_TUNE tile_max; 32K vs 64K: C5 -2 %)
   // host-side trace (DQ_HIP_TRACE=1): per-run phase times on stderr
   bool trace_ = false, trace_rounds_ = false;   // DQ_HIP_TRACE=1 / 2 (per round)
   double tr_wait_us_ = 0, tr_build_us_ = 0, tr_replay_us_ = 0;
