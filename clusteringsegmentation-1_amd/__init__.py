@@ -583,7 +583,8 @@ def last_loop_rounds(device=0):
 
 
 def set_lanes(lanes):
-    """Engine lanes a batch is split over (0: default, DQ_HIP_LANES or 3)."""
+    """Engine lanes a batch is split over (0: default, DQ_HIP_LANES, else 4 with
+    GPU_MAX_HW_QUEUES >= 6, else 3)."""
     lib().dq_hip_set_lanes(int(lanes))
 
 

@@ -6,6 +6,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -151,3 +152,17 @@ def test_library_built_from_these_sources(pkg):
     sid = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(sid)
     assert pkg.build_id() == sid.source_id(), "libdivquant_hip.so is stale: run make -C clusteringsegmentation-1_amd"
+
+
+def test_default_lanes_follow_hw_queues():
+    """A batch's default engine lanes: 3 on HIP's default 4 hardware queues,
+    4 when the process has GPU_MAX_HW_QUEUES >= 6 (each lane's stream plus the
+    caller's on a queue of its own); DQ_HIP_LANES overrides (host-only: no GPU
+    call is made)."""
+    code = ("import sys; sys.path.insert(0, %r); from __graft_entry__ import load_package; "
+            "print(load_package().get_lanes())" % ROOT)
+    env0 = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "DQ_HIP_LANES")}
+    for extra, want in (({}, 3), ({"GPU_MAX_HW_QUEUES": "4"}, 3), ({"GPU_MAX_HW_QUEUES": "8"}, 4),
+                        ({"GPU_MAX_HW_QUEUES": "8", "DQ_HIP_LANES": "2"}, 2)):
+        out = subprocess.check_output([sys.executable, "-c", code], env=dict(env0, **extra), text=True)
+        assert int(out.strip().splitlines()[-1]) == want, (extra, out)
