@@ -836,7 +836,10 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   // partition only sums (PS_STATS); the points of parents with a child left
   // active go out after the split epilogue (PS_LATE), the rest only if a
   // later round reads them (enqueue_host_round, PS_WRITE)
-  R.stats_only = stats_only_;
+  // (rounds of at most one 4K frame's points write them all instead: the
+  // single-frame chain's PS_STATS + PS_LATE launches cost more than PS_FULL's
+  // writes -- C3 -1.5-2 %, C2 -0.5 %; batches keep the stats-only form)
+  R.stats_only = stats_only_ && total > kFusePlanMaxPoints;
   for (int32_t a : plist) {
     const FrameState& f = frames_[nodes_[P.order[a]].frame];
     R.stats_only = R.stats_only && f.splits_queued >= f.job->k - 1;
