@@ -2088,6 +2088,28 @@ void Engine::map_many(const MapJob* jobs, int njobs, hipStream_t stream, bool sy
     DQ_CHECK(jobs[i].k > 0, "colormapSize must be > 0 (DivQuantMapColors.cpp:264)");
     DQ_CHECK(jobs[i].k <= (int)kMapPal, "colormapSize > 16384 is not supported by the LDS palette");
   }
+  // A task maps at most kMapTaskMax pixels: map_lds_kernel stores through a
+  // buffer resource whose byte range (4 n) must stay below 2^31.  Larger jobs
+  // become consecutive tasks over the same colortable (they then share one
+  // palette block and cell table, as a frame's row shards do).
+  std::vector<MapJob> split;
+  {
+    bool big = false;
+    for (int i = 0; i < njobs; ++i) big |= jobs[i].n > kMapTaskMax;
+    if (big) {
+      for (int i = 0; i < njobs; ++i)
+        for (uint32_t o = 0; o == 0 || o < jobs[i].n; o += kMapTaskMax) {
+          MapJob j = jobs[i];
+          j.n = std::min<uint32_t>(kMapTaskMax, jobs[i].n - o);
+          j.d_in = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(jobs[i].d_in) +
+                                                     (size_t)o * (jobs[i].bgr ? 3 : 4));
+          j.d_out = jobs[i].d_out + o;
+          split.push_back(j);
+        }
+      jobs = split.data();
+      njobs = (int)split.size();
+    }
+  }
   // BGR24 frames: map_lds_kernel reads them directly (K <= 1024, 8-B aligned
   // in, 16-B aligned out); otherwise they are packed first (bgr24_pack)
   std::vector<MapJob> packed;

@@ -163,6 +163,9 @@ class Engine {
   // map_colors_mps (DivQuantMapColors.cpp:243-539) on device buffers.
   void map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
            const uint32_t* ct, int k, hipStream_t stream);
+  // pixels per map task (map_many splits larger jobs; 4 n < 2^31 for the
+  // output's buffer resource, 16-B aligned sub-jobs)
+  static constexpr uint32_t kMapTaskMax = 1u << 28;
   struct MapJob {
     const uint32_t* d_in;
     uint32_t n;

@@ -1169,24 +1169,6 @@ __device__ __forceinline__ void chunk_next(ChunkAcc& c) {
   c.end = min(c.t0 + (c.w + 1u) * c.q, c.tend);
 }
 
-// Book one sweep's points [p0, p1) of this child: lanecnt = the lane's new
-// points among them, lanepre = those below the chunk end (slow sweeps).
-__device__ __forceinline__ void chunk_sweep(ChunkAcc& c, uint32_t p0, uint32_t p1, uint32_t lanecnt,
-                                            uint32_t lanepre) {
-  if (!c.on) return;
-  if (p1 <= c.end) {
-    c.acc += p1 - p0;
-    c.lnew += lanecnt;
-    return;
-  }
-  const uint32_t before = c.end - p0;
-  c.acc += before;
-  c.lnew += lanepre;
-  chunk_next(c);
-  c.acc = (p1 - p0) - before;
-  c.lnew = lanecnt - lanepre;
-}
-
 __device__ __forceinline__ void chunk_finish(ChunkAcc& c) {
   if (!c.on) return;
   const uint32_t nn = wave_sum_u32(c.lnew);
@@ -1254,12 +1236,18 @@ __device__ __forceinline__ uint32_t mask_count(const SweepMask& m) {
   return c;
 }
 
-// Count, sums and sums of squares over the slots of a byte mask.
-__device__ __forceinline__ void add_sums_bytes(const Sweep& w, const SweepMask& m, SplitSums& s) {
-  s.cnt += mask_count(m);
+// Count (cnt: mask_count(m)), sums and sums of squares over the slots of a
+// byte mask.
+__device__ __forceinline__ void add_sums_bytes(const Sweep& w, const SweepMask& m, uint32_t cnt, SplitSums& s) {
+  s.cnt += cnt;
 #pragma unroll
   for (int j = 0; j < kVecPerThread; ++j) {
-    const uint32_t wt = m.m[j], mk = (wt << 8) - wt;   // 0x01 -> 0xFF per byte
+    // 0x01 -> 0xFF per byte as a shift and a subtract: left alone the
+    // compiler folds them into a quarter-rate v_mul_lo_u32 (x 0xFF)
+    const uint32_t wt = m.m[j];
+    uint32_t sh = wt << 8;
+    asm("" : "+v"(sh));
+    const uint32_t mk = sh - wt;
     s.sr = __builtin_amdgcn_udot4(w.r[j], wt, s.sr, false);
     s.sg = __builtin_amdgcn_udot4(w.g[j], wt, s.sg, false);
     s.sb = __builtin_amdgcn_udot4(w.b[j], wt, s.sb, false);
@@ -1336,27 +1324,18 @@ struct Stage {
 
 // This wave's points of one sweep into the staging, slot by slot, ranked by
 // ballot (a full sweep: a lane's rank among the new points is its lane id
-// minus its rank among the old ones).  PRE: also count, per lane, the
-// children's split-new points (xm / ym) at child positions below ex / ey.
-template <bool PRE, bool STORE = true>
+// minus its rank among the old ones).  Each run's positions are in slot-major
+// order: slot s's points follow slot s-1's, by lane (run_below relies on it).
+template <bool STORE = true>
 __device__ __forceinline__ void stage_sweep(const Sweep& w, const SweepMask& om, const SweepMask& nm, bool full,
-                                            uint8_t* st, Stage& g, uint32_t l, const SweepMask& xm,
-                                            const SweepMask& ym, uint32_t ex, uint32_t ey, uint32_t& ax,
-                                            uint32_t& ay) {
+                                            uint8_t* st, Stage& g, uint32_t l) {
   constexpr int kSlots = kVecPerThread * 4;
-  // PRE thresholds relative to the regions (ex >= cbo, ey >= cbn: chunk ends
-  // at or past the runs' next positions, or ~0)
-  const uint32_t exs = ex - g.cbo, eys = ey - g.cbn;
   auto put = [&](int s, uint32_t lp) {
     const int j = s >> 2, sh = 8 * (s & 3);
     if (STORE) {   // (STORE false: the run positions only, for the children's counts)
       st[lp] = (uint8_t)(w.r[j] >> sh);
       st[kStagePlane + lp] = (uint8_t)(w.g[j] >> sh);
       st[2 * kStagePlane + lp] = (uint8_t)(w.b[j] >> sh);
-    }
-    if (PRE) {
-      ax += (uint32_t)(slot_in(xm, s) && lp < exs);
-      ay += (uint32_t)(slot_in(ym, s) && lp - kStageRun < eys);
     }
   };
   if (full) {   // (wave-uniform)
@@ -1366,8 +1345,10 @@ __device__ __forceinline__ void stage_sweep(const Sweep& w, const SweepMask& om,
     for (int s = 0; s < kSlots; ++s) {
       const bool o = slot_in(om, s);
       const uint64_t bo = __ballot(o);
-      const uint32_t ro = mbcnt64(bo);
-      put(s, o ? g.po + ro : t - ro);
+      if (STORE) {
+        const uint32_t ro = mbcnt64(bo);
+        put(s, o ? g.po + ro : t - ro);
+      }
       const uint32_t co = (uint32_t)__popcll(bo);
       g.po += co;
       t += 64u - co;
@@ -1378,12 +1359,64 @@ __device__ __forceinline__ void stage_sweep(const Sweep& w, const SweepMask& om,
     for (int s = 0; s < kSlots; ++s) {
       const bool o = slot_in(om, s), n = slot_in(nm, s);
       const uint64_t bo = __ballot(o), bn = __ballot(n);
-      if (o || n) put(s, o ? g.po + mbcnt64(bo) : g.pn + mbcnt64(bn));
+      if (STORE && (o || n)) put(s, o ? g.po + mbcnt64(bo) : g.pn + mbcnt64(bn));
       g.po += (uint32_t)__popcll(bo);
       g.pn += (uint32_t)__popcll(bn);
     }
   }
 }
+
+// Slots of a byte mask as lane bits (bit s = slot s): bytes 0x00 / 0x01 of
+// word j -> bits 4j..4j+3 (the multiply moves byte e's bit to bit 24 + e,
+// no carries).
+__device__ __forceinline__ uint32_t bytes_to_bits(const SweepMask& m) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int j = 0; j < kVecPerThread; ++j) b |= ((m.m[j] * 0x01020408u) >> 24) << (4 * j);
+  return b;
+}
+
+// This lane's points of xb (a subset of its run members mb, bit s = slot s)
+// among the first `rel` positions of the sweep's run (slot-major, lanes by
+// rank within a slot: stage_sweep's order).  Only on sweeps whose run
+// crosses a chunk end: the slot holding position rel - 1 is found by a scan
+// of the slots' ballot counts (a uniform loop); below it every member
+// counts, in it those of rank below the rest.  (Was a compare per slot and
+// lane on every such sweep.)
+__device__ __forceinline__ uint32_t run_below(uint32_t mb, uint32_t xb, uint32_t rel) {
+  uint32_t cum = 0, ss = 0;
+  uint64_t bs;
+#pragma unroll 1
+  for (;; ++ss) {   // (wave-uniform; rel < the run's count, so a slot holds position rel - 1)
+    bs = __ballot((mb >> ss) & 1u);
+    const uint32_t c = (uint32_t)__popcll(bs);
+    if (rel <= cum + c || ss == kVecPerThread * 4 - 1) break;
+    cum += c;
+  }
+  const uint32_t low = (uint32_t)__builtin_popcount(xb & ((1u << ss) - 1u));
+  const bool in = ((xb >> ss) & 1u) != 0u && mbcnt64(bs) < rel - cum;
+  return low + (in ? 1u : 0u);
+}
+
+// Book one sweep's points [p0, p1) of this child's run: mb = the lane's run
+// members, xm = those on the child's split-new side, cnt = mask_count(xm).
+__device__ __forceinline__ void chunk_sweep(ChunkAcc& c, uint32_t p0, uint32_t p1, const SweepMask& mb,
+                                            const SweepMask& xm, uint32_t cnt) {
+  if (!c.on) return;
+  if (p1 <= c.end) {
+    c.acc += p1 - p0;
+    c.lnew += cnt;
+    return;
+  }
+  const uint32_t before = c.end - p0;
+  const uint32_t pre = run_below(bytes_to_bits(mb), bytes_to_bits(xm), before);
+  c.acc += before;
+  c.lnew += pre;
+  chunk_next(c);
+  c.acc = (p1 - p0) - before;
+  c.lnew = cnt - pre;
+}
+
 
 // Lanes 0-15 / 16-31 write the staged bytes i of the old / new run's first
 // chunk whose child positions lie in [max(cb, lo), hi).
@@ -1563,6 +1596,7 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     // HERE (the asm makes x a value of its own): left to the compiler, the
     // loop-carried copy sat at the end of the sweep and waited there for the
     // loads the sweep had just issued, exposing the memory latency per sweep
+    // (2 sweeps of loads in flight measured no faster, tools/psbench)
     RawSweep x = xn;
     asm volatile("" : "+v"(x.v[0]), "+v"(x.v[1]), "+v"(x.v[2]), "+v"(x.v[3]));
     const uint32_t nvs = vs + kWaveSweep;
@@ -1586,10 +1620,10 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
       }
     } else {
       const uint32_t validm = valid_mask<PLANAR>(vs, start, end);
-      const uint32_t oldm = cut ? validm & ~cut_new_mask(sw, (uint32_t)q.shift, q.thr)
-                                : old_mask(sw, validm, q, exact_all);
-      om = bits_to_bytes(oldm);
-      nm = bits_to_bytes(validm & ~oldm);
+      const uint32_t ob = cut ? validm & ~cut_new_mask(sw, (uint32_t)q.shift, q.thr)
+                              : old_mask(sw, validm, q, exact_all);
+      om = bits_to_bytes(ob);
+      nm = bits_to_bytes(validm & ~ob);
     }
     // the children's split pass on the same registers (cut_pos < v_axis <=>
     // v_axis >= thr): each child's new-side slots, counted and summed
@@ -1599,23 +1633,18 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
       xm.m[j] &= om.m[j];   // new for the old child
       ym.m[j] &= nm.m[j];   // new for the new child
     }
+    const uint32_t xc = mask_count(xm), yc = mask_count(ym);
     if (kSums) {
-      add_sums_bytes(sw, xm, so);
-      add_sums_bytes(sw, ym, sn);
+      add_sums_bytes(sw, xm, xc, so);
+      add_sums_bytes(sw, ym, yc, sn);
     }
-    // this wave's points.  A sweep writes at most kWaveSweep points to each
-    // child: when neither child's current chunk can end inside it (fast
-    // sweep), only the lanes' new counts are kept; otherwise every slot's run
-    // is split exactly.
+    // this wave's points into the runs (PS_STATS: the run positions only --
+    // the children's per-(tile, wave) counts are the partition cursors a
+    // later round may need -- no stores)
     const uint32_t oc = g.cbo + g.po, nc = g.cbn + g.pn - kPnOff;
-    const bool fast = oc + kWaveSweep <= cx.end && nc + kWaveSweep <= cy.end;
-    uint32_t ax = 0, ay = 0;
-    // (PS_STATS: the run positions only -- the children's per-(tile, wave)
-    // counts are the partition cursors a later round may need -- no stores)
-    if (fast) stage_sweep<false, kStore>(sw, om, nm, full, st, g, l, xm, ym, 0u, 0u, ax, ay);
-    else stage_sweep<true, kStore>(sw, om, nm, full, st, g, l, xm, ym, cx.end, cy.end, ax, ay);
-    chunk_sweep(cx, oc, g.cbo + g.po, mask_count(xm), ax);
-    chunk_sweep(cy, nc, g.cbn + g.pn - kPnOff, mask_count(ym), ay);
+    stage_sweep<kStore>(sw, om, nm, full, st, g, l);
+    chunk_sweep(cx, oc, g.cbo + g.po, om, xm, xc);
+    chunk_sweep(cy, nc, g.cbn + g.pn - kPnOff, nm, ym, yc);
     if (kStore) stage_flush(st, d, g, l);
     vs = nvs;
     full = nfull;
@@ -2845,7 +2874,7 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   // stores at kOOB (dropped), so every iteration issues the same count of
   // vector-memory operations after its loads (see the loop's top)
   const __amdgpu_buffer_rsrc_t orsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)tk.out, (short)0, (int)min(4u * n, 0x7FFFFFF0u), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)tk.out, (short)0, (int)(4ull * n), 0x00020000);   // (n <= 2^28: Engine::map_many)
 
   // (c2 - 2 dot) << 12 | sad, as (c2 << 12) - (dot << 13) + sad: the low 12
   // bits of the first two terms are zero and sad < 4096, so the OR is an add

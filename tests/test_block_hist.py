@@ -73,6 +73,29 @@ def test_subdivided_colors(pkg):
     assert len(set(ours.tolist())) == 125
 
 
+def test_subdivided_colors_reference_test(pkg):
+    """The reference's own test of this palette, testSegmentColorCube
+    (Test/CoordTest.mm:2101-2170), restated on the library's table: 125
+    entries; the entries with R = G = 0 are exactly five, B = 0, 63, 127, 191,
+    255 in table order, and they are colortable[0..4] = 0xFF000000,
+    0xFF00003F, 0xFF00007F, 0xFF0000BF, 0xFF0000FF (the comment block at
+    :2116-2120); every value 0..255 has a nearest of those five bins (first
+    on ties), 256 in all."""
+    vec = pkg.get_subdivided_colors()
+    assert vec.size == 125
+    filtered = [int(p) & 0xFF for p in vec.tolist() if (int(p) & 0x00FFFF00) == 0]
+    assert filtered == [0, 63, 127, 191, 255]
+    assert vec[:5].tolist() == [0xFF000000, 0xFF00003F, 0xFF00007F, 0xFF0000BF, 0xFF0000FF]
+    counts = {}
+    for i in range(256):
+        best, bi = 256, None
+        for j, f in enumerate(filtered):
+            if abs(i - f) < best:
+                best, bi = abs(i - f), j
+        counts[bi] = counts.get(bi, 0) + 1
+    assert sum(counts.values()) == 256 and sorted(counts) == [0, 1, 2, 3, 4]
+
+
 def test_block_grid(pkg):
     # clusteringCombine (ClusteringSegmentationMain.cpp:138-149)
     assert pkg.block_grid(1778, 1000, 4) == (445, 250)

@@ -477,6 +477,33 @@ def test_map_dense_palettes(gpu, kind):
     assert np.array_equal(out, ref)
 
 
+def test_map_above_task_limit(gpu):
+    """A map of more than 2^28 pixels (Engine::kMapTaskMax: map_lds_kernel's
+    output buffer range) is split into tasks; every pixel, the ragged tail
+    past the split included, is mapped (stores past the range were
+    dropped).  Input: a 65536-pixel random block repeated, so the expected
+    output is the oracle's map of the block, repeated."""
+    import torch
+    blk = fx.xorshift(1 << 16, seed=91)
+    rng = np.random.default_rng(5)
+    pal = rng.integers(0, 1 << 24, 200).astype(np.uint32)
+    ref = np.zeros_like(blk)
+    fx.oracle().dqo_map(fx.vp(blk), ctypes.c_uint32(len(blk)), fx.vp(ref), fx.vp(pal), ctypes.c_int(len(pal)))
+    n = (1 << 28) + 1000
+    reps = (n + len(blk) - 1) // len(blk)
+    t_blk = torch.from_numpy(blk.view(np.int32)).to("cuda:0")
+    t_in = t_blk.repeat(reps)[:n].contiguous()
+    t_out = torch.full_like(t_in, -1)
+    gpu.map_device(t_in, t_out, pal)
+    torch.cuda.synchronize()
+    t_ref = torch.from_numpy(ref.view(np.int32)).to("cuda:0")
+    full = n // len(blk)
+    assert bool((t_out[:full * len(blk)].view(full, -1) == t_ref).all())
+    assert bool((t_out[full * len(blk):] == t_ref[:n - full * len(blk)]).all())
+    del t_in, t_out
+    torch.cuda.empty_cache()
+
+
 def test_cpp_linkage_entry_points(gpu):
     """The C++-linkage symbols the reference's callers link against
     (DivQuantHeader.h:52-96): map_colors_mps (ClusteringSegmentation.cpp:408,
