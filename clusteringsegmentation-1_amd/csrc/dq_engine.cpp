@@ -62,6 +62,8 @@ int32_t split_threshold(double cut) {
 
 }  // namespace
 
+double Engine::host_us_now() { return host_us(); }
+
 // Experiment switches, all behind ONE entry point: DQ_HIP_TUNE is a list of
 // key=value pairs ("tiles=768,lookahead=1").  Every setting leaves the
 // outputs identical (they move work between launches, not arithmetic); the
@@ -366,8 +368,14 @@ uint32_t Engine::wait_status(const uint64_t* slot, uint64_t seq, hipStream_t str
   const double t0 = trace_ ? host_us() : 0.0;
   struct Acc {
     Engine* e; double t0;
-    ~Acc() { if (e->trace_) e->tr_wait_us_ += host_us() - t0; }
+    ~Acc() {
+      if (e->trace_) {
+        e->tr_wait_us_ += host_us() - t0;
+        e->tmark("w");
+      }
+    }
   } acc{this, t0};
+  tmark("W");
   const uint32_t want = (uint32_t)seq;
   auto ready = [&](uint32_t* act) {
     const uint64_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
@@ -699,7 +707,9 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   const double tb1 = trace_ ? host_us() : 0.0;
   // one upload kernel on the round's stream (no copy-engine hop)
   if (trace_ && root_round) tr_first_us_ = host_us() - tr_entry_t0_;
+  tmark("host:tables");
   launch_upload(dblk, d_stage_view_, bytes, stream);
+  tmark("upload");
   if (trace_) tr_build_us_ += host_us() - tb0;
 
   R.seq = ++seq_;
@@ -743,6 +753,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     if (tiles > 0) {
       timed_begin(stream);
       launch_pass(kind, ra, tiles, stream);
+      tmark(kind == PASS_INIT ? "init" : "split");
       timed_end(st, pbytes, stream, units);
     }
   };
@@ -754,6 +765,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
       allreduce_totals(nl, stream);
     }
     launch_epilogue(kind, ra, nr, stream);
+    tmark("epi");
     timed_end(ST_EPILOGUE, 0.0, stream);
   };
   if (root_round) {
@@ -771,6 +783,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   // kernels (stream order: after the upload) so that the host submits the
   // first kernels without it in between (~6-15 us of GPU idle at a call's start)
   DQ_HIP(hipEventRecord(stage_ev_, stream));
+  tmark("stage_ev");
   stage_pending_ = true;
   R.t_enq = tb1;
   return ri;
@@ -805,6 +818,7 @@ bool Engine::plan_list(int ri, std::vector<int32_t>* plist) {
 int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, int max_iters,
                                   hipStream_t stream, const uint32_t* cancel) {
   const double tb0 = trace_ ? host_us() : 0.0;
+  tmark("plan:begin");
   rounds_.emplace_back();
   const int ri = (int)rounds_.size() - 1;
   Round& R = rounds_[ri];
@@ -966,6 +980,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
     launch_partsplit(la, (int)R.ptiles_cap, src_fmt(R.parents), stream);
     timed_end(ST_PARTITION, 0.0, stream);
   }
+  tmark("plan:end");
   if (trace_) tr_build_us_ += host_us() - tb0;
   R.t_enq = trace_ ? host_us() : 0.0;
   return ri;
@@ -1024,6 +1039,7 @@ void Engine::kmeans_iter(Round& R, int it, int max_iters, hipStream_t stream) {
   const double bytes_all = 3.0 * (double)R.total;   // (exact per node: finish_round)
   timed_begin(stream);
   launch_kpass(kind, ra, (int)R.ntiles, stream);
+  tmark("kpass");
   timed_end(st, bytes_all, stream);
   if (timing_) R.km_events.push_back({pending_.size() - 1, it});
   if (ra.tot_mode == TOT_ALLREDUCE) {
@@ -1494,6 +1510,8 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
 
   const double t_run0 = trace_ ? host_us() : 0.0;
   tr_wait_us_ = tr_build_us_ = tr_replay_us_ = 0.0;
+  tr_log_.clear();
+  tmark("run");
   last_planned = last_aborted = 0;
   last_loop_rounds = 0;
   {   // this run's capacities (nothing in flight now)
@@ -1519,7 +1537,9 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     const int ri = q.front();
     if (q.size() == 1 && plan_list(ri, &plist)) q.push_back(enqueue_planned_round(ri, plist, max_iters, stream));
     const int succ = q.size() >= 2 && rounds_[q[1]].planned && rounds_[q[1]].prev == ri ? q[1] : -1;
+    tmark("finish:begin");
     const int replan = finish_round(ri, max_iters, stream, q.size() == 1 && speculate_kmeans_, succ);
+    tmark("finish:end");
     q.pop_front();
     last_rounds++;
     if (rounds_[ri].planned) last_planned++;
@@ -1567,7 +1587,9 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
       arena_hw_[c] = 0;
     }
 
+  tmark("zero");
   for (int i = 0; i < nframes; ++i) finish_frame(frames_[i], i == nframes - 1);
+  tmark("finish_frame");
 
   if (dedup_map) {
     std::vector<MapJob> mj;
@@ -1596,15 +1618,24 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
           if (f.n[sh] > 0) mj.push_back(MapJob{f.in[sh], f.n[sh], j.d_out + f.first[sh], j.ct, m, j.bgr});
     }
     if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream, false);
+    tmark("map:enqueued");
   }
   // Synchronous on return: lookahead launches of the last round may still be
   // queued, and they read the caller's input.
   const double ts0 = trace_ ? host_us() : 0.0;
   sync_stream(stream);
+  tmark("synced");
   if (trace_) tr_mapsync_us_ = host_us() - ts0;
   collect_timing();
   if (trace_) {
     const double t_end = host_us();
+    std::string lg;
+    char buf[64];
+    for (auto& e : tr_log_) {
+      std::snprintf(buf, sizeof buf, " %s@%.1f", e.first, e.second - tr_entry_t0_);
+      lg += buf;
+    }
+    std::fprintf(stderr, "divquant-hip trace: launches%s\n", lg.c_str());
     std::fprintf(stderr, "divquant-hip trace: map prep %.1fus, map launch+sync %.1fus\n",
                  tr_mapprep_us_, tr_mapsync_us_);
     std::fprintf(stderr,

@@ -420,6 +420,13 @@ class Engine {
   double tr_wait_us_ = 0, tr_build_us_ = 0, tr_replay_us_ = 0;
   double tr_mapprep_us_ = 0, tr_mapsync_us_ = 0;
   double tr_entry_t0_ = 0, tr_first_us_ = 0;   // run() entry; entry -> the root round's first launch
+  // DQ_HIP_TRACE: host timestamps of the call's launches and waits (printed
+  // relative to run() entry as one line per call)
+  std::vector<std::pair<const char*, double>> tr_log_;
+  void tmark(const char* what) {
+    if (trace_) tr_log_.emplace_back(what, host_us_now());
+  }
+  static double host_us_now();
 
   // map tables
   uint32_t* d_cell_c32_ = nullptr;    // compact records per map task of a chunk
