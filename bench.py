@@ -21,7 +21,9 @@ Workload (BASELINE.json metric "Mpixels/sec DivQuant K=256 on 4K RGB"):
     detail.c4_rowtile C4's row-tile variant: all 64 frames, each row-sharded
                       over the N ranks, one allreduce of every frame's node
                       totals per pass;
-    detail.bgr24_input the C3 frame and the rank's batch as BGR24 Mats.
+    detail.bgr24_input the C3 frame and the rank's batch as BGR24 Mats;
+    detail.weighted_c3 the C3 frame through the weighted path
+                      (allPixelsUnique=0, the app's live call).
 * --mode rows: F frames of the config (default 1; --config c5: the
   16384x16384 K=1024 gigapixel tile) row-tile sharded over the N ranks
   ("scaling": "strong": the total work is fixed).
@@ -57,8 +59,11 @@ import numpy as np
 # HIP's hardware queues per process (its default is 4): one per engine lane
 # plus the caller's stream, set before anything initialises HIP -- the
 # library then runs 4 lanes per batch (dq_engine.cpp batch_lanes)
+# (GPU_MAX_HW_QUEUES is read once, when HIP initialises: it must be set
+# before any HIP call of the process; the bench line records it)
 _HWQ = int(os.environ.get("DQ_BENCH_HW_QUEUES", "8"))   # (A/B: the queue count to run with)
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) != _HWQ:
+_HWQ_CALLER = os.environ.get("GPU_MAX_HW_QUEUES")
+if int(_HWQ_CALLER or 4) != _HWQ:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_HWQ)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -102,6 +107,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip the HIP-event roofline region")
     ap.add_argument("--no-c3", action="store_true", help="skip the single-frame C3 measurement")
+    ap.add_argument("--no-weighted", action="store_true", help="skip the weighted-path (allPixelsUnique=0) C3 leg")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 (1080p K=256) measurement")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (16384^2 K=1024) measurement")
     ap.add_argument("--no-rowtile", action="store_true", help="skip the C4 row-tile measurement")
@@ -378,9 +384,12 @@ def rows_leg(ctx, cfg, nf, steps, warmup, verify):
     return dt, ok, comm
 
 
-def frame_leg(ctx, cfg, steps, verify):
+def frame_leg(ctx, cfg, steps, verify, uniq=1):
     """One frame of config `cfg` per call (this rank's frame 0 of the config:
-    the fixture's frame at N=1); returns (dt, verified)."""
+    the fixture's frame at N=1); returns (dt, verified).  uniq=0: the weighted
+    path (allPixelsUnique=0, calc_color_table + ordered FP64 folds), checked
+    against the same uniform-weight fixture (the two paths' outputs
+    are identical on 4K noise, from the reference build itself)."""
     torch, pkg, dev, local, rank, world, stream = (ctx[k] for k in
                                                    ("torch", "pkg", "dev", "local", "rank", "world", "stream"))
     w, h, k = CONFIGS[cfg]
@@ -392,7 +401,8 @@ def frame_leg(ctx, cfg, steps, verify):
     last = {}
 
     def one():
-        last["ct"], _ = pkg.quant_device(t_in, t_out, k, max_iters=10, device=local, stream=stream)
+        last["ct"], _ = pkg.quant_device(t_in, t_out, k, max_iters=10, device=local, stream=stream,
+                                         all_pixels_unique=uniq)
     for _ in range(3):
         one()
     dt = max_over_ranks(timed_region(one, steps, world, ctx["sync"]), world, dev)
@@ -550,6 +560,19 @@ def main():
                         "workload": "one 1920x1080 frame per call (C2), K=256, %d rank(s) (replicas)" % world,
                         "verified": ok2}
 
+    # --- the weighted path (allPixelsUnique=0: every live app call site,
+    # ClusteringSegmentation.cpp:1803) on one 4K frame per call
+    if big4k and not a.no_weighted:
+        sw_ = max(1, min(10, a.steps))
+        dtw, okw = frame_leg(ctx, "c3", sw_, verify, uniq=0)
+        detail["weighted_c3"] = {"ms_per_frame": round(dtw * 1e3 / sw_, 3),
+                                 "Mpix_per_s": round(n * world * sw_ / dtw / 1e6, 2), "steps": sw_,
+                                 "workload": "one 3840x2160 frame per call, K=256, quant_recurse(allPixelsUnique=0): "
+                                             "GPU calc_color_table (rocPRIM sorts) + exact ordered FP64 folds, %d "
+                                             "rank(s)" % world,
+                                 "verified": okw}
+        if okw is False:
+            fail("weighted-path output differs from the reference fixture", rank)
     # --- the same frames as OpenCV BGR24 Mats: read directly by
     # the root's passes, partition and map (3 B per pixel, no packing pass);
     # one frame per call (C3 shape) and the rank's batch in one call
@@ -652,6 +675,8 @@ def main():
             "config": {"workload": workload, "frames_per_rank_per_step": nf if a.mode == "frames" else None,
                        "frames_per_step": nf if a.mode == "rows" else None,
                        "engine_lanes": lanes if a.mode == "frames" else 1,
+                       "gpu_max_hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                       "gpu_max_hw_queues_set_by_bench": _HWQ_CALLER != os.environ["GPU_MAX_HW_QUEUES"],
                        "width": w, "height": h, "k": k, "max_iters": 10, "parallelism": parallelism},
             "verified": verified,
             "roofline": roof,

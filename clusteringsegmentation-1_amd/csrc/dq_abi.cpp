@@ -575,8 +575,10 @@ int dq_hip_loopback_rows_dev(int device, int nranks, int nframes, const uint32_t
     return -1;
   for (int i = 0; i < nframes; ++i)
     if (!d_in[i] || !d_out[i]) return -1;
+  // (rank engines are shared by every rank count: rank r of any group reuses
+  // the same engine -- kMaxShard per device at most, not one per (N, r))
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int>, Engine*> engines;
+  static std::map<std::pair<int, int>, Engine*> engines;
   static std::map<std::pair<int, int>, dq::Loopback*> groups;
   std::lock_guard<std::mutex> call(mu);
   DQ_HIP(hipSetDevice(device));
@@ -585,7 +587,7 @@ int dq_hip_loopback_rows_dev(int device, int nranks, int nframes, const uint32_t
   grp->reset_log();
   std::vector<Engine*> es(nranks);
   for (int r = 0; r < nranks; ++r) {
-    Engine*& e = engines[std::make_tuple(device, nranks, r)];
+    Engine*& e = engines[std::make_pair(device, r)];
     if (!e) e = new Engine(device);
     es[r] = e;
   }

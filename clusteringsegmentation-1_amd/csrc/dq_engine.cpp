@@ -104,6 +104,12 @@ Engine::Engine(int device) : device_(device) {
   const char* tr = getenv("DQ_HIP_TRACE");
   trace_ = tr && (tr[0] == '1' || tr[0] == '2');
   trace_rounds_ = tr && tr[0] == '2';
+  // switches of earlier rounds, now DQ_HIP_TUNE keys: refuse them rather than
+  // silently measuring the default
+  for (const char* old : {"DQ_HIP_FULL_ITERS", "DQ_HIP_PLAN", "DQ_HIP_KLOOP_MAX", "DQ_HIP_FUSE_PLAN"})
+    if (getenv(old))
+      die("environment", __FILE__, __LINE__,
+          (std::string(old) + " was removed: use DQ_HIP_TUNE (full_iters=, plan=, kloop_max=, fuse_plan=)").c_str());
   if (const char* t = getenv("DQ_HIP_TUNE")) apply_tune(t);
   DQ_HIP(hipSetDevice(device_));
   DQ_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));

@@ -36,7 +36,8 @@
 // The result is the sequential fold's double, bit for bit.
 // MUST be compiled with -ffp-contract=off (the Makefile does).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "dq_weighted.h"
 
@@ -773,13 +774,20 @@ static inline uint32_t grid_for(uint32_t n) {
   return g == 0 ? 1u : (g > 65535u ? 65535u : g);
 }
 
+// rocPRIM's device-wide radix sort (stable, LSD) and exclusive scan: the
+// temporary storage each needs for n items.
+static void temp_sizes(uint32_t n, size_t* sort1, size_t* sort2, size_t* scan) {
+  (void)rocprim::radix_sort_pairs(nullptr, *sort1, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 24);
+  (void)rocprim::radix_sort_pairs(nullptr, *sort2, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 48);
+  (void)rocprim::exclusive_scan(nullptr, *scan, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
+                                rocprim::plus<uint32_t>());
+}
+
 size_t color_table_scratch_bytes(uint32_t n) {
   size_t sort1 = 0, sort2 = 0, scan = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort1, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 24);
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort2, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 48);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  temp_sizes(n, &sort1, &sort2, &scan);
   const size_t tmp = std::max(sort1, std::max(sort2, scan));
   // key, idx, skey, sidx, flag, pos, ucol_tmp, head, oval, sval (u32) + okey, sokey (u64)
   return ((tmp + 255) & ~(size_t)255) + (size_t)n * (10 * 4 + 2 * 8) + 16 * 256;
@@ -788,11 +796,7 @@ size_t color_table_scratch_bytes(uint32_t n) {
 int launch_color_table(const uint32_t* px, uint32_t n, double norm, void* scratch, size_t scratch_bytes,
                        uint32_t* ucol, double* uw, uint32_t* h_nu, hipStream_t stream) {
   size_t sort1 = 0, sort2 = 0, scan = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort1, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 24);
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort2, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0, 48);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  temp_sizes(n, &sort1, &sort2, &scan);
   size_t tmp = std::max(sort1, std::max(sort2, scan));
   tmp = (tmp + 255) & ~(size_t)255;
   if (scratch_bytes < color_table_scratch_bytes(n)) return -1;
@@ -807,11 +811,12 @@ int launch_color_table(const uint32_t* px, uint32_t n, double norm, void* scratc
   const dim3 g(grid_for(n)), b(256);
   ct_keys_kernel<<<g, b, 0, stream>>>(px, n, key, idx);
   size_t t1 = sort1;
-  if (hipcub::DeviceRadixSort::SortPairs(temp, t1, key, skey, idx, sidx, (int)n, 0, 24, stream) != hipSuccess)
+  if (rocprim::radix_sort_pairs(temp, t1, key, skey, idx, sidx, (size_t)n, 0, 24, stream) != hipSuccess)
     return -2;
   ct_heads_kernel<<<g, b, 0, stream>>>(skey, n, flag);
   size_t t3 = scan;
-  if (hipcub::DeviceScan::ExclusiveSum(temp, t3, flag, pos, (int)n, stream) != hipSuccess) return -2;
+  if (rocprim::exclusive_scan(temp, t3, flag, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), stream) != hipSuccess)
+    return -2;
   // U = pos[n-1] + flag[n-1]
   uint32_t last[2];
   if (hipMemcpyAsync(&last[0], pos + n - 1, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
@@ -821,7 +826,7 @@ int launch_color_table(const uint32_t* px, uint32_t n, double norm, void* scratc
   const uint32_t nu = last[0] + last[1];
   ct_scatter_kernel<<<g, b, 0, stream>>>(skey, sidx, flag, pos, n, ucol_tmp, head, okey, oval);
   size_t t2 = sort2;
-  if (hipcub::DeviceRadixSort::SortPairs(temp, t2, okey, sokey, oval, sval, (int)nu, 0, 48, stream) != hipSuccess)
+  if (rocprim::radix_sort_pairs(temp, t2, okey, sokey, oval, sval, (size_t)nu, 0, 48, stream) != hipSuccess)
     return -2;
   ct_final_kernel<<<dim3(grid_for(nu)), b, 0, stream>>>(sval, ucol_tmp, head, nu, n, norm, ucol, uw);
   *h_nu = nu;

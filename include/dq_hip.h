@@ -211,13 +211,13 @@ uint64_t dq_hip_last_points_full(int device);
 /* Weighted path: tiles of the last run whose folds ran one summand at a time
  * (the exact parallel fold's fallback). */
 uint64_t dq_hip_last_seq_tiles(int device);
-/* Fixed-point finalisation (default on; DQ_HIP_FULL_ITERS=1 turns the default
- * off).  A split whose 2-means pass reproduces the previous pass's exact
+/* Fixed-point finalisation (default on; DQ_HIP_TUNE=full_iters=1 turns the
+ * default off).  A split whose 2-means pass reproduces the previous pass's exact
  * integer sums is final: the remaining iterations of the reference's loop
  * (DivQuantCluster.cpp:613) would recompute the same means and decision.
  * Outputs are identical either way; only the swept points differ. */
 void dq_hip_set_fixed_point(int device, int on);
-/* Device-planned rounds (default on; DQ_HIP_PLAN=0 turns the default off):
+/* Device-planned rounds (default on; DQ_HIP_TUNE=plan=0 turns the default off):
  * while a frame may still need splits, the next round's tables are built on
  * the GPU from the current round's results and the round is enqueued before
  * the host has seen them.  Outputs are identical either way;
@@ -226,7 +226,7 @@ void dq_hip_set_fixed_point(int device, int on);
 void dq_hip_set_planned_rounds(int device, int on);
 int dq_hip_last_planned_rounds(int device);
 /* One-launch 2-means loops: a round whose records all hold at
- * most max_points points (default 49152; DQ_HIP_KLOOP_MAX) and that has at
+ * most max_points points (default 49152; DQ_HIP_TUNE=kloop_max=N) and that has at
  * most one record per CU runs all its 2-means iterations in one
  * kloop_kernel launch, one workgroup per record.  0 turns it off.  Outputs
  * are identical either way.  dq_hip_last_loop_rounds: how many rounds of the
@@ -235,7 +235,10 @@ void dq_hip_set_loop_max(int device, uint32_t max_points);
 int dq_hip_last_loop_rounds(int device);
 
 /* Engine lanes a batch of frames is split over (each: own stream, own host
- * thread; DQ_HIP_LANES, default 3).  lanes = 0 restores the default. */
+ * thread; DQ_HIP_LANES; default 4 when GPU_MAX_HW_QUEUES >= 6 at the first
+ * batch call, else 3 -- HIP reads GPU_MAX_HW_QUEUES once, when it
+ * initialises, so set it before any HIP call of the process).  lanes = 0
+ * restores the default. */
 void dq_hip_set_lanes(int lanes);
 int dq_hip_get_lanes(void);
 
