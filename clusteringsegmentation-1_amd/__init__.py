@@ -89,6 +89,8 @@ def lib():
         "dq_hip_last_planned_rounds": ([c.c_int], c.c_int),
         "dq_hip_set_loop_max": ([c.c_int, c.c_uint32], None),
         "dq_hip_last_loop_rounds": ([c.c_int], c.c_int),
+        "dq_hip_set_persist": ([c.c_int, c.c_int], None),
+        "dq_hip_last_persist_rounds": ([c.c_int], c.c_int),
         "dq_hip_set_timing": ([c.c_int, c.c_int], None),
         "dq_hip_reset_stats": ([c.c_int], None),
         "dq_hip_get_stat": ([c.c_int, c.c_int, c.POINTER(c.c_uint64), c.POINTER(c.c_double),
@@ -580,6 +582,15 @@ def set_loop_max(max_points, device=0):
 
 def last_loop_rounds(device=0):
     return lib().dq_hip_last_loop_rounds(device)
+
+
+def set_persist(on, device=0):
+    """kpersist_kernel rounds on / off (every lane of the device)."""
+    lib().dq_hip_set_persist(device, 1 if on else 0)
+
+
+def last_persist_rounds(device=0):
+    return lib().dq_hip_last_persist_rounds(device)
 
 
 def set_lanes(lanes):

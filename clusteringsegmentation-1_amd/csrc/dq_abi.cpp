@@ -883,6 +883,12 @@ void dq_hip_set_loop_max(int device, uint32_t max_points) {
 
 int dq_hip_last_loop_rounds(int device) { return engine_for(device).last_loop_rounds; }
 
+void dq_hip_set_persist(int device, int on) {
+  for (int l = 0; l < dq::kMaxLanes; ++l) engine_for(device, l).set_persist(on != 0);
+}
+
+int dq_hip_last_persist_rounds(int device) { return engine_for(device).last_persist_rounds; }
+
 void dq_hip_set_timing(int device, int on) { engine_for(device).set_timing(on != 0); }
 
 void dq_hip_set_debug(int device, int flags) {

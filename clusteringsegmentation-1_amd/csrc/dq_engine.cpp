@@ -95,6 +95,7 @@ void Engine::apply_tune(const char* spec) {
     else if (k == "eager_replan") eager_replan_ = v != 0;
     else if (k == "stats_only") stats_only_ = v != 0;
     else if (k == "fuse_plan") fuse_plan_ = v != 0;
+    else if (k == "persist") persist_ = v != 0;                         // kpersist_kernel rounds
     else if (k == "kloop_max") kloop_max_ = (uint32_t)std::max<long>(0, std::min<long>(kLoopMaxLen, v));
     else die("DQ_HIP_TUNE", __FILE__, __LINE__, ("unknown key " + k).c_str());
   }
@@ -1069,10 +1070,26 @@ bool Engine::loop_ok(const Round& R) const {
   return true;
 }
 
-void Engine::kmeans_loop(Round& R, int max_iters, hipStream_t stream) {
-  ++last_loop_rounds;
+// Rounds kloop does not take (records above kloop_max_ points) whose tiles
+// all fit the device's resident workgroups: every 2-means iteration in one
+// kpersist_kernel launch (its records' workgroups must be co-resident: at
+// most kPersistWgsPerCu pass workgroups per CU -- the kernel's occupancy is
+// at least that -- whatever else runs).
+bool Engine::persist_ok(const Round& R) const {
+  if (!persist_ || nshard_ != 1 || cross_process() || R.root || R.ntiles > (size_t)kPersistWgsPerCu * num_cus_)
+    return false;
+  for (int a = 0; a < R.nl; ++a)
+    if (nodes_[R.order[a]].buf == BUF_IN) return false;   // (a root's packed / BGR24 frame)
+  return true;
+}
+
+void Engine::kmeans_loop(Round& R, int max_iters, hipStream_t stream, int kind) {
+  if (kind == 2) ++last_persist_rounds;
+  else ++last_loop_rounds;
   timed_begin(stream);
-  launch_kloop(R.ra, R.nr, max_iters, stream);
+  if (kind == 2) launch_kpersist(R.ra, (int)R.ntiles, max_iters, stream);
+  else launch_kloop(R.ra, R.nr, max_iters, stream);
+  tmark(kind == 2 ? "kpersist" : "kloop");
   timed_end(ST_KLOOP, 0.0, stream);
   if (timing_) R.loop_event = (long)pending_.size() - 1;
 }
@@ -1092,14 +1109,15 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   bool all_proven = false;
   // Late rounds (small records): every 2-means iteration in one launch,
   // waited for on the status word of iteration max_iters - 1
-  const bool loop = fixed_point_ && loop_ok(R);
+  // (kpersist_kernel, the same contract, for rounds of larger records)
+  const int loop = !fixed_point_ ? 0 : loop_ok(R) ? 1 : persist_ok(R) ? 2 : 0;
   // Nothing else queued behind this round (a frame's last rounds): its first
   // 2-means iterations go in before its split status is known -- a record
   // final at the split makes them exit at once (~4 us each); C3's last round
   // needs them and otherwise waited ~15 us for the host to see the status.
   if (speculate && fixed_point_) {
     if (loop) {
-      kmeans_loop(R, max_iters, stream);
+      kmeans_loop(R, max_iters, stream, loop);
       launched = max_iters;
     } else {
       for (; launched < max_iters && launched <= lookahead_; ++launched) kmeans_iter(R, launched, max_iters, stream);
@@ -1126,7 +1144,7 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   int replan = -1;
   if (!all_proven && successor >= 0 && eager_replan_) {
     if (loop && launched == 0) {
-      kmeans_loop(R, max_iters, stream);
+      kmeans_loop(R, max_iters, stream, loop);
       launched = max_iters;
     }
     for (; launched < max_iters; ++launched) kmeans_iter(R, launched, max_iters, stream);
@@ -1136,10 +1154,10 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   }
   if (!all_proven && loop) {
     if (launched == 0) {
-      kmeans_loop(R, max_iters, stream);
+      kmeans_loop(R, max_iters, stream, loop);
       launched = max_iters;
     }
-    DQ_CHECK(wait_status(stat + (max_iters - 1), R.seq, stream) == 0, "kloop_kernel left a record active");
+    DQ_CHECK(wait_status(stat + (max_iters - 1), R.seq, stream) == 0, "kloop / kpersist left a record active");
     all_proven = true;   // (every record final: the loop below has nothing to wait for)
   }
   while (!all_proven) {
@@ -1520,6 +1538,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   tmark("run");
   last_planned = last_aborted = 0;
   last_loop_rounds = 0;
+  last_persist_rounds = 0;
   {   // this run's capacities (nothing in flight now)
     size_t rec_cap = 64, px = 0;
     for (int i = 0; i < nframes; ++i) {

@@ -221,6 +221,7 @@ class Engine {
   int last_planned = 0;               // rounds planned on the device (of last_rounds)
   int last_aborted = 0;               // planned rounds whose plan found a parent unfinished
   int last_loop_rounds = 0;           // rounds whose 2-means iterations ran in one kloop_kernel launch
+  int last_persist_rounds = 0;        // ... in one kpersist_kernel launch
   uint64_t last_points_swept = 0;     // sum over passes of points read (all frames)
   uint64_t last_points_full = 0;      // the same without fixed-point finalisation
   uint64_t last_seq_tiles = 0;        // weighted: tiles folded one summand at a time
@@ -244,6 +245,7 @@ class Engine {
   void set_plan(bool on) { plan_ = on; }
   // kloop_kernel eligibility: records of at most n points (0: never)
   void set_loop_max(uint32_t n) { kloop_max_ = std::min<uint32_t>(n, kLoopMaxLen); }
+  void set_persist(bool on) { persist_ = on; }
   bool plan() const { return plan_; }
   bool fixed_point() const { return fixed_point_; }
   void reset_stats();
@@ -319,7 +321,9 @@ class Engine {
   // All 2-means iterations of round R in one launch (kloop_kernel): every
   // record one shard, planar, at most kloop_max_ points and kLoopMaxTiles tiles.
   bool loop_ok(const Round& R) const;
-  void kmeans_loop(Round& R, int max_iters, hipStream_t stream);
+  bool persist_ok(const Round& R) const;
+  // kind 1: kloop_kernel, 2: kpersist_kernel
+  void kmeans_loop(Round& R, int max_iters, hipStream_t stream, int kind);
   void apply_tune(const char* spec);
   int src_fmt(const std::vector<int>& ids) const;
   void check_arena_zero(hipStream_t stream);
@@ -411,6 +415,8 @@ class Engine {
   void sync_stream(hipStream_t stream);
   bool speculate_kmeans_ = true;      // a round with nothing queued behind it starts its
                                       //   2-means iterations before its split status (DQ_HIP_TUNE spec_kmeans)
+  bool persist_ = true;                // kpersist_kernel for eligible rounds (DQ_HIP_TUNE persist)
+  static constexpr int kPersistWgsPerCu = 4;
   uint32_t kloop_max_ = 49152;        // a record's points at most for kloop_kernel (DQ_HIP_TUNE kloop_max; 0: off)
   int tiles_target_ = 512;            // tiles per big round (DQ_HIP_TUNE tiles; 512 vs 1024: C3 -4 %)
   int node_tiles_ = 8;                // tiles per node at least (DQ_HIP_TUNE node_tiles)

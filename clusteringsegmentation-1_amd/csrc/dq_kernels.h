@@ -193,6 +193,12 @@ constexpr uint32_t kLoopMaxTiles = 1024;
 // 2^32 keeps its u32 sums of squares exact.
 constexpr uint32_t kLoopMaxLen = 61440u * 16u - 32u;
 void launch_kloop(const RoundArgs& a, int nrec, int max_iters, hipStream_t stream);
+// All 2-means iterations of the round in one launch over its ntiles tiles,
+// one workgroup per tile, the records' workgroups meeting per iteration on
+// rdone (kpersist_kernel): one shard per record (TOT_OWN), planar records,
+// ntiles at most the resident workgroups of the device (Engine::persist_ok).
+// Every record arrives on the counter of iteration max_iters - 1.
+void launch_kpersist(const RoundArgs& a, int ntiles, int max_iters, hipStream_t stream);
 // Fused partition + split pass over the round's PartTiles: writes each
 // parent's points into its two children's segments (old half first, then new
 // half) of the child buffer, using the parent's final 2-means decision, and

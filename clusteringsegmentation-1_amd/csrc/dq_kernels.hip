@@ -926,8 +926,12 @@ __global__ __launch_bounds__(kEpiBlock) void epilogue_kernel(RoundArgs a) {
 // TOT_ALLREDUCE the wave only writes the node's totals of this process to
 // a.tot; the allreduce and epilogue_kernel<KIND, TOT_ALLREDUCE> follow.
 // Partials and per-wave counts: see the hand-off comment in kpass_kernel.
+// it_arr: the launch counter / status slot the records arrive on; final_only:
+// arrive only once final (kpersist_kernel: every record arrives once, on the
+// counter of iteration max_iters - 1).
 template <int KIND>
-__device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int node, NodeResult* sres) {
+__device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int node, NodeResult* sres, int it_arr,
+                                                     bool final_only) {
   const int S = a.nshard, r0 = node * S;
   const uint32_t lane = lane_id();
   const uint32_t* pp = reinterpret_cast<const uint32_t*>(a.parts);
@@ -982,8 +986,8 @@ __device__ __forceinline__ void kmeans_epilogue_wave(const RoundArgs& a, int nod
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane < (uint32_t)S)
-    arrive(a.ctr + a.it, (uint32_t)(r0 + lane), (uint32_t)a.nn, !final_results, a.hstat + a.it, a.seq);
+  if (lane < (uint32_t)S && (final_results || !final_only))
+    arrive(a.ctr + it_arr, (uint32_t)(r0 + lane), (uint32_t)a.nn, !final_results, a.hstat + it_arr, a.seq);
 }
 
 template <int KIND>
@@ -1064,7 +1068,111 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) 
     slast = last;
   }
   __syncthreads();
-  if (slast && wave_id() == 0) kmeans_epilogue_wave<KIND>(a, node, sres);
+  if (slast && wave_id() == 0) kmeans_epilogue_wave<KIND>(a, node, sres, a.it, false);
+}
+
+// ---------------------------------------------------------------------------
+// Every 2-means iteration of a round in ONE launch over the round's tiles
+// (one workgroup per tile, as kpass_kernel): a record's
+// workgroups loop over the iterations themselves.  Per iteration each sweeps
+// its tile with the record's current decision and hands its partial to the
+// record's last arriver exactly as kpass_kernel does (write-through stores,
+// drained, agent-scope release add on rdone[it][record]); the last arriver
+// runs the same epilogue wave (node_update on the same exact integer sums:
+// every decision, fixed point and result is kpass's), then publishes the
+// next iteration by a second release add on the same word (ntiles + 1); the
+// others wait for that value with agent-scope loads and acquire before they
+// read the record again.  A record arrives on the counter of iteration
+// max_iters - 1 once, when final (kloop_kernel's status contract), so the
+// host waits for one status word instead of polling every iteration.
+// Waits only on the record's own workgroups, which all arrive before they
+// wait: no cycle.  Eligible rounds (Engine::persist_ok) have at most as many
+// tiles as the GPU holds resident workgroups, so a record's workgroups are
+// co-resident even if none of its round exits; every wait is bounded (a
+// record's workgroups give up after ~2^26 polls and leave its status unset:
+// the host's wait then reports the stream drained without it).
+constexpr uint32_t kPersistSpin = 1u << 26;
+__global__ __launch_bounds__(kBlock, kPassWaves) void kpersist_kernel(RoundArgs a, int32_t max_iters) {
+  const Tile t = a.tiles[blockIdx.x];
+  const int rec = t.node;   // (one shard per record: S == 1, TOT_OWN)
+  const DevNode& nd = a.nodes[rec];
+  const int ntiles = nd.tile_end - nd.tile_begin;
+  __shared__ uint32_t red[kBlock / 64][8];
+  __shared__ int slast, sgo;
+  __shared__ NodeResult sres[1];
+  if (nd.done_it != 0) {   // final at its split: its first tile arrives for it
+    if ((int)blockIdx.x == nd.tile_begin && threadIdx.x == 0)
+      arrive(a.ctr + (max_iters - 1), (uint32_t)rec, (uint32_t)a.nn, false, a.hstat + (max_iters - 1), a.seq);
+    return;
+  }
+  for (int it = 0; it < max_iters; ++it) {
+    const Params q = nd.prm;   // (this iteration's decision: read after the acquire below)
+    LaneSums s;
+    uint32_t ws, we;
+    wave_range(t.start, t.end, wave_id(), ws, we);
+    wave_pass<PASS_KMEANS, true>(nd.src, a.plane, ws, we, q, s);
+    uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
+#pragma unroll
+    for (int k = 0; k < F_NUM; ++k) f[k] = wave_sum_u32(f[k]);
+    const uint32_t vsum = wave_sum_u32(s.vcnt);
+    if (lane_id() == 0) {
+      __hip_atomic_store(a.wparts + blockIdx.x * kTileWaves + wave_id(),
+                         (vsum - f[F_CNT]) | (f[F_CNT] << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[wave_id()][k] = k < F_NUM ? f[k] : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) x += red[w][threadIdx.x];
+      __hip_atomic_store(a.parts[blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x + 131u * (uint32_t)it)) debug_sleep_us(10);
+    if (a.debug & kDebugPrewarm) {   // (tests) the record's lines into this CU's caches before the wait
+      const uint32_t x = __builtin_nontemporal_load(&nd.done_it) + (uint32_t)nd.prm.thr + nd.iter;
+      asm volatile("s_waitcnt vmcnt(0)" ::"v"(x) : "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (kpass_kernel's hand-off)
+    __syncthreads();
+    uint32_t* word = a.rdone + (size_t)it * a.nn + rec;
+    if (threadIdx.x == 0) {
+      const bool last = __hip_atomic_fetch_add(word, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) ==
+                        (uint32_t)ntiles - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      slast = last;
+    }
+    __syncthreads();
+    const bool klast = it == max_iters - 1;
+    if (slast && wave_id() == 0) {
+      if (klast) kmeans_epilogue_wave<PASS_KLAST>(a, rec, sres, max_iters - 1, true);
+      else kmeans_epilogue_wave<PASS_KMEANS>(a, rec, sres, max_iters - 1, true);
+      // the record (decision, state, done_it) and its results are stored:
+      // publish iteration it to the record's other workgroups
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane_id() == 0) __hip_atomic_fetch_add(word, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (klast) return;   // (PASS_KLAST finalises every record)
+    if (threadIdx.x == 0) {   // (the last arriver's own add is already in: no wait)
+      int go = 1;
+      for (uint32_t spin = 0;
+           __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)ntiles + 1u; ++spin) {
+        if (spin == kPersistSpin) {   // (never in a correct run: the record's status stays unset)
+          go = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      sgo = go && nd.done_it == 0;
+    }
+    __syncthreads();
+    if (!sgo) return;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3066,6 +3174,11 @@ void launch_kpass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) 
   const dim3 g(ntiles), b(kBlock);
   if (kind == PASS_KLAST) kpass_kernel<PASS_KLAST><<<g, b, 0, stream>>>(a);
   else kpass_kernel<PASS_KMEANS><<<g, b, 0, stream>>>(a);
+}
+
+void launch_kpersist(const RoundArgs& a, int ntiles, int max_iters, hipStream_t stream) {
+  if (ntiles <= 0) return;
+  kpersist_kernel<<<dim3(ntiles), dim3(kBlock), 0, stream>>>(a, max_iters);
 }
 
 void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream) {

@@ -1,9 +1,11 @@
 """GPU: the cross-workgroup and host hand-offs under forced interleavings.
 
-The engine's only in-kernel hand-off between workgroups is the fused 2-means
+The engine's in-kernel hand-offs between workgroups are the fused 2-means
 pass (kpass_kernel): every workgroup of a record publishes its tile partial
 and per-wave counts, and the record's last arriver reads them all
-(DESIGN.md 3b).  The host hand-offs are the round results and status words in
+(DESIGN.md 3b); and kpersist_kernel, which does the same once per iteration
+and then publishes the record's next decision to the record's other
+workgroups.  The host hand-offs are the round results and status words in
 host-coherent memory, reused by round parity.  Each test forces the state the
 protocol must tolerate (dq_hip_set_debug flags, dq_kernels.h kDebug*) and
 checks every output against the reference build's fixtures:
@@ -64,20 +66,28 @@ def test_handoffs_forced_interleavings_three_lanes(gpu):
     _c4_share(gpu, ALL, lanes=3)
 
 
-def test_c3_forced_interleavings(gpu):
+@pytest.mark.parametrize("persist", [True, False])
+def test_c3_forced_interleavings(gpu, persist):
     """C3 (one 4K frame per call): its last round's 2-means iterations start
     before the split status (speculation) -- the chain the host delay and the
-    plan stall shift the most."""
+    plan stall shift the most.  persist: they run as one kpersist_kernel
+    launch, whose records' workgroups meet per iteration on device counters
+    (prewarm: every workgroup loads its record's lines before it waits, so a
+    wait without the agent-scope acquire would re-read a stale decision;
+    uneven: 1 in 8 workgroups arrive ~10 us late per iteration)."""
     import torch
     fix = fx.load_json("c4.json")["f00"]
     t_in = torch.from_numpy(fx.xorshift(W4 * H4).view(np.int32)).to("cuda:0")
     t_out = torch.empty_like(t_in)
+    gpu.set_persist(persist)
     gpu.set_debug(ALL)
     try:
         for c in range(3):
             ct, _ = gpu.quant_device(t_in, t_out, 256)
             torch.cuda.synchronize()
+            assert (gpu.last_persist_rounds() > 0) == persist
             assert [int(v) for v in ct] == fix["ct"], c
             assert "%016x" % fx.fnv(t_out.cpu().numpy().view(np.uint32)) == fix["out_fnv"], c
     finally:
         gpu.set_debug(0)
+        gpu.set_persist(True)

@@ -355,10 +355,12 @@ def test_one_launch_kmeans_loops(gpu, key):
     bat = fx.load_png_u32(fx.os.path.join(fx.GOLDEN, "png", "batman.png"))[0]
     fix = fx.load_json("png.json")["batman"]
     try:
+        gpu.set_persist(False)
         for lmax in (49152, 0):
             gpu.set_loop_max(lmax)
             out, ct = _quant_dev(gpu, px, c["k"])
             assert (gpu.last_loop_rounds() > 0) == (lmax > 0)
+            assert gpu.last_persist_rounds() == 0
             assert [int(v) for v in ct] == c["ct"]
             assert "%016x" % fx.fnv(out) == c["out_fnv"]
             assert np.array_equal(gpu.last_trace(c["k"]), arrs["trace_" + key])
@@ -369,6 +371,38 @@ def test_one_launch_kmeans_loops(gpu, key):
                 assert "%016x" % fx.fnv(out) == fix["k%d" % k]["out_fnv"], (lmax, k)
     finally:
         gpu.set_loop_max(49152)
+        gpu.set_persist(True)
+
+
+@pytest.mark.parametrize("key", ["3840x2160_k256", "1920x1080_k256", "4096x4096_k1024"])
+def test_persistent_kmeans_rounds(gpu, key):
+    """Rounds of larger records run every 2-means iteration in one
+    kpersist_kernel launch: the records' workgroups meet per
+    iteration on device counters, and the last arriver runs the same FP64
+    update on the same exact sums as kpass_kernel.  With and without it (and
+    with kloop off, so kpersist takes kloop's rounds too): the reference's
+    colortable, output, split trace and centroid doubles; C3's frame must
+    take it."""
+    big = fx.load_json("big.json")
+    if key not in big:
+        pytest.skip("fixture not generated")
+    c = big[key]
+    arrs = fx.load_npz("big.npz")
+    px = fx.xorshift(c["w"] * c["h"])
+    try:
+        for persist, lmax in ((True, 49152), (True, 0), (False, 49152)):
+            gpu.set_persist(persist)
+            gpu.set_loop_max(lmax)
+            out, ct = _quant_dev(gpu, px, c["k"])
+            if key == "3840x2160_k256" or not persist:
+                assert (gpu.last_persist_rounds() > 0) == persist, (persist, lmax)
+            assert [int(v) for v in ct] == c["ct"], (persist, lmax)
+            assert "%016x" % fx.fnv(out) == c["out_fnv"], (persist, lmax)
+            assert np.array_equal(gpu.last_trace(c["k"]), arrs["trace_" + key])
+            _check_centroids(gpu, c["k"], arrs["means_" + key])
+    finally:
+        gpu.set_loop_max(49152)
+        gpu.set_persist(True)
 
 
 def test_kmeans_loop_at_max_len_near_white(gpu):
