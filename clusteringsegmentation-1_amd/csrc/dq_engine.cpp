@@ -1708,15 +1708,8 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     DQ_HIP(hipMalloc(&d_wscratch_, need_scratch));
     cap_wscratch_ = need_scratch;
   }
-  if (n > cap_w_) {
-    DQ_HIP(hipStreamSynchronize(stream));
-    if (d_wcol_) DQ_HIP(hipFree(d_wcol_));
-    if (d_ww_) DQ_HIP(hipFree(d_ww_));
-    DQ_HIP(hipMalloc((void**)&d_wcol_, (size_t)n * 4));
-    DQ_HIP(hipMalloc((void**)&d_ww_, (size_t)n * 8));
-    cap_w_ = n;
-  }
-  ensure_pixels((size_t)n + 4);
+  // P0 / P1 hold the points' 8-B records (colour | count << 32): 2 words each
+  ensure_pixels(2 * (size_t)n + 8);
   // norm_factor = 1 / (ceil(numRows / dec) * ceil(numCols / dec)) (:184)
   const double norm = 1.0 / (std::ceil((double)rows / (double)job.dec) * std::ceil((double)cols / (double)job.dec));
   const uint32_t* pts = job.d_in;
@@ -1727,9 +1720,11 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     pts = d_p1_;
   }
   uint32_t nu = 0;
-  const int rc = launch_color_table(pts, n, norm, d_wscratch_, cap_wscratch_, d_wcol_, d_ww_, &nu, stream);
+  // (the root's points, in calc_color_table's order, straight into P0: the
+  // colour table has read P1's decimated points by then)
+  const int rc = launch_color_table(pts, n, d_wscratch_, cap_wscratch_, reinterpret_cast<uint64_t*>(d_p0_), &nu,
+                                    stream);
   DQ_CHECK(rc == 0, "colour table failed");
-  launch_iota(d_p0_, nu, stream);
 
   frames_.assign(1, FrameState());
   nodes_.clear();
@@ -1802,8 +1797,8 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
       const Seg& sg = seg(active[a], 0);
       WState& w = hw[a];
       std::memset(&w, 0, sizeof w);
-      w.src = nd.buf == BUF_P0 ? d_p0_ : d_p1_;
-      w.dst = nd.buf == BUF_P0 ? d_p1_ : d_p0_;
+      w.src = reinterpret_cast<const uint64_t*>(nd.buf == BUF_P0 ? d_p0_ : d_p1_);
+      w.dst = reinterpret_cast<uint64_t*>(nd.buf == BUF_P0 ? d_p1_ : d_p0_);
       w.off = sg.off;
       w.len = sg.len;
       w.tile_begin = t;
@@ -1836,8 +1831,7 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     WArgs wa;
     wa.nodes = reinterpret_cast<WState*>(db);
     wa.tiles = reinterpret_cast<const WTile*>(db + o_tiles);
-    wa.ucol = d_wcol_;
-    wa.uw = d_ww_;
+    wa.norm = norm;
     wa.tsum = reinterpret_cast<double*>(db + o_tsum);
     wa.tpre = reinterpret_cast<double*>(db + o_tpre);
     wa.fold = reinterpret_cast<WFold*>(db + o_fold);

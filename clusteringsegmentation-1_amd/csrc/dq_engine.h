@@ -449,9 +449,6 @@ class Engine {
   size_t cap_mapstage_ = 0;
   void ensure_map_stage(size_t nmaps);
   // weighted path buffers
-  uint32_t* d_wcol_ = nullptr;        // unique colours
-  double* d_ww_ = nullptr;            // their weights
-  size_t cap_w_ = 0;
   void* d_wscratch_ = nullptr;        // colour-table scratch (sorts)
   size_t cap_wscratch_ = 0;
   void* d_wnodes_ = nullptr;          // a round's WState records, tiles, fold tables, results

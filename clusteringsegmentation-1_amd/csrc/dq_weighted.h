@@ -10,12 +10,13 @@ namespace dq {
 
 // calc_color_table (DivQuantMapColors.cpp:82-203) on the device: the unique
 // colours of px[0..n) in the reference's output order (hash bucket ascending,
-// first occurrence descending inside a bucket) into ucol, weights norm*count
-// into uw (n entries of room each); *h_nu = the number of colours.  Waits for
-// the stream once (the colour count).  Returns 0, or < 0 (-1: scratch too small).
+// first occurrence descending inside a bucket) as point records colour |
+// count << 32 into rec (n entries of room; the weight of a point is norm *
+// count, :195); *h_nu = the number of colours.  Waits for the stream once
+// (the colour count).  Returns 0, or < 0 (-1: scratch too small).
 size_t color_table_scratch_bytes(uint32_t n);
-int launch_color_table(const uint32_t* px, uint32_t n, double norm, void* scratch, size_t scratch_bytes,
-                       uint32_t* ucol, double* uw, uint32_t* h_nu, hipStream_t stream);
+int launch_color_table(const uint32_t* px, uint32_t n, void* scratch, size_t scratch_bytes, uint64_t* rec,
+                       uint32_t* h_nu, hipStream_t stream);
 
 // ---------------------------------------------------------------------------
 // DivQuantCluster<false,*,true> (DivQuantCluster.cpp:133-1097) over a round of
@@ -33,8 +34,8 @@ enum WPass : int32_t { WP_INIT = 0, WP_SPLIT = 1, WP_KM = 2 };
 // One node of a weighted round: its record and the state carried across the
 // round's passes (written by the chain kernel).
 struct alignas(16) WState {
-  const uint32_t* src;        // point ids (into ucol / uw) at src[off .. off+len), point order
-  uint32_t* dst;              // the children's ids: old half at dst[off ..), then the new half
+  const uint64_t* src;        // point records (colour | count << 32) at src[off .. off+len), point order
+  uint64_t* dst;              // the children's records: old half at dst[off ..), then the new half
   uint32_t off, len;
   int32_t tile_begin, tile_end;
   int32_t root;               // 1: the init folds first (DivQuantClusterInitMeanAndVar, :36-123)
@@ -88,8 +89,7 @@ struct alignas(16) WQuick {
 struct WArgs {
   WState* nodes;
   const WTile* tiles;
-  const uint32_t* ucol;
-  const double* uw;
+  double norm;                // calc_color_table's norm_factor (a point's weight: norm * count)
   double* tsum;               // [tile][8] the tile's sums (any order: an estimate)
   double* tpre;               // [tile][8] exclusive node prefix of tsum
   WFold* fold;                // [tile][kWCh]
@@ -109,7 +109,5 @@ void launch_wfinish(const WArgs& a, hipStream_t stream);           // partition 
 // every index lies inside the input.
 void launch_cut_gather(const uint32_t* in, uint32_t* out, uint32_t nr, uint32_t nc, uint32_t dec,
                        uint32_t stride, uint32_t sr, uint32_t sg, uint32_t sb, hipStream_t stream);
-// dst[i] = i (the root's point ids)
-void launch_iota(uint32_t* dst, uint32_t n, hipStream_t stream);
 
 }  // namespace dq

@@ -78,14 +78,16 @@ __global__ void ct_scatter_kernel(const uint32_t* __restrict__ skey, const uint3
   }
 }
 
+// The points in calc_color_table's order as (colour | count << 32) records:
+// a pass reads a point's colour and its weight norm * count (:195) from its
+// own record, in node order (the partitions move records, not ids).
 __global__ void ct_final_kernel(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ ucol_tmp,
-                                const uint32_t* __restrict__ head, uint32_t nu, uint32_t n, double norm,
-                                uint32_t* __restrict__ ucol, double* __restrict__ uw) {
+                                const uint32_t* __restrict__ head, uint32_t nu, uint32_t n,
+                                uint64_t* __restrict__ rec) {
   for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < nu; j += gridDim.x * 256u) {
     const uint32_t u = sval[j];
     const uint32_t count = (u + 1 < nu ? head[u + 1] : n) - head[u];
-    ucol[j] = ucol_tmp[u];
-    uw[j] = norm * (int)count;   // weights[index] = norm_factor * bucket->value (:195)
+    rec[j] = (uint64_t)ucol_tmp[u] | ((uint64_t)count << 32);
   }
 }
 
@@ -117,6 +119,9 @@ __device__ __forceinline__ double w_prod(int ch, uint32_t R, uint32_t G, uint32_
   }
 }
 
+// weights[index] = norm_factor * bucket->value (:195), from a point's record
+__device__ __forceinline__ double w_weight(const WArgs& a, uint64_t rec) { return a.norm * (int)(uint32_t)(rec >> 32); }
+
 struct WPts {
   uint32_t R[kWPer], G[kWPer], B[kWPer];
   double w[kWPer];
@@ -132,9 +137,9 @@ __device__ __forceinline__ void w_load(const WArgs& a, const WState& st, const W
     q.R[k] = q.G[k] = q.B[k] = 0;
     q.w[k] = 0.0;
     if (p < t.end) {
-      const uint32_t id = st.src[p];
-      const uint32_t c = a.ucol[id];
-      q.w[k] = a.uw[id];
+      const uint64_t r = st.src[p];
+      const uint32_t c = (uint32_t)r;
+      q.w[k] = w_weight(a, r);
       q.R[k] = (c >> 16) & 0xFF;
       q.G[k] = (c >> 8) & 0xFF;
       q.B[k] = c & 0xFF;
@@ -236,6 +241,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
   __shared__ int s_wk[kW][3];              // per wave: first / last member key (-1: none), starts
   __shared__ unsigned long long s_m[kWSeg];
   __shared__ int s_e[kWSeg];
+  __shared__ long long s_fm[kW];
   for (int ch = 0; ch < kWCh; ++ch) {
     double x[kWPer];
     double T = 0.0;
@@ -243,6 +249,57 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
     for (int k = 0; k < kWPer; ++k) {
       x[k] = w_x(q, k, ch);
       T += x[k];
+    }
+    // One-binade tile (nearly every tile past a node's first few): with the
+    // tile's prefix estimate P0 and its sum estimate Tt, every summand's
+    // interval lies inside [P0 (1 - 2^-20), (P0 + Tt) (1 + 2^-20)] (the
+    // prefixes grow from P0, the summands are >= 0, and the estimates' errors
+    // are far inside the margin), so when that interval is in one binade e
+    // every nonzero summand is a run member of e: the description is one
+    // segment (e, sum of RNE(x / 2^(e-52))) -- no scans, no slots.  A tie
+    // anywhere in the tile (x / u exactly halfway) takes the general path.
+    {
+      const double P0 = a.tpre[(size_t)blockIdx.x * 8 + ch], Tt = a.tsum[(size_t)blockIdx.x * 8 + ch];
+      const double lo = P0 * (1.0 - kWMargin), hi = (P0 + Tt) * (1.0 + kWMargin);
+      const int el = lo > 0.0 ? w_binade(lo) : 0;
+      if (lo > 0.0 && el == w_binade(hi)) {   // (block-uniform: tile values)
+        long long mm = 0;
+        int tie = 0;
+#pragma unroll
+        for (int k = 0; k < kWPer; ++k) {
+          const double tt = ldexp(x[k], 52 - el);   // exact (x < 2^(el+1)); 0 for a non-summand
+          const double fl = floor(tt), fr = tt - fl;
+          tie |= fr == 0.5;
+          mm += (long long)fl + (fr > 0.5 ? 1 : 0);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) mm += __shfl_xor(mm, o, 64);
+        if (lane == 0) s_fm[wv] = mm;
+        if (!__syncthreads_or(tie)) {
+          long long M = 0;
+          for (int w = 0; w < kW; ++w) M += s_fm[w];
+          if (threadIdx.x == 0) {
+            WFold& f = a.fold[(size_t)blockIdx.x * kWCh + ch];
+            WQuick& qk = a.quick[(size_t)blockIdx.x * kWCh + ch];
+            if (M == 0) {
+              f.nseg = 0;
+              qk.e = kWNone;
+              qk.m = 0;
+            } else {
+              WSegment g;
+              g.e = el;
+              g.pad = 0;
+              g.v = (int64_t)M;
+              f.seg[0] = g;
+              f.nseg = 1;
+              qk.e = el;
+              qk.m = (int64_t)M;
+            }
+          }
+          __syncthreads();   // (s_fm reused by the next fold)
+          continue;
+        }
+      }
     }
     // block exclusive scan of the lanes' totals (an estimate: any rounding)
     double inc = T;
@@ -439,10 +496,10 @@ __device__ void w_fold_tile_seq(const WArgs& a, const WState& st, const WTile& t
     const uint32_t p = b + lane;
     double x = 0.0;
     if (p < t.end) {
-      const uint32_t id = st.src[p];
-      const uint32_t c = a.ucol[id];
+      const uint64_t r = st.src[p];
+      const uint32_t c = (uint32_t)r;
       const uint32_t R = (c >> 16) & 0xFF, G = (c >> 8) & 0xFF, B = c & 0xFF;
-      if (w_take(pass, st, R, G, B)) x = w_prod(ch, R, G, B, a.uw[id]);
+      if (w_take(pass, st, R, G, B)) x = w_prod(ch, R, G, B, w_weight(a, r));
     }
     const uint32_t n = min(64u, t.end - b);
     for (uint32_t j = 0; j < n; ++j) s += __shfl(x, (int)j, 64);
@@ -662,27 +719,11 @@ __global__ __launch_bounds__(64) void wk_chain(WArgs a, int pass) {
   }
 }
 
-// Round end, step 1: per tile, the new-side count of the final membership.
-__global__ __launch_bounds__(kWThreads) void wk_part_count(WArgs a) {
-  const WTile t = a.tiles[blockIdx.x];
-  const WState& st = a.nodes[t.node];
-  WPts q;
-  w_load(a, st, t, WP_KM, q);
-  uint32_t c = (uint32_t)__popc(q.take);
-  __shared__ uint32_t red[kWThreads / 64];
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t v = 0;
-    for (int w = 0; w < kWThreads / 64; ++w) v += red[w];
-    a.pbase[(size_t)blockIdx.x * 2 + 1] = v;
-  }
-}
-
-// Step 2: per node (one wave), the tiles' old / new bases; the node's results
-// (:820-871) into res.
+// Round end, step 1: per node (one wave), the tiles' old / new bases -- a
+// tile's new-side count under the final membership is its count of taken
+// summands in the node's last pass (tsum[.][7]: the pass whose decision
+// produced the final sums; a final node's tiles are skipped by later passes)
+// -- and the node's results (:820-871) into res.
 __global__ __launch_bounds__(64) void wk_part_scan(WArgs a) {
   const WState& st = a.nodes[blockIdx.x];
   const int lane = (int)threadIdx.x;
@@ -692,7 +733,7 @@ __global__ __launch_bounds__(64) void wk_part_scan(WArgs a) {
     uint32_t nw = 0, ol = 0;
     if (i < st.tile_end) {
       const WTile t = a.tiles[i];
-      nw = a.pbase[(size_t)i * 2 + 1];
+      nw = (uint32_t)a.tsum[(size_t)i * 8 + 7];
       ol = (t.end - t.start) - nw;
     }
     uint32_t io = ol, in = nw;
@@ -736,9 +777,11 @@ __global__ __launch_bounds__(64) void wk_part_scan(WArgs a) {
   }
 }
 
-// Step 3: per tile, the stable partition of its ids by the final decision
-// (old half first; point order kept in both halves, as the reference's
-// gather by ascending index, :894-1026).
+// Step 2: per tile, the stable partition of its records by the final
+// decision (old half first; point order kept in both halves, as the
+// reference's gather by ascending index, :894-1026): each record to its rank
+// in the tile's old / new run in LDS, then both runs out in coalesced 8-B
+// stores.
 __global__ __launch_bounds__(kWThreads) void wk_part_scatter(WArgs a) {
   const WTile t = a.tiles[blockIdx.x];
   const WState& st = a.nodes[t.node];
@@ -757,13 +800,25 @@ __global__ __launch_bounds__(kWThreads) void wk_part_scatter(WArgs a) {
   __shared__ uint32_t s_w[kWThreads / 64][2];
   if (lane == 63) { s_w[wv][0] = io; s_w[wv][1] = in; }
   __syncthreads();
-  uint32_t bo = a.pbase[(size_t)blockIdx.x * 2] + io - no, bn = a.pbase[(size_t)blockIdx.x * 2 + 1] + in - nn;
-  for (uint32_t w = 0; w < wv; ++w) { bo += s_w[w][0]; bn += s_w[w][1]; }
-  const uint32_t n_old = st.len - st.n_new;
+  __shared__ uint64_t s_rec[kWTile];
+  uint32_t to = io - no, tn = in - nn, tno = 0;   // this lane's ranks in the tile's runs; the old run's size
+  for (uint32_t w = 0; w < kWThreads / 64; ++w) {
+    if (w < wv) { to += s_w[w][0]; tn += s_w[w][1]; }
+    tno += s_w[w][0];
+  }
   for (uint32_t k = 0; k < nv; ++k) {
-    const uint32_t id = st.src[p0 + k];
-    if ((q.take >> k) & 1u) st.dst[st.off + n_old + bn++] = id;
-    else st.dst[st.off + bo++] = id;
+    const uint64_t r = st.src[p0 + k];
+    if ((q.take >> k) & 1u) s_rec[tno + tn++] = r;
+    else s_rec[to++] = r;
+  }
+  __syncthreads();
+  const uint32_t tlen = t.end - t.start;
+  const uint32_t n_old = st.len - st.n_new;
+  uint64_t* const dold = st.dst + st.off + a.pbase[(size_t)blockIdx.x * 2];
+  uint64_t* const dnew = st.dst + st.off + n_old + a.pbase[(size_t)blockIdx.x * 2 + 1];
+  for (uint32_t i = threadIdx.x; i < tlen; i += kWThreads) {
+    if (i < tno) dold[i] = s_rec[i];
+    else dnew[i - tno] = s_rec[i];
   }
 }
 }  // namespace
@@ -793,8 +848,8 @@ size_t color_table_scratch_bytes(uint32_t n) {
   return ((tmp + 255) & ~(size_t)255) + (size_t)n * (10 * 4 + 2 * 8) + 16 * 256;
 }
 
-int launch_color_table(const uint32_t* px, uint32_t n, double norm, void* scratch, size_t scratch_bytes,
-                       uint32_t* ucol, double* uw, uint32_t* h_nu, hipStream_t stream) {
+int launch_color_table(const uint32_t* px, uint32_t n, void* scratch, size_t scratch_bytes, uint64_t* rec,
+                       uint32_t* h_nu, hipStream_t stream) {
   size_t sort1 = 0, sort2 = 0, scan = 0;
   temp_sizes(n, &sort1, &sort2, &scan);
   size_t tmp = std::max(sort1, std::max(sort2, scan));
@@ -828,14 +883,11 @@ int launch_color_table(const uint32_t* px, uint32_t n, double norm, void* scratc
   size_t t2 = sort2;
   if (rocprim::radix_sort_pairs(temp, t2, okey, sokey, oval, sval, (size_t)nu, 0, 48, stream) != hipSuccess)
     return -2;
-  ct_final_kernel<<<dim3(grid_for(nu)), b, 0, stream>>>(sval, ucol_tmp, head, nu, n, norm, ucol, uw);
+  ct_final_kernel<<<dim3(grid_for(nu)), b, 0, stream>>>(sval, ucol_tmp, head, nu, n, rec);
   *h_nu = nu;
   return 0;
 }
 
-__global__ void iota_kernel(uint32_t* __restrict__ dst, uint32_t n) {
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) dst[i] = i;
-}
 
 // One output point per lane, grid-stride: the row / column split of t is one
 // 32-bit division per point (nr * nc < 2^32); an HBM gather (4 B read at the
@@ -859,10 +911,6 @@ void launch_cut_gather(const uint32_t* in, uint32_t* out, uint32_t nr, uint32_t 
   cut_gather_kernel<<<dim3(grid_for(nr * nc)), dim3(256), 0, stream>>>(in, out, nr, nc, dec, stride, sr, sg, sb);
 }
 
-void launch_iota(uint32_t* dst, uint32_t n, hipStream_t stream) {
-  if (n == 0) return;
-  iota_kernel<<<dim3(grid_for(n)), dim3(256), 0, stream>>>(dst, n);
-}
 
 
 void launch_wpass(int pass, const WArgs& a, hipStream_t stream) {
@@ -875,7 +923,6 @@ void launch_wpass(int pass, const WArgs& a, hipStream_t stream) {
 
 void launch_wfinish(const WArgs& a, hipStream_t stream) {
   if (a.ntiles <= 0 || a.nn <= 0) return;
-  wk_part_count<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a);
   wk_part_scan<<<dim3(a.nn), dim3(64), 0, stream>>>(a);
   wk_part_scatter<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a);
 }
