@@ -1078,9 +1078,20 @@ bool Engine::loop_ok(const Round& R) const {
 bool Engine::persist_ok(const Round& R) const {
   if (!persist_ || nshard_ != 1 || cross_process() || R.root || R.ntiles > (size_t)kPersistWgsPerCu * num_cus_)
     return false;
+  return persist_ok_layout(R);
+}
+
+bool Engine::persist_ok_layout(const Round& R) const {
   for (int a = 0; a < R.nl; ++a)
     if (nodes_[R.order[a]].buf == BUF_IN) return false;   // (a root's packed / BGR24 frame)
   return true;
+}
+
+size_t Engine::max_record_tiles(const Round& R) const {
+  size_t m = 1;
+  for (int r = 0; r < R.nr && r < (int)R.tbeg.size() && r < (int)R.tend.size(); ++r)
+    m = std::max<size_t>(m, (size_t)(R.tend[r] - R.tbeg[r]));
+  return m;
 }
 
 void Engine::kmeans_loop(Round& R, int max_iters, hipStream_t stream, int kind) {
@@ -1110,7 +1121,14 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
   // Late rounds (small records): every 2-means iteration in one launch,
   // waited for on the status word of iteration max_iters - 1
   // (kpersist_kernel, the same contract, for rounds of larger records)
-  const int loop = !fixed_point_ ? 0 : loop_ok(R) ? 1 : persist_ok(R) ? 2 : 0;
+  int loop = !fixed_point_ ? 0 : loop_ok(R) ? 1 : persist_ok(R) ? 2 : 0;
+  // a round too big for kpersist's co-residency bound (its tiles) may still
+  // take it once the split status says how few records are active: its
+  // final records' workgroups exit at once, so the active records' tiles are
+  // what must fit.  Then the speculative first iterations are not launched.
+  const bool persist_later = fixed_point_ && loop == 0 && persist_ && nshard_ == 1 && !cross_process() &&
+                             !R.root && persist_ok_layout(R);
+  if (persist_later) speculate = false;
   // Nothing else queued behind this round (a frame's last rounds): its first
   // 2-means iterations go in before its split status is known -- a record
   // final at the split makes them exit at once (~4 us each); C3's last round
@@ -1123,7 +1141,13 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
       for (; launched < max_iters && launched <= lookahead_; ++launched) kmeans_iter(R, launched, max_iters, stream);
     }
   }
-  if (fixed_point_) all_proven = wait_status(stat + max_iters, R.seq, stream) == 0;
+  uint32_t split_active = 0;
+  if (fixed_point_) {
+    split_active = wait_status(stat + max_iters, R.seq, stream);
+    all_proven = split_active == 0;
+  }
+  if (persist_later && !all_proven && (size_t)split_active * max_record_tiles(R) <= (size_t)kPersistWgsPerCu * num_cus_)
+    loop = 2;
   if (R.planned) {   // the plan's counts equal the host's mirror of its layout
     const uint32_t* hc = h_counts_ + 4 * R.par;
     const uint32_t ab = __atomic_load_n(hc + 2, __ATOMIC_ACQUIRE);

@@ -322,6 +322,8 @@ class Engine {
   // record one shard, planar, at most kloop_max_ points and kLoopMaxTiles tiles.
   bool loop_ok(const Round& R) const;
   bool persist_ok(const Round& R) const;
+  bool persist_ok_layout(const Round& R) const;   // planar records (not a root's frame)
+  size_t max_record_tiles(const Round& R) const;
   // kind 1: kloop_kernel, 2: kpersist_kernel
   void kmeans_loop(Round& R, int max_iters, hipStream_t stream, int kind);
   void apply_tune(const char* spec);
