@@ -2919,6 +2919,14 @@ __global__ __launch_bounds__(kBlock) void map_kernel(const MapTask* __restrict__
 //     a per-lane loop.
 // Same keys and the same answer as map_kernel.
 constexpr int kMapQ = 64;
+#ifndef DQ_MAP_PF
+#define DQ_MAP_PF 2
+#endif
+constexpr uint32_t kMapPf = DQ_MAP_PF;   // iterations of pixels in flight ahead (1 or 2)
+#ifndef DQ_MAP_LC
+#define DQ_MAP_LC 1
+#endif
+constexpr bool kMapLc = DQ_MAP_LC;       // packed pixels: lane-contiguous 16-B chunks
 // 12 BGR24 bytes (3 words, little-endian) -> 4 packed 0x00RRGGBB words.
 __device__ __forceinline__ u32x4 bgr12_to_px4(uint32_t w0, uint32_t w1, uint32_t w2) {
   u32x4 o;
@@ -2968,14 +2976,27 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   typedef const __attribute__((address_space(1))) u32x2v g_cu2;
   g_cu2* in2 = (g_cu2*)tk.in;
   constexpr bool bgr = BGR;   // (every task of a launch has the same pixel format)
-  auto load_group = [&](uint32_t gi, u32x4& a, u32x4& b) {
+  const uint32_t ngrp = n / kMapPx;
+  const uint32_t lb = blockIdx.x - tk.block_begin;
+  const uint32_t g0 = lb * tk.grp_per_block;
+  const uint32_t g1 = min(ngrp, g0 + tk.grp_per_block);
+  // packed pixels: the lane's two 16-B chunks of its wave's 2 KB, lane-
+  // contiguous per load instruction (chunks lane and 64 + lane of the wave's
+  // 128) when kMapLc, else the lane's own 32 B (chunks 2 lane, 2 lane + 1)
+  auto chunk = [&](uint32_t gi, uint32_t h) -> uint32_t {
+    return kMapLc ? 2u * (gi - lane) + 64u * h + lane : 2u * gi + h;
+  };
+  auto load_group = [&](uint32_t gi, u32x4& a, u32x4& b) {   // (nothing past the task's groups)
     if (bgr) {
-      const u32x2v x0 = in2[3 * gi], x1 = in2[3 * gi + 1], x2 = in2[3 * gi + 2];
-      a = (u32x4){x0.x, x0.y, x1.x, x1.y};
-      b = (u32x4){x2.x, x2.y, 0u, 0u};
+      if (gi < g1) {
+        const u32x2v x0 = in2[3 * gi], x1 = in2[3 * gi + 1], x2 = in2[3 * gi + 2];
+        a = (u32x4){x0.x, x0.y, x1.x, x1.y};
+        b = (u32x4){x2.x, x2.y, 0u, 0u};
+      }
     } else {
-      a = in4[2 * gi];
-      b = in4[2 * gi + 1];
+      const uint32_t c0 = chunk(gi, 0), c1 = chunk(gi, 1);
+      if (c0 < 2u * g1) a = in4[c0];
+      if (c1 < 2u * g1) b = in4[c1];
     }
   };
   // the output through a buffer resource: a lane past the task's groups
@@ -3040,30 +3061,27 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
     return answer(S, best);
   };
 
-  const uint32_t ngrp = n / kMapPx;
-  const uint32_t lb = blockIdx.x - tk.block_begin;
-  const uint32_t g0 = lb * tk.grp_per_block;
-  const uint32_t g1 = min(ngrp, g0 + tk.grp_per_block);
-  // the next iteration's pixels are loaded before this one's are mapped
-  u32x4 na = (u32x4){0u, 0u, 0u, 0u}, nb = na;
-  if (g0 + threadIdx.x < g1) load_group(g0 + threadIdx.x, na, nb);
-  // an iteration's two stores, here as no-ops: the loop's top waits for the
-  // previous loads only, entered from here or from the previous iteration
-  __builtin_amdgcn_raw_buffer_store_b128(na, orsrc, (int)kOOB, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b128(na, orsrc, (int)kOOB, 0, 0);
-  for (uint32_t gb = g0; gb < g1; gb += kMapLdsBlock) {
+  // the pixels of the next kMapPf iterations are in flight while one
+  // iteration's are mapped: kMapPf register buffers, used in turn (the
+  // iteration reloads the buffer it consumed)
+  auto noop_stores = [&]() {   // an iteration's two stores, as no-ops (kOOB)
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4){0u, 0u, 0u, 0u}, orsrc, (int)kOOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4){0u, 0u, 0u, 0u}, orsrc, (int)kOOB, 0, 0);
+  };
+  auto iter = [&](uint32_t gb, u32x4& ca, u32x4& cb) {
     const uint32_t g = gb + threadIdx.x;
-    const bool have = g < g1;
+    // (the lane's pixels 0-3 / 4-7: chunk(g, 0) / chunk(g, 1))
+    const bool have_a = bgr ? g < g1 : chunk(g, 0) < 2u * g1;
+    const bool have_b = bgr ? g < g1 : chunk(g, 1) < 2u * g1;
     uint32_t px[kMapPx];
     {
-      // a copy of the loads issued one iteration ago, made HERE (the asm makes
-      // it a value of its own): left to the compiler, the loop-carried copy
-      // sat at the end of the iteration and waited there for the loads the
-      // iteration had just issued
-      u32x4 a = na, b = nb;
+      // a copy of the loads issued kMapPf iterations ago, made HERE (the asm
+      // makes it a value of its own): left to the compiler, the loop-carried
+      // copy sat at the end of the iteration and waited there for the loads
+      // the iteration had just issued
+      u32x4 a = ca, b = cb;
       asm volatile("" : "+v"(a), "+v"(b));
-      const uint32_t gn = g + kMapLdsBlock;
-      if (gn < g1) load_group(gn, na, nb);
+      load_group(g + kMapPf * kMapLdsBlock, ca, cb);
       if (bgr) {
         const u32x4 lo = bgr12_to_px4(a[0], a[1], a[2]), hi = bgr12_to_px4(a[3], b[0], b[1]);
 #pragma unroll
@@ -3099,7 +3117,7 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
     uint32_t ovm = 0;
 #pragma unroll
     for (int e = 0; e < kMapPx; ++e) ovm |= (uint32_t)((rec[e] >> 30) == 0) << e;
-    if (!have) ovm = 0;
+    ovm &= (have_a ? 0x0Fu : 0u) | (have_b ? 0xF0u : 0u);
     const uint32_t cnt = (uint32_t)__builtin_popcount(ovm);
     uint32_t inc = cnt;
 #pragma unroll
@@ -3137,10 +3155,26 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
     {
       // (nontemporal, aux bit 1: streamed past the caches -- the next call's
       // root pass found its frame in L2 / MALL instead of the map's output)
-      const int o = (int)(have ? 32u * g : kOOB);
-      __builtin_amdgcn_raw_buffer_store_b128((u32x4){res[0], res[1], res[2], res[3]}, orsrc, o, 0, 2);
-      __builtin_amdgcn_raw_buffer_store_b128((u32x4){res[4], res[5], res[6], res[7]}, orsrc, o + 16, 0, 2);
+      const int oa = (int)(have_a ? 16u * (bgr ? 2u * g : chunk(g, 0)) : kOOB);
+      const int ob = (int)(have_b ? 16u * (bgr ? 2u * g + 1u : chunk(g, 1)) : kOOB);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){res[0], res[1], res[2], res[3]}, orsrc, oa, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){res[4], res[5], res[6], res[7]}, orsrc, ob, 0, 2);
     }
+  };
+  // (the prologue issues what an iteration issues after its loads, so the
+  // loop's top waits for the same count of operations on entry and after
+  // an iteration: its own buffer's loads only)
+  u32x4 na = (u32x4){0u, 0u, 0u, 0u}, nb = na, ma = na, mb = na;
+  load_group(g0 + threadIdx.x, na, nb);
+  noop_stores();
+  if (kMapPf == 2) {
+    load_group(g0 + kMapLdsBlock + threadIdx.x, ma, mb);
+    noop_stores();
+  }
+  for (uint32_t gb = g0; gb < g1; gb += kMapPf * kMapLdsBlock) {
+    iter(gb, na, nb);
+    if (kMapPf == 1 || gb + kMapLdsBlock >= g1) continue;   // (uniform)
+    iter(gb + kMapLdsBlock, ma, mb);
   }
   // tail (n % kMapPx points): the task's first workgroup, whole palette
   const uint32_t t = ngrp * kMapPx + threadIdx.x;
