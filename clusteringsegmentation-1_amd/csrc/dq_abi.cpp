@@ -7,7 +7,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -49,11 +48,6 @@ int current_device() {
 bool quiet() {
   const char* q = std::getenv("DQ_HIP_QUIET");
   return q && *q && *q != '0';
-}
-
-double now_ms() {
-  using namespace std::chrono;
-  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
 }
 
 // First-occurrence colortable dedup (quant_util.cpp:93-118).
@@ -935,7 +929,9 @@ void quant_recurse(uint32_t numPixels, const uint32_t* inPixelsPtr, uint32_t* ou
   Engine& e = engine_for(current_device());
   std::lock_guard<std::mutex> g(e.mutex());
   hipStream_t st = e.stream();
-  const double t0 = now_ms();
+  // the reference's timing lines (quant_util.cpp:48-66, 141-145): clock()
+  // CPU time of this process from t1, the map line cumulative from t1 too
+  const clock_t t1 = clock();
   e.stage_in(inPixelsPtr, numPixels, st);
   dq::FrameJob j;
   j.d_in = e.staged_in();
@@ -947,9 +943,9 @@ void quant_recurse(uint32_t numPixels, const uint32_t* inPixelsPtr, uint32_t* ou
   report_empty(j.num_empty);
   uint32_t k = (uint32_t)j.k_out;
   *numClustersPtr = k;
-  const double t1 = now_ms();
+  clock_t t2 = clock();
   if (!quiet()) {
-    long el = (long)(t1 - t0);
+    const long el = timediff(t1, t2);
     std::printf("quant_varpart_fast() elapsed: %ld ms aka %0.2f s\n", el, el / 1000.0f);
   }
   k = dedup_colortable(outColortablePtr, k);
@@ -958,8 +954,9 @@ void quant_recurse(uint32_t numPixels, const uint32_t* inPixelsPtr, uint32_t* ou
   DQ_HIP(hipMemcpyAsync(outPixelsPtr, e.staged_out(), (size_t)numPixels * 4,
                         hipMemcpyDeviceToHost, st));
   DQ_HIP(hipStreamSynchronize(st));
+  t2 = clock();
   if (!quiet()) {
-    long el = (long)(now_ms() - t1);
+    const long el = timediff(t1, t2);
     std::printf("map_colors_mps() elapsed: %ld ms aka %0.2f s\n", el, el / 1000.0f);
   }
 }
