@@ -95,6 +95,7 @@ void Engine::apply_tune(const char* spec) {
     else if (k == "eager_replan") eager_replan_ = v != 0;
     else if (k == "stats_only") stats_only_ = v != 0;
     else if (k == "fuse_plan") fuse_plan_ = v != 0;
+    else if (k == "fold_split") fold_split_ = v != 0;                   // split totals from the partition
     else if (k == "persist") persist_ = v != 0;                         // kpersist_kernel rounds
     else if (k == "kloop_max") kloop_max_ = (uint32_t)std::max<long>(0, std::min<long>(kLoopMaxLen, v));
     else die("DQ_HIP_TUNE", __FILE__, __LINE__, ("unknown key " + k).c_str());
@@ -572,7 +573,9 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   const size_t o_rd = o_wp + al(ntiles * kTileWaves * sizeof(uint32_t));
   // then the records' summaries (written as each becomes final; the next plan's scan)
   const size_t o_sum = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
-  const size_t bytes = o_sum + al((size_t)nr * sizeof(RecSummary));
+  // then the partition's per-parent arrival words (split totals folded in)
+  const size_t o_sd = o_sum + al((size_t)nr * sizeof(RecSummary));
+  const size_t bytes = o_sd + al((size_t)nr * sizeof(uint32_t));
   R.bytes = bytes;
   if (mode == TOT_ALLREDUCE) ensure_totals(nl, stream);
   // the staging is rewritten: its previous upload must have run
@@ -745,8 +748,14 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   ra.plane = cap_px_;
   ra.tot_mode = mode;
   ra.ps_mode = PS_FULL;
+  // allreduced totals with one shard and every record a partitioned parent's
+  // child: the partition's last workgroups write the split totals (no
+  // nodesum_kernel launch)
+  const bool fold = fold_split_ && mode == TOT_ALLREDUCE && S == 1 && n_own == 0 && nptiles > 0;
+  ra.sdone = fold ? reinterpret_cast<uint32_t*>(dblk + o_sd) : nullptr;
   if (nmat > 0) {
     RoundArgs ma = ra;
+    ma.sdone = nullptr;
     ma.ptiles = reinterpret_cast<const PartTile*>(dblk + o_mpt);
     ma.ps_mode = PS_WRITE;
     timed_begin(stream);
@@ -768,7 +777,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     ra.it = it < 0 ? 0 : it;
     timed_begin(stream);
     if (mode == TOT_ALLREDUCE) {
-      launch_nodesum(kind, ra, nl, stream);
+      if (!(kind == PASS_SPLIT && fold)) launch_nodesum(kind, ra, nl, stream);
       allreduce_totals(nl, stream);
     }
     launch_epilogue(kind, ra, nr, stream);
@@ -887,7 +896,8 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   const size_t o_wp = o_ctr + al((size_t)(max_iters + 1) * sizeof(LaunchCtr));
   const size_t o_rd = o_wp + al(R.tiles_cap * kTileWaves * sizeof(uint32_t));
   const size_t o_sum = o_rd + al((size_t)max_iters * nr * sizeof(uint32_t));
-  const size_t bytes = o_sum + al(nr * sizeof(RecSummary));   // ([o_ctr, bytes): zero on entry)
+  const size_t o_sd = o_sum + al(nr * sizeof(RecSummary));   // (the partition's per-parent arrivals)
+  const size_t bytes = o_sd + al(nr * sizeof(uint32_t));     // ([o_ctr, bytes): zero on entry)
   R.bytes = bytes;
   char* dblk = arena_alloc(bytes, stream);
   R.dn = reinterpret_cast<DevNode*>(dblk);
@@ -948,6 +958,9 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   ra.plane = cap_px_;
   ra.tot_mode = mode;
   ra.ps_mode = R.stats_only ? PS_STATS : PS_FULL;
+  // (split totals folded into the partition, as in enqueue_host_round)
+  const bool fold = fold_split_ && mode == TOT_ALLREDUCE && S == 1;
+  ra.sdone = fold ? reinterpret_cast<uint32_t*>(dblk + o_sd) : nullptr;
   // the plan and the partition in one launch (arena block zero) for rounds of
   // about one wave of partition workgroups (4 per CU) over at most one 4K
   // frame's points: there the plan's launch and round trips are on the
@@ -975,7 +988,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   }
   timed_begin(stream);
   if (mode == TOT_ALLREDUCE) {   // (an aborted round's nodesum writes nothing; every rank
-    launch_nodesum(PASS_SPLIT, ra, R.nl, stream);   //  aborts the same rounds: same totals)
+    if (!fold) launch_nodesum(PASS_SPLIT, ra, R.nl, stream);   //  aborts the same rounds: same totals)
     allreduce_totals(R.nl, stream);
   }
   launch_epilogue(PASS_SPLIT, ra, R.nr, stream);
@@ -983,6 +996,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   if (R.stats_only) {   // the points of every parent with a child still active
     RoundArgs la = ra;
     la.ps_mode = PS_LATE;
+    la.sdone = nullptr;
     timed_begin(stream);
     launch_partsplit(la, (int)R.ptiles_cap, src_fmt(R.parents), stream);
     timed_end(ST_PARTITION, 0.0, stream);

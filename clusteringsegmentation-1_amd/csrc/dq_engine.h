@@ -379,6 +379,8 @@ class Engine {
   // fused plan + partition launch, plansplit_kernel)
   std::vector<size_t> arena_hw_;
   bool fuse_plan_ = true;             // plansplit_kernel for one-shard planned rounds (DQ_HIP_TUNE fuse_plan)
+  bool fold_split_ = true;            // allreduced one-shard rounds: the partition's last workgroups
+                                      //   write the split totals, no nodesum_kernel (DQ_HIP_TUNE fold_split)
   char* h_stage_ = nullptr;           // pinned
   size_t cap_stage_tab_ = 0;
   TilePartial* d_parts_ = nullptr;    // per tile of the round

@@ -71,6 +71,10 @@ struct RoundArgs {
   int32_t tot_mode;         // where a record's pass totals come from (TotMode)
   int32_t ps_mode;          // what partsplit_kernel does (PsMode)
   RecSummary* rsum;         // per record, written with its final results (the next plan's scan)
+  uint32_t* sdone;          // TOT_ALLREDUCE, one shard: per parent (at its first listed
+                            //   child's record index), its partition workgroups finished --
+                            //   the last writes the children's split totals to tot (no
+                            //   nodesum_kernel); nullptr otherwise
 };
 
 // partsplit_kernel's work (RoundArgs::ps_mode):

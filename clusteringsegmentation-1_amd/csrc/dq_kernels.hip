@@ -1767,7 +1767,78 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
 // FMT: the source format of every parent of the launch (FMT_ANY: read from
 // each record -- every path compiled into one kernel, whose register
 // allocation is then the largest path's).
-template <int MODE, int FMT>
+// The children's split totals of a parent whose part tiles this launch
+// partitions, by the parent's last workgroup to finish (RoundArgs::sdone;
+// TOT_ALLREDUCE with one shard: exactly nodesum_kernel<PASS_SPLIT>'s sums,
+// without its launch).  Hand-off as kpass_kernel's: the partials (sparts,
+// write-through stores) drained by every wave before the workgroup's one
+// agent-scope release add; the last arriver acquires before it reads them.
+// KOFF: the byte offset of the launch's RoundArgs in its kernarg segment --
+// the arguments and the part tile are loaded again here, through a laundered
+// pointer: kept live across the partition, they spilled its registers.
+template <size_t KOFF>
+__device__ __forceinline__ void split_totals_last(uint64_t (*red64)[8]) {
+  typedef __attribute__((address_space(4))) const char* k_cp;
+  k_cp kp = (k_cp)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kp));
+  RoundArgs a;
+  __builtin_memcpy(&a, (const char*)kp + KOFF, sizeof(RoundArgs));
+  if (!a.sdone) return;
+  __shared__ int s_last;
+  PartTile pt;
+  {
+    typedef const __attribute__((address_space(1))) u32x4 g_cu4_;
+    static_assert(sizeof(PartTile) % 16 == 0, "16-B words");
+    const g_cu4_* src = (const g_cu4_*)(a.ptiles + blockIdx.x);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(PartTile) / 16); ++i) reinterpret_cast<u32x4*>(&pt)[i] = src[i];
+  }
+  const int32_t key = pt.child[0] >= 0 ? pt.child[0] : pt.child[1];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const g_cnode& P = *(g_cnode*)pt.parent;
+    const uint32_t nt = (uint32_t)(P.tile_end - P.tile_begin);   // the parent's part tiles
+    const bool last = __hip_atomic_fetch_add(a.sdone + key, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) ==
+                      nt - 1u;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  for (int c = 0; c < 2; ++c) {
+    const int32_t ch = pt.child[c];
+    if (ch < 0) continue;   // (uniform: a child this round does not split)
+    // (sum_record<PASS_SPLIT>'s fused-partials branch, through global pointers)
+    const g_cnode& w = *(g_cnode*)(a.nodes + ch);
+    const int side = w.split_side, pb = w.split_pb, pe = w.split_pe;
+    const g_cu4* sp4 = (const g_cu4*)a.sparts;
+    uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0}, tot[7];
+    for (int i = pb + (int)threadIdx.x; i < pe; i += kBlock) {
+      const u32x4 x = sp4[4 * i + 2 * side], y = sp4[4 * i + 2 * side + 1];
+      acc[0] += x[0];
+      acc[1] += x[1];
+      acc[2] += x[2];
+      acc[3] += x[3];
+      acc[4] += y[0];
+      acc[5] += y[1];
+      acc[6] += y[2];
+    }
+    block_sum7(acc, red64, tot);   // (valid in thread 0)
+    if (threadIdx.x == 0) {
+      typedef __attribute__((address_space(1))) uint64_t g_u64;
+      g_u64* g = (g_u64*)(a.tot + (size_t)ch * 8);   // (one shard: record = logical node)
+      for (int k = 0; k < F_NUM; ++k) g[k] = tot[k];
+      g[7] = 0;
+    }
+    __syncthreads();   // (red64 reused)
+  }
+}
+
+template <int MODE, int FMT, size_t KOFF>
 __device__ __forceinline__ void partsplit_tile(const RoundArgs& a, const PartTile& pt, const ChildInfo& ci0,
                                                const ChildInfo& ci1, uint8_t* stage, uint32_t (*red)[16]) {
   g_cnode& nd = *(g_cnode*)pt.parent;
@@ -1799,6 +1870,10 @@ __device__ __forceinline__ void partsplit_tile(const RoundArgs& a, const PartTil
     // (2 TilePartials: 16 words)
     __hip_atomic_store(a.sparts[2 * blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (MODE == PS_FULL || MODE == PS_STATS) {
+    __shared__ uint64_t red64[kBlock / 64][8];
+    split_totals_last<KOFF>(red64);
+  }
 }
 
 template <int MODE, int FMT>
@@ -1810,7 +1885,7 @@ __device__ __forceinline__ void partsplit_body(const RoundArgs& a, uint8_t* stag
     if (!a0 && !a1) return;
   }
   const ChildInfo ci0 = child_info(a.nodes, pt.child[0]), ci1 = child_info(a.nodes, pt.child[1]);
-  partsplit_tile<MODE, FMT>(a, pt, ci0, ci1, stage, red);
+  partsplit_tile<MODE, FMT, 0>(a, pt, ci0, ci1, stage, red);
 }
 
 // One kernel per (mode, parent format): each gets the registers its own path
@@ -2325,7 +2400,8 @@ __device__ __forceinline__ void plansplit_body(const PlanArgs& pa, const RoundAr
     c->tl = __builtin_amdgcn_readfirstlane(c->tl);
     c->tb = __builtin_amdgcn_readfirstlane(c->tb);
   }
-  partsplit_tile<MODE, FMT>(a, pt, ci0, ci1, stage, red);
+  static_assert(sizeof(PlanArgs) % alignof(RoundArgs) == 0, "kernarg layout: (PlanArgs, RoundArgs) packed");
+  partsplit_tile<MODE, FMT, sizeof(PlanArgs)>(a, pt, ci0, ci1, stage, red);
 }
 
 template <int MODE, int FMT>
