@@ -301,7 +301,8 @@ void Engine::ensure_round(size_t rec_cap, size_t tiles_cap, size_t, size_t stagi
                           int max_iters, hipStream_t stream) {
   const bool grow = staging_bytes > cap_stage_tab_ || !h_stage_ || !stage_ev_ || rec_cap > cap_res_ ||
                     !h_res_ || (size_t)max_iters + 1 > cap_stat_ || !h_stat_ || !h_counts_ ||
-                    tiles_cap > cap_parts_ || !d_parts_ || 2 * tiles_cap > cap_sparts_ || !d_sparts_;
+                    tiles_cap > cap_parts_ || !d_parts_ || tiles_cap > cap_parts2_ || !d_parts2_ ||
+                    2 * tiles_cap > cap_sparts_ || !d_sparts_;
   if (!grow) return;
   DQ_HIP(hipStreamSynchronize(stream));
   if (staging_bytes > cap_stage_tab_ || !h_stage_) {
@@ -339,6 +340,7 @@ void Engine::ensure_round(size_t rec_cap, size_t tiles_cap, size_t, size_t stagi
     DQ_HIP(hipHostGetDevicePointer((void**)&d_counts_h_, h_counts_, 0));
   }
   grow_device(&d_parts_, &cap_parts_, tiles_cap);
+  grow_device(&d_parts2_, &cap_parts2_, tiles_cap);
   grow_device(&d_sparts_, &cap_sparts_, std::max<size_t>(2 * tiles_cap, 2));
 }
 
@@ -728,6 +730,7 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
   ra.tiles = dt;
   ra.nodes = dn;
   ra.parts = d_parts_;
+  ra.parts2 = d_parts2_;
   ra.wparts = reinterpret_cast<uint32_t*>(dblk + o_wp);
   ra.ptiles = reinterpret_cast<const PartTile*>(dblk + o_pt);
   ra.sparts = d_sparts_;
@@ -937,6 +940,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   ra.tiles = R.dt;
   ra.nodes = R.dn;
   ra.parts = d_parts_;
+  ra.parts2 = d_parts2_;
   ra.wparts = reinterpret_cast<uint32_t*>(dblk + o_wp);
   ra.ptiles = pa.cpt;
   ra.sparts = d_sparts_;

@@ -384,6 +384,8 @@ class Engine {
   char* h_stage_ = nullptr;           // pinned
   size_t cap_stage_tab_ = 0;
   TilePartial* d_parts_ = nullptr;    // per tile of the round
+  TilePartial* d_parts2_ = nullptr;   // per tile: kpersist_kernel's odd iterations
+  size_t cap_parts2_ = 0;
   TilePartial* d_sparts_ = nullptr;   // per PartTile of the round
   size_t cap_parts_ = 0, cap_sparts_ = 0;
   // host-coherent pinned memory the epilogues write (results, status words),

@@ -47,6 +47,9 @@ struct RoundArgs {
   Tile* tiles;              // the round's tiles (kept: a later round partitions through them)
   DevNode* nodes;           // the round's node records (kept, as tiles)
   TilePartial* parts;       // one per tile, rewritten by every pass
+  TilePartial* parts2;      // one per tile: kpersist_kernel's odd iterations (its
+                            //   workgroups read a whole record's partials while others
+                            //   already write the next iteration's)
   uint32_t* wparts;         // per (tile, wave): old | new << 16 of the last pass (the
                             //   split pass's: own split pass, or added up by partsplit)
   const PartTile* ptiles;   // fused partition + split work of this round

@@ -1073,49 +1073,82 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) 
 
 // ---------------------------------------------------------------------------
 // Every 2-means iteration of a round in ONE launch over the round's tiles
-// (one workgroup per tile, as kpass_kernel): a record's
-// workgroups loop over the iterations themselves.  Per iteration each sweeps
-// its tile with the record's current decision and hands its partial to the
-// record's last arriver exactly as kpass_kernel does (write-through stores,
-// drained, agent-scope release add on rdone[it][record]); the last arriver
-// runs the same epilogue wave (node_update on the same exact integer sums:
-// every decision, fixed point and result is kpass's), then publishes the
-// next iteration by a second release add on the same word (ntiles + 1); the
-// others wait for that value with agent-scope loads and acquire before they
-// read the record again.  A record arrives on the counter of iteration
-// max_iters - 1 once, when final (kloop_kernel's status contract), so the
-// host waits for one status word instead of polling every iteration.
+// (one workgroup per tile, as kpass_kernel).  Each workgroup
+// keeps its own LDS copy of its record and loops over the iterations: it
+// sweeps its tile with the copy's decision, stores its partial (write-
+// through; partials alternate between two buffers by iteration parity) and
+// its per-wave counts, drains them and makes one agent-scope RELEASE add on
+// rdone[it][record]; then it waits until the word counts every tile of the
+// record (the add that returns ntiles - 1 needs no wait), acquires, sums the
+// record's partials itself and runs node_update on its copy -- the same
+// function on the same exact integer sums in every workgroup, so every copy
+// takes the same decision, fixed point and result as kpass's single
+// epilogue.  No second hand-off per iteration: each workgroup computes what
+// a last arriver would have published.  When the record is final, the
+// workgroup of its first tile writes the record back, the partition cursors
+// (this iteration's per-wave counts), the results and the record's one
+// arrival on the counter of iteration max_iters - 1 (kloop_kernel's status
+// contract); the others exit.  A workgroup reads the partials of iteration
+// it after the record's workgroups all stored them, and it overwrites its
+// own buffer of that parity only at it + 2, after every workgroup arrived at
+// it + 1 -- which each does after its reads of iteration it.
 // Waits only on the record's own workgroups, which all arrive before they
 // wait: no cycle.  Eligible rounds (Engine::persist_ok) have at most as many
-// tiles as the GPU holds resident workgroups, so a record's workgroups are
-// co-resident even if none of its round exits; every wait is bounded (a
-// record's workgroups give up after ~2^26 polls and leave its status unset:
-// the host's wait then reports the stream drained without it).
+// active records' tiles as the GPU holds resident workgroups, so a record's
+// workgroups are co-resident even if none of its round exits; every wait is
+// bounded (a record's workgroups give up after ~2^26 polls and leave its
+// status unset: the host's wait then reports the stream drained without it).
 constexpr uint32_t kPersistSpin = 1u << 26;
+
+// A Params copy in LDS read into SGPRs (wave-uniform: every lane holds the
+// same bytes).
+__device__ __forceinline__ Params uniform_params(const Params& p) {
+  Params q;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&p);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&q);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(Params) / 4); ++i) d[i] = (uint32_t)__builtin_amdgcn_readfirstlane(s[i]);
+  return q;
+}
+
 __global__ __launch_bounds__(kBlock, kPassWaves) void kpersist_kernel(RoundArgs a, int32_t max_iters) {
+  typedef __attribute__((address_space(1))) u32x4 g_u4;
   const Tile t = a.tiles[blockIdx.x];
   const int rec = t.node;   // (one shard per record: S == 1, TOT_OWN)
-  const DevNode& nd = a.nodes[rec];
-  const int ntiles = nd.tile_end - nd.tile_begin;
+  DevNode* gw = a.nodes + rec;
+  const uint32_t lane = lane_id();
+  __shared__ __attribute__((aligned(16))) DevNode sw;   // this workgroup's copy of the record
+  __shared__ NodeResult sres;
   __shared__ uint32_t red[kBlock / 64][8];
-  __shared__ int slast, sgo;
-  __shared__ NodeResult sres[1];
-  if (nd.done_it != 0) {   // final at its split: its first tile arrives for it
-    if ((int)blockIdx.x == nd.tile_begin && threadIdx.x == 0)
+  __shared__ int sgo, sfin;
+  static_assert(sizeof(DevNode) % 16 == 0, "the record is staged in 16-B words");
+  constexpr int kW16 = (int)(sizeof(DevNode) / 16);
+  if (threadIdx.x < (uint32_t)kW16) reinterpret_cast<u32x4*>(&sw)[threadIdx.x] = ((const g_cu4*)gw)[threadIdx.x];
+  __syncthreads();
+  const int tb = sw.tile_begin, te = sw.tile_end;
+  const int ntiles = te - tb;
+  const bool lead = (int)blockIdx.x == tb;   // the record's first tile: its final stores
+  if (sw.done_it != 0) {   // final at its split: its first tile arrives for it
+    if (lead && threadIdx.x == 0)
       arrive(a.ctr + (max_iters - 1), (uint32_t)rec, (uint32_t)a.nn, false, a.hstat + (max_iters - 1), a.seq);
     return;
   }
+  const uintptr_t srcw = (uintptr_t)sw.src;   // (each half through uint32_t: readfirstlane returns int)
+  const uint8_t* src = (const uint8_t*)(((uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(srcw >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)srcw));
   for (int it = 0; it < max_iters; ++it) {
-    const Params q = nd.prm;   // (this iteration's decision: read after the acquire below)
+    const bool klast = it == max_iters - 1;
+    TilePartial* parts = (it & 1) ? a.parts2 : a.parts;
+    const Params q = uniform_params(sw.prm);   // (this iteration's decision)
     LaneSums s;
     uint32_t ws, we;
     wave_range(t.start, t.end, wave_id(), ws, we);
-    wave_pass<PASS_KMEANS, true>(nd.src, a.plane, ws, we, q, s);
+    wave_pass<PASS_KMEANS, true>(src, a.plane, ws, we, q, s);
     uint32_t f[8] = {s.cnt, s.sr, s.sg, s.sb, s.qr, s.qg, s.qb, 0};
 #pragma unroll
     for (int k = 0; k < F_NUM; ++k) f[k] = wave_sum_u32(f[k]);
     const uint32_t vsum = wave_sum_u32(s.vcnt);
-    if (lane_id() == 0) {
+    if (lane == 0) {
       __hip_atomic_store(a.wparts + blockIdx.x * kTileWaves + wave_id(),
                          (vsum - f[F_CNT]) | (f[F_CNT] << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
@@ -1126,52 +1159,72 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void kpersist_kernel(RoundArgs 
       uint32_t x = 0;
 #pragma unroll
       for (int w = 0; w < kBlock / 64; ++w) x += red[w][threadIdx.x];
-      __hip_atomic_store(a.parts[blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(parts[blockIdx.x].f + threadIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if ((a.debug & kDebugUneven) && debug_unlucky(blockIdx.x + 131u * (uint32_t)it)) debug_sleep_us(10);
-    if (a.debug & kDebugPrewarm) {   // (tests) the record's lines into this CU's caches before the wait
-      const uint32_t x = __builtin_nontemporal_load(&nd.done_it) + (uint32_t)nd.prm.thr + nd.iter;
+    if ((a.debug & kDebugPrewarm) && wave_id() == 0) {   // (tests) the record's partials into this CU's caches
+      const uint32_t* pp = reinterpret_cast<const uint32_t*>(parts);
+      uint32_t x = 0;
+      for (int i = tb + (int)lane; i < te; i += 64)
+        for (int k = 0; k < 8; ++k) x += pp[(size_t)i * 8 + k];
       asm volatile("s_waitcnt vmcnt(0)" ::"v"(x) : "memory");
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (kpass_kernel's hand-off)
     __syncthreads();
     uint32_t* word = a.rdone + (size_t)it * a.nn + rec;
     if (threadIdx.x == 0) {
-      const bool last = __hip_atomic_fetch_add(word, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) ==
-                        (uint32_t)ntiles - 1;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      slast = last;
-    }
-    __syncthreads();
-    const bool klast = it == max_iters - 1;
-    if (slast && wave_id() == 0) {
-      if (klast) kmeans_epilogue_wave<PASS_KLAST>(a, rec, sres, max_iters - 1, true);
-      else kmeans_epilogue_wave<PASS_KMEANS>(a, rec, sres, max_iters - 1, true);
-      // the record (decision, state, done_it) and its results are stored:
-      // publish iteration it to the record's other workgroups
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane_id() == 0) __hip_atomic_fetch_add(word, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (klast) return;   // (PASS_KLAST finalises every record)
-    if (threadIdx.x == 0) {   // (the last arriver's own add is already in: no wait)
       int go = 1;
-      for (uint32_t spin = 0;
-           __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)ntiles + 1u; ++spin) {
-        if (spin == kPersistSpin) {   // (never in a correct run: the record's status stays unset)
-          go = 0;
-          break;
+      if (__hip_atomic_fetch_add(word, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)ntiles - 1u) {
+        for (uint32_t spin = 0;
+             __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)ntiles; ++spin) {
+          if (spin == kPersistSpin) {   // (never in a correct run: the record's status stays unset)
+            go = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_s_sleep(2);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      sgo = go && nd.done_it == 0;
+      sgo = go;
     }
     __syncthreads();
     if (!sgo) return;
+    // every workgroup: the record's totals, the FP64 update on its copy
+    if (wave_id() == 0) {
+      const uint32_t* pp = reinterpret_cast<const uint32_t*>(parts);
+      uint64_t tot[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
+      for (int i = tb + (int)lane; i < te; i += 64)
+#pragma unroll
+        for (int k = 0; k < F_NUM; ++k)
+          tot[k] += __hip_atomic_load(pp + (size_t)i * 8 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < F_NUM; ++k) tot[k] = wave_sum_u64(tot[k]);
+      if (lane == 0) {
+        const bool fin = klast ? node_update<PASS_KLAST>(&sw, &sres, tot, a.fixed_point != 0)
+                               : node_update<PASS_KMEANS>(&sw, &sres, tot, a.fixed_point != 0);
+        if (fin) {
+          for (int c = 0; c < 3; ++c) { sres.tm[c] = sw.tm[c]; sres.tv[c] = sw.tv[c]; }
+          sw.n_new_local = (uint32_t)tot[F_CNT];
+          sres.n_new_local = (uint32_t)tot[F_CNT];
+          sres.done_it = sw.done_it;
+        }
+        sfin = fin ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    if (sfin) {   // (uniform; PASS_KLAST finalises every record)
+      if (lead && wave_id() == 0) {   // the record, its cursors, results and arrival
+        if (lane < (uint32_t)kW16) ((g_u4*)gw)[lane] = reinterpret_cast<const u32x4*>(&sw)[lane];
+        record_cursors<true>(a.tiles, a.wparts, tb, te, lane);
+        store_result(a.hres + rec, a.dres ? a.dres + rec : nullptr, sres, lane, sw.len, a.seq,
+                     a.rsum ? a.rsum + rec : nullptr, &sw);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          arrive(a.ctr + (max_iters - 1), (uint32_t)rec, (uint32_t)a.nn, false, a.hstat + (max_iters - 1), a.seq);
+      }
+      return;
+    }
   }
 }
 

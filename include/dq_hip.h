@@ -235,9 +235,10 @@ void dq_hip_set_loop_max(int device, uint32_t max_points);
 int dq_hip_last_loop_rounds(int device);
 /* One-launch 2-means loops over a round's tiles (default on,
  * DQ_HIP_TUNE=persist=0 turns the default off): a round kloop does not take,
- * of one shard per record, planar records and at most 4 tiles per CU, runs
- * all its 2-means iterations in one kpersist_kernel launch, a record's
- * workgroups meeting per iteration.  Outputs are identical either way.
+ * of one shard per record, planar records and at most 4 tiles per CU (or,
+ * once its split status is known, at most 4 tiles per CU of records still
+ * active), runs all its 2-means iterations in one kpersist_kernel launch, a
+ * record's workgroups meeting per iteration.  Outputs are identical either way.
  * dq_hip_last_persist_rounds: how many rounds of the last run did so. */
 void dq_hip_set_persist(int device, int on);
 int dq_hip_last_persist_rounds(int device);
