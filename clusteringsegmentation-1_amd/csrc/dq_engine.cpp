@@ -96,7 +96,6 @@ void Engine::apply_tune(const char* spec) {
     else if (k == "stats_only") stats_only_ = v != 0;
     else if (k == "fuse_plan") fuse_plan_ = v != 0;
     else if (k == "fold_split") fold_split_ = v != 0;                   // split totals from the partition
-    else if (k == "fuse_init") fuse_init_ = v != 0;                     // root's INIT update in the split pass
     else if (k == "persist") persist_ = v != 0;                         // kpersist_kernel rounds
     else if (k == "kloop_max") kloop_max_ = (uint32_t)std::max<long>(0, std::min<long>(kLoopMaxLen, v));
     else die("DQ_HIP_TUNE", __FILE__, __LINE__, ("unknown key " + k).c_str());
@@ -788,24 +787,17 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     tmark("epi");
     timed_end(ST_EPILOGUE, 0.0, stream);
   };
-  // a root round with its records' own totals: the INIT update inside the
-  // split pass (pass_kernel's init_fused), no INIT epilogue launch
-  const bool init_fused = root_round && fuse_init_ && mode == TOT_OWN && S == 1 && nt_own == (size_t)nt;
   if (root_round) {
     pass(PASS_INIT, ST_INIT, nt, bytes_all, (double)total);
-    if (!init_fused) epilogue(PASS_INIT, -1);
+    epilogue(PASS_INIT, -1);
   }
-  ra.init_fused = init_fused ? 1 : 0;
   pass(PASS_SPLIT, ST_SPLIT, (int)nt_own, own_bytes, (double)own_total);
-  ra.init_fused = 0;
   if (nptiles > 0) {
     timed_begin(stream);
     launch_partsplit(ra, (int)nptiles, src_fmt(parents), stream);
     timed_end(ST_PARTITION, part_bytes, stream, (double)parent_total);
   }
-  if (init_fused) ra.parts = d_parts2_;   // (the split partials; later launches: parts again)
   epilogue(PASS_SPLIT, max_iters);
-  ra.parts = d_parts_;
   // the staging's reuse waits for this event; recorded behind the round's
   // kernels (stream order: after the upload) so that the host submits the
   // first kernels without it in between (~6-15 us of GPU idle at a call's start)
@@ -1653,20 +1645,16 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   }
   const double t_clu = trace_ ? host_us() : 0.0;
   // The next run's planned rounds find their blocks zero: clear what this run
-  // used, behind the last round's kernels.  With a map, behind the map's
-  // launches (the clear's own launch, ~5 us of host time, then stays off the
-  // path from the last round's results to the map's first kernel; on the GPU
-  // it runs after the map, 2-3 us); at the next run's start it delayed the
-  // first round by ~8 us.
-  auto clear_arena = [&]() {
-    for (size_t c = 0; c < arena_.size(); ++c)
-      if (arena_hw_[c] > 0) {
-        launch_zero(arena_[c].first, arena_hw_[c], stream);   // (chunks and allocations: 256-B multiples)
-        arena_hw_[c] = 0;
-      }
-    tmark("zero");
-  };
-  if (!dedup_map) clear_arena();
+  // used, behind the last round's kernels -- here, before the host's colour
+  // table work, so the clear runs while the host dedups instead of behind the
+  // map (at the next run's start it delayed the first round by ~8 us).
+  for (size_t c = 0; c < arena_.size(); ++c)
+    if (arena_hw_[c] > 0) {
+      launch_zero(arena_[c].first, arena_hw_[c], stream);   // (chunks and allocations: 256-B multiples)
+      arena_hw_[c] = 0;
+    }
+
+  tmark("zero");
   for (int i = 0; i < nframes; ++i) finish_frame(frames_[i], i == nframes - 1);
   tmark("finish_frame");
 
@@ -1698,7 +1686,6 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
     }
     if (!mj.empty()) map_many(mj.data(), (int)mj.size(), stream, false);
     tmark("map:enqueued");
-    clear_arena();
   }
   // Synchronous on return: lookahead launches of the last round may still be
   // queued, and they read the caller's input.

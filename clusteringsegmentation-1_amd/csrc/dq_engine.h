@@ -379,7 +379,6 @@ class Engine {
   // fused plan + partition launch, plansplit_kernel)
   std::vector<size_t> arena_hw_;
   bool fuse_plan_ = true;             // plansplit_kernel for one-shard planned rounds (DQ_HIP_TUNE fuse_plan)
-  bool fuse_init_ = true;             // root rounds: the INIT update inside the split pass (DQ_HIP_TUNE fuse_init)
   bool fold_split_ = true;            // allreduced one-shard rounds: the partition's last workgroups
                                       //   write the split totals, no nodesum_kernel (DQ_HIP_TUNE fold_split)
   char* h_stage_ = nullptr;           // pinned

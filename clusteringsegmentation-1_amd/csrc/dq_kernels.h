@@ -74,9 +74,6 @@ struct RoundArgs {
   int32_t tot_mode;         // where a record's pass totals come from (TotMode)
   int32_t ps_mode;          // what partsplit_kernel does (PsMode)
   RecSummary* rsum;         // per record, written with its final results (the next plan's scan)
-  int32_t init_fused;       // pass_kernel<PASS_SPLIT> of a root round: each workgroup runs
-                            //   the INIT update itself (no INIT epilogue launch), partials
-                            //   to parts2
   uint32_t* sdone;          // TOT_ALLREDUCE, one shard: per parent (at its first listed
                             //   child's record index), its partition workgroups finished --
                             //   the last writes the children's split totals to tot (no

@@ -517,69 +517,14 @@ __device__ bool node_update(DevNode* w, NodeResult* r, const uint64_t t[F_NUM], 
 // segment, so every point of the workgroup shares the node's parameters and
 // the sums need no per-point binning: packed lane partials -> wave sums ->
 // LDS -> one 32-B partial per tile.
-// A Params copy in LDS read into SGPRs (wave-uniform: every lane holds the
-// same bytes).
-__device__ __forceinline__ Params uniform_params(const Params& p) {
-  Params q;
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(&p);
-  uint32_t* d = reinterpret_cast<uint32_t*>(&q);
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(Params) / 4); ++i) d[i] = (uint32_t)__builtin_amdgcn_readfirstlane(s[i]);
-  return q;
-}
-
 // Waves per SIMD the pass kernels are compiled for (VGPR budget 512 / n).
-// RoundArgs::init_fused (the split pass of a root round, one shard, own
-// totals): every workgroup first runs the root's INIT update itself --
-// epilogue_kernel<PASS_INIT>'s sums over the INIT pass's partials and its
-// node_update, on an LDS copy of the record (the same integers into the same
-// function: every copy takes the same cut) -- and the workgroup of the
-// record's first tile writes the record back for the split epilogue; the
-// split partials then go to parts2 (other workgroups may still be reading
-// the INIT partials).  Saves the INIT epilogue's launch on every call's
-// first round.
 constexpr int kPassWaves = 4;
 template <int KIND>
 __global__ __launch_bounds__(kBlock, kPassWaves) void pass_kernel(RoundArgs a) {
   const Tile t = a.tiles[blockIdx.x];
   const DevNode& nd = a.nodes[t.node];
   if ((KIND == PASS_KMEANS || KIND == PASS_KLAST) && nd.done_it != 0) return;   // final
-  Params q;
-  TilePartial* parts_out = a.parts;
-  if (KIND == PASS_SPLIT && a.init_fused) {
-    typedef __attribute__((address_space(1))) u32x4 g_u4;
-    __shared__ __attribute__((aligned(16))) DevNode sw;
-    static_assert(sizeof(DevNode) % 16 == 0, "the record is staged in 16-B words");
-    constexpr int kW16 = (int)(sizeof(DevNode) / 16);
-    DevNode* gw = a.nodes + t.node;
-    if (threadIdx.x < (uint32_t)kW16) reinterpret_cast<u32x4*>(&sw)[threadIdx.x] = ((const g_cu4*)gw)[threadIdx.x];
-    __syncthreads();
-    if (wave_id() == 0) {
-      const uint32_t lane = lane_id();
-      const g_cu4* parts4 = (const g_cu4*)a.parts;
-      uint64_t tot[F_NUM] = {0, 0, 0, 0, 0, 0, 0};
-      for (int i = sw.tile_begin + (int)lane; i < sw.tile_end; i += 64) {
-        const u32x4 x = parts4[2 * i], y = parts4[2 * i + 1];
-        tot[0] += x[0];
-        tot[1] += x[1];
-        tot[2] += x[2];
-        tot[3] += x[3];
-        tot[4] += y[0];
-        tot[5] += y[1];
-        tot[6] += y[2];
-      }
-#pragma unroll
-      for (int k = 0; k < F_NUM; ++k) tot[k] = wave_sum_u64(tot[k]);
-      if (lane == 0) (void)node_update<PASS_INIT>(&sw, nullptr, tot, a.fixed_point != 0);
-    }
-    __syncthreads();
-    q = uniform_params(sw.prm);
-    if ((int)blockIdx.x == sw.tile_begin && threadIdx.x < (uint32_t)kW16)
-      ((g_u4*)gw)[threadIdx.x] = reinterpret_cast<const u32x4*>(&sw)[threadIdx.x];
-    parts_out = a.parts2;
-  } else {
-    q = nd.prm;
-  }
+  const Params q = nd.prm;
   constexpr int kNF = F_NUM;
 
   __shared__ uint32_t red[kBlock / 64][8];
@@ -607,7 +552,7 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void pass_kernel(RoundArgs a) {
     uint32_t x = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) x += red[w][threadIdx.x];
-    as_gw(parts_out[blockIdx.x].f)[threadIdx.x] = x;
+    as_gw(a.parts[blockIdx.x].f)[threadIdx.x] = x;
   }
 }
 
@@ -1154,6 +1099,17 @@ __global__ __launch_bounds__(kBlock, kPassWaves) void kpass_kernel(RoundArgs a) 
 // bounded (a record's workgroups give up after ~2^26 polls and leave its
 // status unset: the host's wait then reports the stream drained without it).
 constexpr uint32_t kPersistSpin = 1u << 26;
+
+// A Params copy in LDS read into SGPRs (wave-uniform: every lane holds the
+// same bytes).
+__device__ __forceinline__ Params uniform_params(const Params& p) {
+  Params q;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&p);
+  uint32_t* d = reinterpret_cast<uint32_t*>(&q);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(Params) / 4); ++i) d[i] = (uint32_t)__builtin_amdgcn_readfirstlane(s[i]);
+  return q;
+}
 
 __global__ __launch_bounds__(kBlock, kPassWaves) void kpersist_kernel(RoundArgs a, int32_t max_iters) {
   typedef __attribute__((address_space(1))) u32x4 g_u4;
