@@ -579,31 +579,34 @@ __device__ void w_decision(WState& w) {   // :616-623
 // chunks of 64 (one per lane): consecutive run tiles of one binade applied as
 // one integer sum, the others one by one -- then the reference's FP64
 // epilogue of the pass (lane-uniform; lane 0 stores).
-__global__ __launch_bounds__(64) void wk_chain(WArgs a, int pass) {
+// One wave per fold (kWCh waves per node): the seven folds are independent
+// chains over the same tiles, walked side by side; wave 0 then runs the
+// pass's epilogue on the seven sums.
+constexpr int kWChainThreads = 64 * kWCh;
+__global__ __launch_bounds__(kWChainThreads) void wk_chain(WArgs a, int pass) {
   WState& st = a.nodes[blockIdx.x];
   if (st.done) return;
-  const uint32_t lane = threadIdx.x;
-  double acc[kWCh];
+  const uint32_t lane = threadIdx.x & 63;
+  const int ch = (int)(threadIdx.x >> 6);   // this wave's fold
+  __shared__ double s_acc[kWCh];
+  __shared__ uint32_t s_cnt;
+  double s = 0.0;
   uint32_t cnt = 0;
-  for (int ch = 0; ch < kWCh; ++ch) acc[ch] = 0.0;
   for (int b = st.tile_begin; b < st.tile_end; b += 64) {
     const int ti = b + (int)lane;
     const bool have = ti < st.tile_end;
     const int nt = min(64, st.tile_end - b);
-    uint32_t c = have ? a.quick[(size_t)ti * kWCh].cnt : 0u;
+    if (ch == 0) {
+      uint32_t c = have ? a.quick[(size_t)ti * kWCh].cnt : 0u;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
-    cnt += c;
-    WQuick q7[kWCh];   // (every fold's record of the lane's tile in flight together)
-#pragma unroll
-    for (int ch = 0; ch < kWCh; ++ch) {
-      q7[ch].e = kWNone;
-      q7[ch].m = 0;
-      if (have) q7[ch] = a.quick[(size_t)ti * kWCh + ch];
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
+      cnt += c;
     }
-    for (int ch = 0; ch < kWCh; ++ch) {
-      const WQuick qk = q7[ch];
-      double s = acc[ch];
+    WQuick qk;
+    qk.e = kWNone;
+    qk.m = 0;
+    if (have) qk = a.quick[(size_t)ti * kWCh + ch];
+    {
       // walk: [pos, next complex) by binade groups, then the complex tile
       const uint64_t cm = __ballot(have && qk.e == kWComplex);
       int pos = 0;
@@ -652,9 +655,17 @@ __global__ __launch_bounds__(64) void wk_chain(WArgs a, int pass) {
         if (nc < nt) w_apply_tile(a, st, b + nc, pass, ch, s);
         pos = nc + 1;
       }
-      acc[ch] = s;
     }
   }
+  if (lane == 0) {
+    s_acc[ch] = s;
+    if (ch == 0) s_cnt = cnt;
+  }
+  __syncthreads();
+  if (ch != 0) return;
+  double acc[kWCh];
+  for (int c = 0; c < kWCh; ++c) acc[c] = s_acc[c];
+  cnt = s_cnt;
   // the pass's epilogue (every lane computes the same values; lane 0 stores)
   WState w = st;
   if (pass == WP_INIT) {   // DivQuantClusterInitMeanAndVar (:90-104), weighted
@@ -918,7 +929,7 @@ void launch_wpass(int pass, const WArgs& a, hipStream_t stream) {
   wk_tilesum<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_prefix<<<dim3(a.nn), dim3(64), 0, stream>>>(a);
   wk_classify<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
-  wk_chain<<<dim3(a.nn), dim3(64), 0, stream>>>(a, pass);
+  wk_chain<<<dim3(a.nn), dim3(kWChainThreads), 0, stream>>>(a, pass);
 }
 
 void launch_wfinish(const WArgs& a, hipStream_t stream) {
