@@ -228,10 +228,17 @@ __device__ __forceinline__ int w_binade(double v) {
 // the last member of the nearest earlier lane that has one).  The slots are
 // sequence order by construction, whatever the keys do along the tile.
 constexpr int kWKeyBias = 1100;   // binade e of a double in [-1074, 1023] -> e + bias in [26, 2123]
+// One workgroup per (tile, fold): the seven folds' descriptions of a tile
+// are independent, and were classified one after another (each with its
+// barriers) by one workgroup; the fold index varies fastest in the grid so a
+// tile's seven workgroups run together and share its lines in L2.
 __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
-  const WTile t = a.tiles[blockIdx.x];
+  const uint32_t ti = blockIdx.x / (uint32_t)kWCh;
+  const int ch = (int)(blockIdx.x % (uint32_t)kWCh);
+  const WTile t = a.tiles[ti];
   const WState& st = a.nodes[t.node];
   if (st.done) return;
+  if (ch == 0 && threadIdx.x == 0) a.quick[(size_t)ti * kWCh].cnt = (uint32_t)a.tsum[(size_t)ti * 8 + 7];
   WPts q;
   w_load(a, st, t, pass, q);
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -242,7 +249,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
   __shared__ unsigned long long s_m[kWSeg];
   __shared__ int s_e[kWSeg];
   __shared__ long long s_fm[kW];
-  for (int ch = 0; ch < kWCh; ++ch) {
+  {
     double x[kWPer];
     double T = 0.0;
 #pragma unroll
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
     // segment (e, sum of RNE(x / 2^(e-52))) -- no scans, no slots.  A tie
     // anywhere in the tile (x / u exactly halfway) takes the general path.
     {
-      const double P0 = a.tpre[(size_t)blockIdx.x * 8 + ch], Tt = a.tsum[(size_t)blockIdx.x * 8 + ch];
+      const double P0 = a.tpre[(size_t)ti * 8 + ch], Tt = a.tsum[(size_t)ti * 8 + ch];
       const double lo = P0 * (1.0 - kWMargin), hi = (P0 + Tt) * (1.0 + kWMargin);
       const int el = lo > 0.0 ? w_binade(lo) : 0;
       if (lo > 0.0 && el == w_binade(hi)) {   // (block-uniform: tile values)
@@ -279,8 +286,8 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
           long long M = 0;
           for (int w = 0; w < kW; ++w) M += s_fm[w];
           if (threadIdx.x == 0) {
-            WFold& f = a.fold[(size_t)blockIdx.x * kWCh + ch];
-            WQuick& qk = a.quick[(size_t)blockIdx.x * kWCh + ch];
+            WFold& f = a.fold[(size_t)ti * kWCh + ch];
+            WQuick& qk = a.quick[(size_t)ti * kWCh + ch];
             if (M == 0) {
               f.nseg = 0;
               qk.e = kWNone;
@@ -296,8 +303,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
               qk.m = (int64_t)M;
             }
           }
-          __syncthreads();   // (s_fm reused by the next fold)
-          continue;
+          return;
         }
       }
     }
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
     if (lane == 63) s_wt[wv] = inc;
     for (int b = (int)threadIdx.x; b < kWSeg; b += kWThreads) s_m[b] = 0ull;
     __syncthreads();
-    double P = a.tpre[(size_t)blockIdx.x * 8 + ch];
+    double P = a.tpre[(size_t)ti * 8 + ch];
     for (uint32_t w = 0; w < wv; ++w) P += s_wt[w];
     const double up = __shfl_up(inc, 1, 64);   // (every lane: a shuffle's source lane must be active)
     P += lane == 0 ? 0.0 : up;
@@ -448,7 +454,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
       if (cur >= 0 && cur < kWSeg) atomicAdd(&s_m[cur], acc);
     }
     __syncthreads();
-    WFold& f = a.fold[(size_t)blockIdx.x * kWCh + ch];
+    WFold& f = a.fold[(size_t)ti * kWCh + ch];
     const int ns = nseg > kWSeg ? -1 : nseg;
     if (ns > 0) {
       for (int i = (int)threadIdx.x; i < ns; i += kWThreads) {
@@ -461,7 +467,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
     }
     if (threadIdx.x == 0) {
       f.nseg = ns;
-      WQuick& qk = a.quick[(size_t)blockIdx.x * kWCh + ch];
+      WQuick& qk = a.quick[(size_t)ti * kWCh + ch];
       if (ns == 0) {
         qk.e = kWNone;
         qk.m = 0;
@@ -473,9 +479,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
         qk.m = 0;
       }
     }
-    __syncthreads();   // (shared arrays reused by the next fold)
   }
-  if (threadIdx.x == 0) a.quick[(size_t)blockIdx.x * kWCh].cnt = (uint32_t)a.tsum[(size_t)blockIdx.x * 8 + 7];
 }
 
 // s += u_e * M for a run of binade e; false if s is not in binade e or the
@@ -928,7 +932,7 @@ void launch_wpass(int pass, const WArgs& a, hipStream_t stream) {
   if (a.ntiles <= 0 || a.nn <= 0) return;
   wk_tilesum<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_prefix<<<dim3(a.nn), dim3(64), 0, stream>>>(a);
-  wk_classify<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
+  wk_classify<<<dim3(a.ntiles * kWCh), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_chain<<<dim3(a.nn), dim3(kWChainThreads), 0, stream>>>(a, pass);
 }
 
