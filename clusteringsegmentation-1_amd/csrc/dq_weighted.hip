@@ -800,12 +800,23 @@ __global__ __launch_bounds__(64) void wk_part_scan(WArgs a) {
 __global__ __launch_bounds__(kWThreads) void wk_part_scatter(WArgs a) {
   const WTile t = a.tiles[blockIdx.x];
   const WState& st = a.nodes[t.node];
-  WPts q;
-  w_load(a, st, t, WP_KM, q);
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t p0 = t.start + (uint32_t)kWPer * threadIdx.x;
   const uint32_t nv = p0 < t.end ? min((uint32_t)kWPer, t.end - p0) : 0u;
-  const uint32_t nn = (uint32_t)__popc(q.take), no = nv - nn;
+  // the lane's records, loaded once (the decision needs only the colour: no
+  // weights), kept for the staging below
+  uint64_t rv[kWPer];
+  uint32_t take = 0;
+#pragma unroll
+  for (int k = 0; k < kWPer; ++k) {
+    rv[k] = 0;
+    if ((uint32_t)k < nv) {
+      rv[k] = st.src[p0 + (uint32_t)k];
+      const uint32_t c = (uint32_t)rv[k];
+      if (w_take(WP_KM, st, (c >> 16) & 0xFF, (c >> 8) & 0xFF, c & 0xFF)) take |= 1u << k;
+    }
+  }
+  const uint32_t nn = (uint32_t)__popc(take), no = nv - nn;
   uint32_t io = no, in = nn;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -821,10 +832,12 @@ __global__ __launch_bounds__(kWThreads) void wk_part_scatter(WArgs a) {
     if (w < wv) { to += s_w[w][0]; tn += s_w[w][1]; }
     tno += s_w[w][0];
   }
-  for (uint32_t k = 0; k < nv; ++k) {
-    const uint64_t r = st.src[p0 + k];
-    if ((q.take >> k) & 1u) s_rec[tno + tn++] = r;
-    else s_rec[to++] = r;
+#pragma unroll
+  for (int k = 0; k < kWPer; ++k) {
+    if ((uint32_t)k < nv) {
+      if ((take >> k) & 1u) s_rec[tno + tn++] = rv[k];
+      else s_rec[to++] = rv[k];
+    }
   }
   __syncthreads();
   const uint32_t tlen = t.end - t.start;
