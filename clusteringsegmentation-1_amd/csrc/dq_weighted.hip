@@ -190,11 +190,13 @@ __global__ __launch_bounds__(kWThreads) void wk_tilesum(WArgs a, int pass) {
 }
 
 // Pass step 2: per node (one wave), the exclusive prefix of its tiles' sums.
-__global__ __launch_bounds__(64) void wk_prefix(WArgs a) {
+// (one wave per fold: the folds' prefixes are independent)
+__global__ __launch_bounds__(64 * kWCh) void wk_prefix(WArgs a) {
   const WState& st = a.nodes[blockIdx.x];
   if (st.done) return;
-  const int lane = (int)threadIdx.x;
-  for (int ch = 0; ch < kWCh; ++ch) {
+  const int lane = (int)(threadIdx.x & 63);
+  {
+    const int ch = (int)(threadIdx.x >> 6);
     double run = 0.0;
     for (int b = st.tile_begin; b < st.tile_end; b += 64) {
       const int i = b + lane;
@@ -944,7 +946,7 @@ void launch_cut_gather(const uint32_t* in, uint32_t* out, uint32_t nr, uint32_t 
 void launch_wpass(int pass, const WArgs& a, hipStream_t stream) {
   if (a.ntiles <= 0 || a.nn <= 0) return;
   wk_tilesum<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
-  wk_prefix<<<dim3(a.nn), dim3(64), 0, stream>>>(a);
+  wk_prefix<<<dim3(a.nn), dim3(64 * kWCh), 0, stream>>>(a);
   wk_classify<<<dim3(a.ntiles * kWCh), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_chain<<<dim3(a.nn), dim3(kWChainThreads), 0, stream>>>(a, pass);
 }
