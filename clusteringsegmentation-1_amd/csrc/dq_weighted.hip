@@ -65,7 +65,7 @@ __global__ void ct_heads_kernel(const uint32_t* __restrict__ skey, uint32_t n, u
 __global__ void ct_scatter_kernel(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sidx,
                                   const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
                                   uint32_t n, uint32_t* __restrict__ ucol, uint32_t* __restrict__ head,
-                                  uint64_t* __restrict__ okey, uint32_t* __restrict__ oval) {
+                                  uint64_t* __restrict__ okey) {
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
     if (!flag[i]) continue;
     const uint32_t u = pos[i], c = skey[i];
@@ -74,20 +74,17 @@ __global__ void ct_scatter_kernel(const uint32_t* __restrict__ skey, const uint3
     ucol[u] = c;
     head[u] = i;
     okey[u] = (h << 32) | (uint64_t)(0xFFFFFFFFu - sidx[i]);
-    oval[u] = u;
   }
 }
 
 // The points in calc_color_table's order as (colour | count << 32) records:
 // a pass reads a point's colour and its weight norm * count (:195) from its
 // own record, in node order (the partitions move records, not ids).
-__global__ void ct_final_kernel(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ ucol_tmp,
-                                const uint32_t* __restrict__ head, uint32_t nu, uint32_t n,
-                                uint64_t* __restrict__ rec) {
-  for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < nu; j += gridDim.x * 256u) {
-    const uint32_t u = sval[j];
+__global__ void ct_records_kernel(const uint32_t* __restrict__ ucol_tmp, const uint32_t* __restrict__ head,
+                                  uint32_t nu, uint32_t n, uint64_t* __restrict__ orec) {
+  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < nu; u += gridDim.x * 256u) {
     const uint32_t count = (u + 1 < nu ? head[u + 1] : n) - head[u];
-    rec[j] = (uint64_t)ucol_tmp[u] | ((uint64_t)count << 32);
+    orec[u] = (uint64_t)ucol_tmp[u] | ((uint64_t)count << 32);
   }
 }
 
@@ -865,7 +862,7 @@ static void temp_sizes(uint32_t n, size_t* sort1, size_t* sort2, size_t* scan) {
   (void)rocprim::radix_sort_pairs(nullptr, *sort1, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                   (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 24);
   (void)rocprim::radix_sort_pairs(nullptr, *sort2, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 48);
+                                  (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n, 0, 48);
   (void)rocprim::exclusive_scan(nullptr, *scan, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
                                 rocprim::plus<uint32_t>());
 }
@@ -874,8 +871,8 @@ size_t color_table_scratch_bytes(uint32_t n) {
   size_t sort1 = 0, sort2 = 0, scan = 0;
   temp_sizes(n, &sort1, &sort2, &scan);
   const size_t tmp = std::max(sort1, std::max(sort2, scan));
-  // key, idx, skey, sidx, flag, pos, ucol_tmp, head, oval, sval (u32) + okey, sokey (u64)
-  return ((tmp + 255) & ~(size_t)255) + (size_t)n * (10 * 4 + 2 * 8) + 16 * 256;
+  // key, idx, skey, sidx, flag, pos, ucol_tmp, head (u32) + okey, sokey, orec (u64)
+  return ((tmp + 255) & ~(size_t)255) + (size_t)n * (8 * 4 + 3 * 8) + 16 * 256;
 }
 
 int launch_color_table(const uint32_t* px, uint32_t n, void* scratch, size_t scratch_bytes, uint64_t* rec,
@@ -891,8 +888,8 @@ int launch_color_table(const uint32_t* px, uint32_t n, void* scratch, size_t scr
   auto take32 = [&]() { uint32_t* q = reinterpret_cast<uint32_t*>(p); p += ((size_t)n * 4 + 255) & ~(size_t)255; return q; };
   auto take64 = [&]() { uint64_t* q = reinterpret_cast<uint64_t*>(p); p += ((size_t)n * 8 + 255) & ~(size_t)255; return q; };
   uint32_t *key = take32(), *idx = take32(), *skey = take32(), *sidx = take32(), *flag = take32(), *pos = take32();
-  uint32_t *ucol_tmp = take32(), *head = take32(), *oval = take32(), *sval = take32();
-  uint64_t *okey = take64(), *sokey = take64();
+  uint32_t *ucol_tmp = take32(), *head = take32();
+  uint64_t *okey = take64(), *sokey = take64(), *orec = take64();
   const dim3 g(grid_for(n)), b(256);
   ct_keys_kernel<<<g, b, 0, stream>>>(px, n, key, idx);
   size_t t1 = sort1;
@@ -909,11 +906,13 @@ int launch_color_table(const uint32_t* px, uint32_t n, void* scratch, size_t scr
       hipStreamSynchronize(stream) != hipSuccess)
     return -2;
   const uint32_t nu = last[0] + last[1];
-  ct_scatter_kernel<<<g, b, 0, stream>>>(skey, sidx, flag, pos, n, ucol_tmp, head, okey, oval);
+  ct_scatter_kernel<<<g, b, 0, stream>>>(skey, sidx, flag, pos, n, ucol_tmp, head, okey);
+  // The records are built in unique-colour order (coalesced) and sorted as
+  // 8-byte payloads straight into rec: no gather after the sort.
+  ct_records_kernel<<<dim3(grid_for(nu)), b, 0, stream>>>(ucol_tmp, head, nu, n, orec);
   size_t t2 = sort2;
-  if (rocprim::radix_sort_pairs(temp, t2, okey, sokey, oval, sval, (size_t)nu, 0, 48, stream) != hipSuccess)
+  if (rocprim::radix_sort_pairs(temp, t2, okey, sokey, orec, rec, (size_t)nu, 0, 48, stream) != hipSuccess)
     return -2;
-  ct_final_kernel<<<dim3(grid_for(nu)), b, 0, stream>>>(sval, ucol_tmp, head, nu, n, rec);
   *h_nu = nu;
   return 0;
 }
