@@ -229,11 +229,16 @@ __device__ __forceinline__ int w_binade(double v) {
 constexpr int kWKeyBias = 1100;   // binade e of a double in [-1074, 1023] -> e + bias in [26, 2123]
 // One workgroup per (tile, fold): the seven folds' descriptions of a tile
 // are independent, and were classified one after another (each with its
-// barriers) by one workgroup; the fold index varies fastest in the grid so a
-// tile's seven workgroups run together and share its lines in L2.
+// barriers) by one workgroup.  Workgroups are dealt round-robin over the 8
+// XCDs (b and b + 8 share one; speed only, nothing relies on it), so a
+// tile's seven workgroups take seven consecutive slots of ONE residue class
+// b % 8: they run together on one XCD and read the tile through its L2
+// instead of fetching it into seven.
 __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
-  const uint32_t ti = blockIdx.x / (uint32_t)kWCh;
-  const int ch = (int)(blockIdx.x % (uint32_t)kWCh);
+  const uint32_t slot = blockIdx.x >> 3;
+  const uint32_t ti = (slot / (uint32_t)kWCh) * 8u + (blockIdx.x & 7u);
+  const int ch = (int)(slot % (uint32_t)kWCh);
+  if (ti >= (uint32_t)a.ntiles) return;
   const WTile t = a.tiles[ti];
   const WState& st = a.nodes[t.node];
   if (st.done) return;
@@ -946,7 +951,7 @@ void launch_wpass(int pass, const WArgs& a, hipStream_t stream) {
   if (a.ntiles <= 0 || a.nn <= 0) return;
   wk_tilesum<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_prefix<<<dim3(a.nn), dim3(64 * kWCh), 0, stream>>>(a);
-  wk_classify<<<dim3(a.ntiles * kWCh), dim3(kWThreads), 0, stream>>>(a, pass);
+  wk_classify<<<dim3(((a.ntiles + 7) / 8) * 8 * kWCh), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_chain<<<dim3(a.nn), dim3(kWChainThreads), 0, stream>>>(a, pass);
 }
 
