@@ -64,9 +64,10 @@ struct alignas(16) WTile {
 // in tile order as at most kWSeg segments -- a run of binade e adding the
 // exact integer sum M of RNE(x / 2^(e-52)), or one special summand x added
 // in hardware.  nseg < 0: more segments than that (a node's first tile has
-// 20-40: its sum crosses a binade every few summands from s = 0): the chain
-// folds the tile's summands one at a time.
-constexpr int kWSeg = 64;
+// 20-40: its sum crosses a binade every few summands from s = 0; on a 4K
+// noise frame 7 of the deep levels' first tiles had more than 64): the
+// chain folds the tile's summands one at a time (~20 us per tile and fold).
+constexpr int kWSeg = 128;
 constexpr int32_t kWSpecial = -100002;   // segment kind: a special summand (v = its bits)
 struct alignas(16) WSegment {
   int32_t e;                  // binade of a run, or kWSpecial

@@ -18,7 +18,7 @@ import pytest
 
 TILE = 4096
 MARGIN = 2.0 ** -20
-SEG_MAX = 64        # kWSeg
+SEG_MAX = 128       # kWSeg
 
 
 def seq_fold(x):

@@ -33,7 +33,7 @@ def main():
         ts.append((time.perf_counter() - t0) * 1e3)
     ok = bench.check_frame(pkg, o, ct, bench.frame_fixture(w, h, k, 0))
     print(json.dumps({"weighted_c3_ms": sorted(ts)[len(ts) // 2], "all_ms": [round(x, 3) for x in ts],
-                      "verified": ok}))
+                      "verified": ok, "seq_tiles_last_call": pkg.last_seq_tiles()}))
 
 
 if __name__ == "__main__":
