@@ -145,6 +145,28 @@ __device__ __forceinline__ void w_load(const WArgs& a, const WState& st, const W
   }
 }
 
+// The same points, lane-interleaved (point k of a lane is the tile's
+// k * kWThreads + lane): coalesced, for folds whose order does not matter
+// (the tile sums, the one-binade tiles' integer sums).
+__device__ __forceinline__ void w_load_co(const WArgs& a, const WState& st, const WTile& t, int pass, WPts& q) {
+  q.take = 0;
+#pragma unroll
+  for (int k = 0; k < kWPer; ++k) {
+    const uint32_t p = t.start + (uint32_t)(k * kWThreads) + threadIdx.x;
+    q.R[k] = q.G[k] = q.B[k] = 0;
+    q.w[k] = 0.0;
+    if (p < t.end) {
+      const uint64_t r = st.src[p];
+      const uint32_t c = (uint32_t)r;
+      q.w[k] = w_weight(a, r);
+      q.R[k] = (c >> 16) & 0xFF;
+      q.G[k] = (c >> 8) & 0xFF;
+      q.B[k] = c & 0xFF;
+      if (w_take(pass, st, q.R[k], q.G[k], q.B[k])) q.take |= 1u << k;
+    }
+  }
+}
+
 __device__ __forceinline__ double w_x(const WPts& q, int k, int ch) {
   return ((q.take >> k) & 1u) ? w_prod(ch, q.R[k], q.G[k], q.B[k], q.w[k]) : 0.0;
 }
@@ -162,7 +184,7 @@ __global__ __launch_bounds__(kWThreads) void wk_tilesum(WArgs a, int pass) {
   const WState& st = a.nodes[t.node];
   if (st.done) return;
   WPts q;
-  w_load(a, st, t, pass, q);
+  w_load_co(a, st, t, pass, q);
   __shared__ double red[kWThreads / 64][8];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
@@ -243,8 +265,6 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
   const WState& st = a.nodes[t.node];
   if (st.done) return;
   if (ch == 0 && threadIdx.x == 0) a.quick[(size_t)ti * kWCh].cnt = (uint32_t)a.tsum[(size_t)ti * 8 + 7];
-  WPts q;
-  w_load(a, st, t, pass, q);
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   constexpr int kW = kWThreads / 64;
   __shared__ double s_wt[kW];
@@ -253,6 +273,62 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
   __shared__ unsigned long long s_m[kWSeg];
   __shared__ int s_e[kWSeg];
   __shared__ long long s_fm[kW];
+  // One-binade tile (nearly every tile past a node's first few): with the
+  // tile's prefix estimate P0 and its sum estimate Tt, every summand's
+  // interval lies inside [P0 (1 - 2^-20), (P0 + Tt) (1 + 2^-20)] (the
+  // prefixes grow from P0, the summands are >= 0, and the estimates' errors
+  // are far inside the margin), so when that interval is in one binade e
+  // every nonzero summand is a run member of e: the description is one
+  // segment (e, sum of RNE(x / 2^(e-52))) -- no scans, no slots, and the
+  // order of the summands does not matter (an integer sum): the tile is
+  // loaded coalesced.  A tie anywhere in the tile (x / u exactly halfway)
+  // takes the general path.
+  {
+    const double P0 = a.tpre[(size_t)ti * 8 + ch], Tt = a.tsum[(size_t)ti * 8 + ch];
+    const double lo = P0 * (1.0 - kWMargin), hi = (P0 + Tt) * (1.0 + kWMargin);
+    const int el = lo > 0.0 ? w_binade(lo) : 0;
+    if (lo > 0.0 && el == w_binade(hi)) {   // (block-uniform: tile values)
+      WPts qc;
+      w_load_co(a, st, t, pass, qc);
+      long long mm = 0;
+      int tie = 0;
+#pragma unroll
+      for (int k = 0; k < kWPer; ++k) {
+        const double tt = ldexp(w_x(qc, k, ch), 52 - el);   // exact (x < 2^(el+1)); 0 for a non-summand
+        const double fl = floor(tt), fr = tt - fl;
+        tie |= fr == 0.5;
+        mm += (long long)fl + (fr > 0.5 ? 1 : 0);
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mm += __shfl_xor(mm, o, 64);
+      if (lane == 0) s_fm[wv] = mm;
+      if (!__syncthreads_or(tie)) {
+        long long M = 0;
+        for (int w = 0; w < kW; ++w) M += s_fm[w];
+        if (threadIdx.x == 0) {
+          WFold& f = a.fold[(size_t)ti * kWCh + ch];
+          WQuick& qk = a.quick[(size_t)ti * kWCh + ch];
+          if (M == 0) {
+            f.nseg = 0;
+            qk.e = kWNone;
+            qk.m = 0;
+          } else {
+            WSegment g;
+            g.e = el;
+            g.pad = 0;
+            g.v = (int64_t)M;
+            f.seg[0] = g;
+            f.nseg = 1;
+            qk.e = el;
+            qk.m = (int64_t)M;
+          }
+        }
+        return;
+      }
+    }
+  }
+  WPts q;
+  w_load(a, st, t, pass, q);
   {
     double x[kWPer];
     double T = 0.0;
@@ -260,56 +336,6 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
     for (int k = 0; k < kWPer; ++k) {
       x[k] = w_x(q, k, ch);
       T += x[k];
-    }
-    // One-binade tile (nearly every tile past a node's first few): with the
-    // tile's prefix estimate P0 and its sum estimate Tt, every summand's
-    // interval lies inside [P0 (1 - 2^-20), (P0 + Tt) (1 + 2^-20)] (the
-    // prefixes grow from P0, the summands are >= 0, and the estimates' errors
-    // are far inside the margin), so when that interval is in one binade e
-    // every nonzero summand is a run member of e: the description is one
-    // segment (e, sum of RNE(x / 2^(e-52))) -- no scans, no slots.  A tie
-    // anywhere in the tile (x / u exactly halfway) takes the general path.
-    {
-      const double P0 = a.tpre[(size_t)ti * 8 + ch], Tt = a.tsum[(size_t)ti * 8 + ch];
-      const double lo = P0 * (1.0 - kWMargin), hi = (P0 + Tt) * (1.0 + kWMargin);
-      const int el = lo > 0.0 ? w_binade(lo) : 0;
-      if (lo > 0.0 && el == w_binade(hi)) {   // (block-uniform: tile values)
-        long long mm = 0;
-        int tie = 0;
-#pragma unroll
-        for (int k = 0; k < kWPer; ++k) {
-          const double tt = ldexp(x[k], 52 - el);   // exact (x < 2^(el+1)); 0 for a non-summand
-          const double fl = floor(tt), fr = tt - fl;
-          tie |= fr == 0.5;
-          mm += (long long)fl + (fr > 0.5 ? 1 : 0);
-        }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) mm += __shfl_xor(mm, o, 64);
-        if (lane == 0) s_fm[wv] = mm;
-        if (!__syncthreads_or(tie)) {
-          long long M = 0;
-          for (int w = 0; w < kW; ++w) M += s_fm[w];
-          if (threadIdx.x == 0) {
-            WFold& f = a.fold[(size_t)ti * kWCh + ch];
-            WQuick& qk = a.quick[(size_t)ti * kWCh + ch];
-            if (M == 0) {
-              f.nseg = 0;
-              qk.e = kWNone;
-              qk.m = 0;
-            } else {
-              WSegment g;
-              g.e = el;
-              g.pad = 0;
-              g.v = (int64_t)M;
-              f.seg[0] = g;
-              f.nseg = 1;
-              qk.e = el;
-              qk.m = (int64_t)M;
-            }
-          }
-          return;
-        }
-      }
     }
     // block exclusive scan of the lanes' totals (an estimate: any rounding)
     double inc = T;
