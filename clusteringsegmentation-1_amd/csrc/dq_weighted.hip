@@ -833,15 +833,24 @@ __global__ __launch_bounds__(kWThreads) void wk_part_scatter(WArgs a) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t p0 = t.start + (uint32_t)kWPer * threadIdx.x;
   const uint32_t nv = p0 < t.end ? min((uint32_t)kWPer, t.end - p0) : 0u;
-  // the lane's records, loaded once (the decision needs only the colour: no
-  // weights), kept for the staging below
+  // The tile's records in through LDS: coalesced global loads (lane-
+  // interleaved), then each lane reads its kWPer consecutive records (one
+  // pad slot per kWPer records: conflict-free 8-B reads).  Loaded once (the
+  // decision needs only the colour: no weights) and kept for the staging.
+  __shared__ uint64_t s_rec[kWTile + kWTile / kWPer];
+#pragma unroll
+  for (int k = 0; k < kWPer; ++k) {
+    const uint32_t p = (uint32_t)(k * kWThreads) + threadIdx.x;
+    if (t.start + p < t.end) s_rec[p + p / (uint32_t)kWPer] = st.src[t.start + p];
+  }
+  __syncthreads();
   uint64_t rv[kWPer];
   uint32_t take = 0;
 #pragma unroll
   for (int k = 0; k < kWPer; ++k) {
     rv[k] = 0;
     if ((uint32_t)k < nv) {
-      rv[k] = st.src[p0 + (uint32_t)k];
+      rv[k] = s_rec[threadIdx.x * (uint32_t)(kWPer + 1) + (uint32_t)k];
       const uint32_t c = (uint32_t)rv[k];
       if (w_take(WP_KM, st, (c >> 16) & 0xFF, (c >> 8) & 0xFF, c & 0xFF)) take |= 1u << k;
     }
@@ -855,8 +864,7 @@ __global__ __launch_bounds__(kWThreads) void wk_part_scatter(WArgs a) {
   }
   __shared__ uint32_t s_w[kWThreads / 64][2];
   if (lane == 63) { s_w[wv][0] = io; s_w[wv][1] = in; }
-  __syncthreads();
-  __shared__ uint64_t s_rec[kWTile];
+  __syncthreads();   // (also: every lane's records are out of s_rec)
   uint32_t to = io - no, tn = in - nn, tno = 0;   // this lane's ranks in the tile's runs; the old run's size
   for (uint32_t w = 0; w < kWThreads / 64; ++w) {
     if (w < wv) { to += s_w[w][0]; tn += s_w[w][1]; }
