@@ -61,11 +61,12 @@ __global__ void ct_heads_kernel(const uint32_t* __restrict__ skey, uint32_t n, u
 
 // Run heads -> unique colour u: its colour, first occurrence (the sort is
 // stable, so the run's first index) and the run start; the ordering key
-// (hash << 32) | ~first sorts by bucket ascending, first occurrence descending.
+// (hash << nb) | (n - 1 - first) sorts by bucket ascending, first occurrence
+// descending.
 __global__ void ct_scatter_kernel(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sidx,
                                   const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
                                   uint32_t n, uint32_t* __restrict__ ucol, uint32_t* __restrict__ head,
-                                  uint64_t* __restrict__ okey) {
+                                  uint32_t nb, uint64_t* __restrict__ okey) {
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
     if (!flag[i]) continue;
     const uint32_t u = pos[i], c = skey[i];
@@ -73,7 +74,7 @@ __global__ void ct_scatter_kernel(const uint32_t* __restrict__ skey, const uint3
     const uint64_t h = (uint64_t)(((R * 33023 + G * 30013 + B * 27011) & 0x7fffffff) % 20023);   // HASH, :56-62
     ucol[u] = c;
     head[u] = i;
-    okey[u] = (h << 32) | (uint64_t)(0xFFFFFFFFu - sidx[i]);
+    okey[u] = (h << nb) | (uint64_t)(n - 1u - sidx[i]);   // (hash, descending index) in 15 + nb bits
   }
 }
 
@@ -897,11 +898,20 @@ static inline uint32_t grid_for(uint32_t n) {
 
 // rocPRIM's device-wide radix sort (stable, LSD) and exclusive scan: the
 // temporary storage each needs for n items.
+// The second sort's key: the colour's hash (15 bits, < 20023) above the
+// point's index reversed in nb bits, nb = the bits of n - 1 (fewer radix
+// passes than a 32-bit field for n < 2^25).
+static uint32_t index_bits(uint32_t n) {
+  uint32_t nb = 1;
+  while (nb < 32 && ((n - 1u) >> nb) != 0) ++nb;
+  return nb;
+}
+
 static void temp_sizes(uint32_t n, size_t* sort1, size_t* sort2, size_t* scan) {
   (void)rocprim::radix_sort_pairs(nullptr, *sort1, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                   (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 24);
   (void)rocprim::radix_sort_pairs(nullptr, *sort2, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                  (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n, 0, 48);
+                                  (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n, 0, 15 + index_bits(n));
   (void)rocprim::exclusive_scan(nullptr, *scan, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
                                 rocprim::plus<uint32_t>());
 }
@@ -945,12 +955,13 @@ int launch_color_table(const uint32_t* px, uint32_t n, void* scratch, size_t scr
       hipStreamSynchronize(stream) != hipSuccess)
     return -2;
   const uint32_t nu = last[0] + last[1];
-  ct_scatter_kernel<<<g, b, 0, stream>>>(skey, sidx, flag, pos, n, ucol_tmp, head, okey);
+  const uint32_t nb = index_bits(n);
+  ct_scatter_kernel<<<g, b, 0, stream>>>(skey, sidx, flag, pos, n, ucol_tmp, head, nb, okey);
   // The records are built in unique-colour order (coalesced) and sorted as
   // 8-byte payloads straight into rec: no gather after the sort.
   ct_records_kernel<<<dim3(grid_for(nu)), b, 0, stream>>>(ucol_tmp, head, nu, n, orec);
   size_t t2 = sort2;
-  if (rocprim::radix_sort_pairs(temp, t2, okey, sokey, orec, rec, (size_t)nu, 0, 48, stream) != hipSuccess)
+  if (rocprim::radix_sort_pairs(temp, t2, okey, sokey, orec, rec, (size_t)nu, 0, 15 + nb, stream) != hipSuccess)
     return -2;
   *h_nu = nu;
   return 0;
