@@ -182,6 +182,101 @@ def cpu_baseline(w, h, k):
                       "%.2f s, single thread (host has %d cores)" % (w, h, k, dt, os.cpu_count() or 0)}
 
 
+class _Quiet:
+    """fd 1 to /dev/null around the reference's calls (it prints two timer
+    lines per quant_recurse on stdout: the bench keeps stdout one JSON line)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        self.null = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(self.null, 1)
+
+    def __exit__(self, *exc):
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        os.close(self.null)
+
+
+def cpu_baseline_regions(regions, k, min_s=0.25):
+    """cpu_baseline for the weighted regions leg: the reference build
+    (oracle/_ref, one core) on each region, quant_recurse(K, allPixelsUnique=0)
+    -- ClusteringSegmentation.cpp:1779-1803's call -- timed over repeated calls
+    (at least min_s of CPU time per region), and its outputs, which the GPU's
+    are checked against.  None when the reference build is absent."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libdqref.so")
+    if not os.path.exists(ref_so):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dq_fixtures as fx
+    lib = ctypes.CDLL(ref_so)
+    res = []
+    for px in regions:
+        n = px.size
+        out = np.zeros(n, np.uint32)
+        ct = np.zeros(k, np.uint32)
+        calls, t = 0, 0.0
+        with _Quiet():
+            while t < min_s or calls < 1:
+                kk = ctypes.c_uint32(k)
+                t0 = time.perf_counter()
+                lib.quant_recurse(ctypes.c_uint32(n), fx.vp(px), fx.vp(out), ctypes.byref(kk), fx.vp(ct),
+                                  ctypes.c_int(0))
+                t += time.perf_counter() - t0
+                calls += 1
+        res.append({"us": t / calls * 1e6, "calls": calls, "out": out.copy(), "ct": ct[:kk.value].copy()})
+    return res
+
+
+def weighted_regions(pkg, torch, dev, stream, k, sides, image="batman", calls=0, cpu=True):
+    """The app's live weighted call at region sizes: square crops side x side
+    of the reference's sample image (tests/golden/png), quant_recurse(K,
+    allPixelsUnique=0) per call on device-resident pixels (one region per
+    call, synchronised like the app's loop over regions), beside the reference
+    build on the same crops; GPU outputs checked against the reference's."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dq_fixtures as fx
+    img, w, h = fx.load_png_u32(os.path.join(GOLDEN, "png", image + ".png"))
+    img = img.reshape(h, w)
+    regions = []
+    for s in sides:
+        s = min(s, w, h)
+        y0, x0 = (h - s) // 2, (w - s) // 2
+        regions.append(np.ascontiguousarray(img[y0:y0 + s, x0:x0 + s]).reshape(-1))
+    refs = cpu_baseline_regions(regions, k) if cpu else None
+    rows = []
+    for i, px in enumerate(regions):
+        n = px.size
+        t_in = torch.from_numpy(px.view(np.int32)).to(dev)
+        t_out = torch.empty_like(t_in)
+        nc = calls or max(20, min(400, int(2e6 / max(n, 1))))
+        last = {}
+
+        def one():
+            last["ct"], _ = pkg.quant_device(t_in, t_out, k, max_iters=10, stream=stream, all_pixels_unique=0)
+        for _ in range(3):
+            one()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(nc):
+            one()
+            torch.cuda.synchronize(dev)   # (the app's loop uses each region's result before the next)
+        gpu_us = (time.perf_counter() - t0) / nc * 1e6
+        row = {"n": int(n), "side": int(round(n ** 0.5)), "unique_colours": int(len(np.unique(px))),
+               "gpu_us_per_call": round(gpu_us, 1), "gpu_calls": nc}
+        if refs is not None:
+            r = refs[i]
+            out = t_out.cpu().numpy().view(np.uint32)
+            row["ref_cpu_us_per_call"] = round(r["us"], 1)
+            row["ref_cpu_calls"] = r["calls"]
+            row["gpu_over_cpu_speedup"] = round(r["us"] / gpu_us, 2)
+            row["verified"] = bool(np.array_equal(last["ct"], r["ct"]) and np.array_equal(out, r["out"]))
+        rows.append(row)
+        del t_in, t_out
+    return rows
+
+
 def init_dist():
     """(rank, world, local_rank) from the torchrun environment; one process
     per GPU over RCCL ("nccl"), or gloo without a GPU (CPU tests)."""

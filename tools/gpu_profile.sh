@@ -12,7 +12,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$1
 mkdir -p $O
 cd $R
-B="bench.py --lanes 1 --no-c3 --no-c2 --no-c5 --no-rowtile --no-bgr --no-cpu-baseline"
+B="bench.py --lanes 1 --no-c3 --no-c2 --no-c5 --no-rowtile --no-bgr --no-weighted --no-cpu-baseline"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- \
   python3 -u $B > $O/bench_prof.json 2> $O/bench_prof.err || { tail -20 $O/bench_prof.err; exit 1; }
 python3 tools/roofline_check.py $O/bench_prof.json $O/prof > $O/roofline_check.txt

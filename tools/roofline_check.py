@@ -37,6 +37,31 @@ def main():
     if not hit:
         raise SystemExit("kernel %s not in %s" % (roof["kernel"], stats[0]))
     r = hit[0]
+    # per instantiation (VERDICT r05 hygiene: the mixed average hides that
+    # PS_FULL alone runs longer): rocprof's own average per template, with
+    # the bytes of one launch on the engine work model when every launch of
+    # the instantiation covers every point of the step (one engine lane: the
+    # root partition, PS_FULL, PS_STATS); PS_LATE writes only the parents of
+    # records still active after their split (no fixed byte count)
+    per = []
+    pts = roof.get("points_per_launch")
+    model = {"<0, 0>": ("PS_FULL", 6.0), "<0, 2>": ("root PS_FULL from packed frames", 7.0),
+             "<0, 1>": ("root PS_FULL from BGR24 frames", 6.0), "<1, 0>": ("PS_STATS", 3.0),
+             "<2, 0>": ("PS_LATE", None), "<3, 0>": ("PS_WRITE", None)}
+    for row in rows:
+        nm = row["Name"].split("(")[0]
+        if ("dq::" + sym + "<") not in nm:
+            continue
+        t = nm[nm.index("<"):]
+        what, bpp = model.get(t, (t, None))
+        us = float(row["AverageNs"]) / 1e3
+        e = {"name": nm.replace("void ", ""), "mode": what, "calls": int(row["Calls"]), "rocprof_avg_us": round(us, 2),
+             "rocprof_min_us": round(float(row["MinNs"]) / 1e3, 2), "rocprof_max_us": round(float(row["MaxNs"]) / 1e3, 2)}
+        if bpp and pts:
+            e["engine_bytes_per_launch"] = round(bpp * d["config"].get("frames_per_rank_per_step", 1) *
+                                                 d["config"]["width"] * d["config"]["height"])
+            e["frac"] = round(e["engine_bytes_per_launch"] / (us * 1e-6) / 1e9 / roof["peak"], 4)
+        per.append(e)
     avg_us = float(r["AverageNs"]) / 1e3
     frac = roof["alg_bytes_per_launch"] / (avg_us * 1e-6) / 1e9 / roof["peak"]
     print(json.dumps({
@@ -46,6 +71,7 @@ def main():
         "rocprof_name": r["Name"], "rocprof_calls": int(r["Calls"]), "rocprof_avg_us": round(avg_us, 2),
         "ratio_rocprof_over_bench": round(avg_us / roof["avg_launch_us"], 4),
         "frac_from_rocprof_avg": round(frac, 4),
+        "per_instantiation": per,
         "stats_file": os.path.relpath(stats[0], os.path.dirname(os.path.abspath(sys.argv[1]))),
     }, indent=1))
 
