@@ -23,7 +23,9 @@ Workload (BASELINE.json metric "Mpixels/sec DivQuant K=256 on 4K RGB"):
                       totals per pass;
     detail.bgr24_input the C3 frame and the rank's batch as BGR24 Mats;
     detail.weighted_c3 the C3 frame through the weighted path
-                      (allPixelsUnique=0, the app's live call).
+                      (allPixelsUnique=0, the app's live call);
+    detail.weighted_regions that call at the app's region sizes (10^3 -
+                      10^6 pixels, K=4) beside the reference build.
 * --mode rows: F frames of the config (default 1; --config c5: the
   16384x16384 K=1024 gigapixel tile) row-tile sharded over the N ranks
   ("scaling": "strong": the total work is fixed).
@@ -265,6 +267,10 @@ def weighted_regions(pkg, torch, dev, stream, k, sides, image="batman", calls=0,
         gpu_us = (time.perf_counter() - t0) / nc * 1e6
         row = {"n": int(n), "side": int(round(n ** 0.5)), "unique_colours": int(len(np.unique(px))),
                "gpu_us_per_call": round(gpu_us, 1), "gpu_calls": nc}
+        prof = pkg.last_wsmall_profile() if hasattr(pkg, "last_wsmall_profile") else {}
+        row["path"] = "one launch (dq_wsmall.hip)" if prof else "multi-kernel rounds (dq_weighted.hip)"
+        if prof:
+            row["kernel_phases_us"] = {k: (round(v, 1) if isinstance(v, float) else v) for k, v in prof.items()}
         if refs is not None:
             r = refs[i]
             out = t_out.cpu().numpy().view(np.uint32)
@@ -668,6 +674,21 @@ def main():
                                  "verified": okw}
         if okw is False:
             fail("weighted-path output differs from the reference fixture", rank)
+        # the app's own call size: quant_recurse(N_region, .., K=4,
+        # allPixelsUnique=0) per superpixel region (ClusteringSegmentation.cpp:
+        # 1779-1803), square crops of the reference's sample image at 10^3 -
+        # 10^6 pixels, one region per call; the reference build on the same
+        # crops beside it (rank 0, N=1: the cpu_baseline's kind), the GPU's
+        # outputs checked against the reference's
+        rows = weighted_regions(pkg, torch, dev, stream, 4, [32, 100, 316, 1000],
+                                cpu=(rank == 0 and world == 1 and not a.no_cpu_baseline))
+        detail["weighted_regions"] = {
+            "workload": "quant_recurse(N, K=4, allPixelsUnique=0) on square crops of tests/golden/png/batman.png, "
+                        "one region per call, device-resident pixels; ref_cpu = the reference build "
+                        "(oracle/_ref, unmodified DivQuant sources), one core",
+            "regions": rows}
+        if any(r.get("verified") is False for r in rows):
+            fail("weighted-region outputs differ from the reference build's", rank, regions=rows)
     # --- the same frames as OpenCV BGR24 Mats: read directly by
     # the root's passes, partition and map (3 B per pixel, no packing pass);
     # one frame per call (C3 shape) and the rank's batch in one call

@@ -90,6 +90,8 @@ def lib():
         "dq_hip_set_loop_max": ([c.c_int, c.c_uint32], None),
         "dq_hip_last_loop_rounds": ([c.c_int], c.c_int),
         "dq_hip_set_persist": ([c.c_int, c.c_int], None),
+        "dq_hip_set_wsmall": ([c.c_int, c.c_int], None),
+        "dq_hip_last_wsmall_profile": ([c.c_int, c.c_void_p, c.c_int], c.c_int),
         "dq_hip_last_persist_rounds": ([c.c_int], c.c_int),
         "dq_hip_set_timing": ([c.c_int, c.c_int], None),
         "dq_hip_reset_stats": ([c.c_int], None),
@@ -587,6 +589,25 @@ def last_loop_rounds(device=0):
 def set_persist(on, device=0):
     """kpersist_kernel rounds on / off (every lane of the device)."""
     lib().dq_hip_set_persist(device, 1 if on else 0)
+
+
+def set_wsmall(on, device=0):
+    """The one-launch weighted path for small inputs on / off (every lane)."""
+    lib().dq_hip_set_wsmall(device, 1 if on else 0)
+
+
+def last_wsmall_profile(device=0):
+    """The last weighted call's one-launch phase profile in microseconds
+    (hash set, colour table, clustering, map, of which fold passes and
+    partitions) and its passes by kind; {} if it did not take that path."""
+    buf = np.zeros(8, np.uint64)
+    if lib().dq_hip_last_wsmall_profile(device, buf.ctypes.data_as(ctypes.c_void_p), 8) < 8:
+        return {}
+    t = [float(v) / 100.0 for v in buf[:7]]   # 100 MHz ticks -> us
+    k = int(buf[7])
+    return {"hash_us": t[1] - t[0], "table_us": t[2] - t[1], "cluster_us": t[3] - t[2], "map_us": t[4] - t[3],
+            "passes_us": t[5], "partitions_us": t[6],
+            "passes": {"init": k & 0xFFFF, "split": (k >> 16) & 0xFFFF, "kmeans": (k >> 32) & 0xFFFF}}
 
 
 def last_persist_rounds(device=0):

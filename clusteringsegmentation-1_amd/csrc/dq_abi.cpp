@@ -865,6 +865,13 @@ int dq_hip_last_rounds(int device) { return engine_for(device).last_rounds; }
 uint64_t dq_hip_last_points_swept(int device) { return engine_for(device).last_points_swept; }
 uint64_t dq_hip_last_points_full(int device) { return engine_for(device).last_points_full; }
 uint64_t dq_hip_last_seq_tiles(int device) { return engine_for(device).last_seq_tiles; }
+
+int dq_hip_last_wsmall_profile(int device, uint64_t* out, int nout) {
+  const std::vector<uint64_t>& p = engine_for(device).last_wsmall_prof;
+  const int n = std::min<int>(nout, (int)p.size());
+  for (int i = 0; i < n; ++i) out[i] = p[i];
+  return n;
+}
 void dq_hip_set_fixed_point(int device, int on) { engine_for(device).set_fixed_point(on != 0); }
 void dq_hip_set_planned_rounds(int device, int on) {
   for (int l = 0; l < dq::kMaxLanes; ++l) engine_for(device, l).set_plan(on != 0);
@@ -882,6 +889,10 @@ void dq_hip_set_persist(int device, int on) {
 }
 
 int dq_hip_last_persist_rounds(int device) { return engine_for(device).last_persist_rounds; }
+
+void dq_hip_set_wsmall(int device, int on) {
+  for (int l = 0; l < dq::kMaxLanes; ++l) engine_for(device, l).set_wsmall(on != 0);
+}
 
 void dq_hip_set_timing(int device, int on) { engine_for(device).set_timing(on != 0); }
 

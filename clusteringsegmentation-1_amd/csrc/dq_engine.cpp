@@ -97,6 +97,7 @@ void Engine::apply_tune(const char* spec) {
     else if (k == "fuse_plan") fuse_plan_ = v != 0;
     else if (k == "fold_split") fold_split_ = v != 0;                   // split totals from the partition
     else if (k == "persist") persist_ = v != 0;                         // kpersist_kernel rounds
+    else if (k == "wsmall") wsmall_ = v != 0;                           // one-launch small weighted calls
     else if (k == "kloop_max") kloop_max_ = (uint32_t)std::max<long>(0, std::min<long>(kLoopMaxLen, v));
     else die("DQ_HIP_TUNE", __FILE__, __LINE__, ("unknown key " + k).c_str());
   }
@@ -1740,6 +1741,11 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     DQ_CHECK(nr * nc <= 0xFFFFFFF0ull, "too many points");
   }
   const uint32_t n = gather ? (uint32_t)(nr * nc) : job.n;
+  last_wsmall_prof.clear();
+  // a small input (a superpixel region: ClusteringSegmentation.cpp:1779-1803)
+  // in one launch; more colours than it holds -> the rounds below
+  if (wsmall_ && !gather && n <= kWsMaxN && job.k <= kWsMaxK && run_weighted_small(job, max_iters, dedup_map, stream))
+    return;
   if (!h_wactive_) DQ_HIP(hipHostMalloc((void**)&h_wactive_, 64, hipHostMallocDefault));
   ensure_round(2 * (size_t)job.k + 64, 1024, 0, 0, max_iters, stream);   // staging, results
   // scratch: colour table, unique colours + weights, two id buffers (P0/P1)
@@ -1985,6 +1991,62 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     if (job.d_out) map(job.d_in, job.n, job.d_out, job.ct, m, stream);
   }
   DQ_HIP(hipStreamSynchronize(stream));
+}
+
+// The whole weighted call in one workgroup (dq_wsmall.hip): colour table,
+// DivQuantCluster<false,*,true> split by split, final centres, dedup and --
+// for at most kWsMapMax colours -- the map.  Returns false when the input has
+// more colours than the kernel holds (nothing written; the caller runs the
+// rounds).  Synchronous, as run_weighted.
+bool Engine::run_weighted_small(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream) {
+  if (!h_wsres_) {
+    DQ_HIP(hipHostMalloc((void**)&h_wsres_, sizeof(WSmallResult), hipHostMallocCoherent | hipHostMallocMapped));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_wsres_, h_wsres_, 0));
+    DQ_HIP(hipMalloc((void**)&d_wsmap_, sizeof(WsMapTab)));
+  }
+  __atomic_store_n(&h_wsres_->status, 0u, __ATOMIC_RELEASE);
+  WSmallArgs wa;
+  wa.px = job.d_in;
+  wa.out = dedup_map ? job.d_out : nullptr;
+  wa.res = d_wsres_;
+  wa.maptab = d_wsmap_;
+  // norm_factor = 1 / (ceil(numRows / dec) * ceil(numCols / dec)) (:184), rows = dec = 1
+  wa.norm = 1.0 / (std::ceil(1.0 / 1.0) * std::ceil((double)job.n / 1.0));
+  wa.n = job.n;
+  wa.k = job.k;
+  wa.max_iters = max_iters;
+  wa.fixed_point = fixed_point_ ? 1 : 0;
+  DQ_HIP(launch_wsmall(wa, stream));
+  sync_stream(stream);
+  const WSmallResult& r = *h_wsres_;
+  const uint32_t st = __atomic_load_n(&r.status, __ATOMIC_ACQUIRE);
+  if (st == 2) return false;
+  DQ_CHECK(st == 1, st == 3 ? "small weighted kernel: partition count differs from the fold count"
+                            : "small weighted kernel: no result");
+  const int k = job.k;
+  job.k_out = (int)r.k_raw;
+  job.num_empty = (int)r.num_empty;
+  for (uint32_t i = 0; i < r.k_raw; ++i) job.ct[i] = r.ct[i];
+  last_means.assign(r.means, r.means + (size_t)k * 3);
+  last_sizes.assign(r.sizes, r.sizes + k);
+  last_trace.assign(r.trace, r.trace + (size_t)(k - 1) * 4);
+  last_rounds = 1;
+  last_planned = last_aborted = 0;
+  last_points_swept = last_points_full = 0;
+  last_seq_tiles = 0;
+  last_wsmall_prof.assign(r.prof, r.prof + 8);
+  if (dedup_map) {   // first-occurrence dedup (quant_util.cpp:93-118), as run_weighted
+    int m = 0;
+    for (int i = 0; i < job.k_out; ++i) {
+      bool seen = false;
+      for (int j = 0; j < m && !seen; ++j) seen = job.ct[j] == job.ct[i];
+      if (!seen) job.ct[m++] = job.ct[i];
+    }
+    DQ_CHECK(m == (int)r.m, "small weighted kernel: dedup count differs from the host's");
+    job.k_out = m;
+    if (job.d_out && !r.mapped) map(job.d_in, job.n, job.d_out, job.ct, m, stream);
+  }
+  return true;
 }
 
 // ---------------------------------------------------------------------------

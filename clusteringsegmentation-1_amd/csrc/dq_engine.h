@@ -23,6 +23,7 @@
 
 #include "dq_internal.h"
 #include "dq_kernels.h"
+#include "dq_weighted.h"
 
 namespace dq {
 
@@ -225,6 +226,7 @@ class Engine {
   uint64_t last_points_swept = 0;     // sum over passes of points read (all frames)
   uint64_t last_points_full = 0;      // the same without fixed-point finalisation
   uint64_t last_seq_tiles = 0;        // weighted: tiles folded one summand at a time
+  std::vector<uint64_t> last_wsmall_prof;   // weighted, one launch: WSmallResult::prof (empty: not taken)
 
   void set_timing(bool on) { timing_ = on; }
   bool timing() const { return timing_; }
@@ -246,6 +248,8 @@ class Engine {
   // kloop_kernel eligibility: records of at most n points (0: never)
   void set_loop_max(uint32_t n) { kloop_max_ = std::min<uint32_t>(n, kLoopMaxLen); }
   void set_persist(bool on) { persist_ = on; }
+  // the one-workgroup weighted path for small inputs (launch_wsmall; default on)
+  void set_wsmall(bool on) { wsmall_ = on; }
   bool plan() const { return plan_; }
   bool fixed_point() const { return fixed_point_; }
   void reset_stats();
@@ -459,6 +463,11 @@ class Engine {
   size_t cap_wscratch_ = 0;
   void* d_wnodes_ = nullptr;          // a round's WState records, tiles, fold tables, results
   uint32_t* h_wactive_ = nullptr;     // pinned: the round's nodes not final after the split
+  bool wsmall_ = true;                // small weighted calls in one launch (DQ_HIP_TUNE wsmall)
+  WSmallResult* h_wsres_ = nullptr;   // host-coherent: its result
+  WSmallResult* d_wsres_ = nullptr;
+  WsMapTab* d_wsmap_ = nullptr;       // device: its palette for the grid map
+  bool run_weighted_small(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream);
   size_t cap_wnodes_ = 0;
 
   std::vector<Node> nodes_;

@@ -111,4 +111,53 @@ void launch_wfinish(const WArgs& a, hipStream_t stream);           // partition 
 void launch_cut_gather(const uint32_t* in, uint32_t* out, uint32_t nr, uint32_t nc, uint32_t dec,
                        uint32_t stride, uint32_t sr, uint32_t sg, uint32_t sb, hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// The whole weighted quant_recurse of a SMALL input in one workgroup
+// (dq_wsmall.hip): the app calls quant_recurse(N_region, .., K=4,
+// allPixelsUnique=0) once per superpixel region (ClusteringSegmentation.cpp:
+// 1779-1803), 10^3-10^5 pixels each, where the multi-kernel path above pays
+// ~1 ms of launches and host round trips per call against the reference's
+// 30-1000 us on one core.  One launch: calc_color_table in LDS (hash table,
+// counting sort by bucket, first occurrence descending inside a bucket),
+// then DivQuantCluster<false,*,true> split by split in the reference's own
+// order (:346-892, the greedy choice on the device), every fold sequential in
+// point order as the reference's (one wave per fold; 64 summands added as one
+// exact integer run when they provably stay in one binade), the stable
+// partitions in LDS, the final centres and the first-occurrence dedup
+// (quant_util.cpp:93-118), and -- for at most kWsMapMax deduped colours,
+// where std::sort is libstdc++'s insertion sort (stable) -- the palette sort,
+// lut_init and map_colors_mps (DivQuantMapColors.cpp:227-527) too.
+constexpr uint32_t kWsMaxN = 131071;   // pixels (first occurrences fit 17 bits)
+constexpr uint32_t kWsMaxU = 6144;     // unique colours (LDS: two 48-KB record buffers)
+constexpr int kWsMaxK = 64;            // clusters
+constexpr int kWsMapMax = 16;          // deduped colours mapped in the kernel
+struct WSmallResult {                  // host-coherent pinned memory
+  uint32_t status;                     // 1: done; 2: more than kWsMaxU colours (nothing else valid)
+  uint32_t nu, k_raw, num_empty;       // colours; ct entries before the dedup; empty clusters
+  uint32_t mapped, m, passes, pad;     // out written; deduped colours; fold passes run
+  uint32_t ct[kWsMaxK];                // final centres, empty clusters dropped (:1029-1096)
+  double means[kWsMaxK * 3];           // mean[] per cluster index (diagnostics)
+  int64_t sizes[kWsMaxK];
+  int64_t trace[(kWsMaxK - 1) * 4];    // new_index old_index |C| |new| per split
+  // phase profile (wall_clock64 ticks, 100 MHz): [0] start, [1] hash set
+  // built, [2] table sorted, [3] clustering done, [4] map done; [5] ticks in
+  // fold passes, [6] in partitions; [7] passes by kind: init | split << 16 | 2-means << 32
+  uint64_t prof[8];
+};
+struct WsMapTab {                      // device: the palette for the grid map of a larger input
+  uint32_t go, m;                      // go: wsmall_kernel left a palette (0: nothing to map)
+  uint32_t pal[kWsMapMax];             // sorted by R+G+B (sort_color)
+  uint16_t lut[766];                   // lut_init
+};
+struct WSmallArgs {
+  const uint32_t* px;                  // n pixels (device)
+  uint32_t* out;                       // mapped colours, or nullptr (cluster only)
+  WSmallResult* res;                   // device view of the host-coherent result
+  WsMapTab* maptab;                    // device scratch (the map of inputs above 16384 pixels)
+  double norm;                         // calc_color_table's norm_factor (:184)
+  uint32_t n;
+  int32_t k, max_iters, fixed_point;
+};
+hipError_t launch_wsmall(const WSmallArgs& a, hipStream_t stream);   // (the launch's error, if any)
+
 }  // namespace dq

@@ -242,6 +242,19 @@ int dq_hip_last_loop_rounds(int device);
  * dq_hip_last_persist_rounds: how many rounds of the last run did so. */
 void dq_hip_set_persist(int device, int on);
 int dq_hip_last_persist_rounds(int device);
+/* The weighted path (allPixelsUnique = 0) of a small input -- at most 131071
+ * pixels, 6144 colours, 64 clusters, no cut_bits / decimation: a superpixel
+ * region of the app, ClusteringSegmentation.cpp:1779-1803 -- in ONE launch of
+ * one workgroup (DESIGN.md 5d'; default on, DQ_HIP_TUNE=wsmall=0 turns the
+ * default off): colour table, the splits in the reference's order with its
+ * sequential folds, dedup and, for at most 16 deduped colours, the map.
+ * Outputs are identical either way. */
+void dq_hip_set_wsmall(int device, int on);
+/* Phase profile of the last weighted call if it took the one-launch path
+ * (0 values otherwise): wall_clock64 ticks (100 MHz) at its start, hash set,
+ * sorted colour table, clustering, map; ticks in fold passes and partitions;
+ * passes by kind (init | split << 16 | 2-means << 32).  Returns the count. */
+int dq_hip_last_wsmall_profile(int device, uint64_t* out, int nout);
 
 /* Engine lanes a batch of frames is split over (each: own stream, own host
  * thread; DQ_HIP_LANES; default 4 when GPU_MAX_HW_QUEUES >= 6 at the first

@@ -149,7 +149,16 @@ def test_map_colors_mps(gpu):
     assert not bad, bad
 
 
-def test_weighted_path(gpu):
+@pytest.fixture(params=[True, False], ids=["wsmall", "rounds"])
+def wpath(gpu, request):
+    """Both weighted paths: small inputs in one launch (dq_wsmall.hip) and the
+    multi-kernel rounds (dq_weighted.hip) they would otherwise take."""
+    gpu.set_wsmall(request.param)
+    yield request.param
+    gpu.set_wsmall(True)
+
+
+def test_weighted_path(gpu, wpath):
     """allPixelsUnique=0 (every live app call site, ClusteringSegmentation.cpp:1803):
     the reference's weighted outputs -- calc_color_table order + ordered FP64
     folds -- on the synthetic fixtures and on the 352 duplicate-heavy /
@@ -172,7 +181,7 @@ def test_weighted_path(gpu):
     assert not bad, bad
 
 
-def test_weighted_trace_and_centroids(gpu):
+def test_weighted_trace_and_centroids(gpu, wpath):
     """The weighted path's split trace (sizes in unique colours) and centroid
     doubles against the reference's (instrumented build, weighted2.npz)."""
     import torch
@@ -193,7 +202,7 @@ def test_weighted_trace_and_centroids(gpu):
         _check_centroids(gpu, s["k"], arrs["means_%d" % i])
 
 
-def test_weighted_vs_oracle_sweep(gpu):
+def test_weighted_vs_oracle_sweep(gpu, wpath):
     """Fresh seeded duplicate-heavy inputs against the oracle's weighted restatement."""
     rng = np.random.default_rng(777)
     for trial in range(40):

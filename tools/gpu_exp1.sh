@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 6 experiment: partition / copy rates at frame-sized (Infinity-Cache
 # resident) inputs, and the 8 x 4K share with each lane's frames run one at
-# a time (DQ_HIP_TUNE lane_frames=1) against the default.
+# a time (DQ_HIP_TUNE lane_frames=1) against the default.  (lane_frames was a
+# key of the experiment build only, removed after it measured 1.41 vs 1.13 ms.)
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/exp1
