@@ -1817,7 +1817,8 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     const size_t o_fold = o_tpre + al((size_t)nt * 8 * sizeof(double));
     const size_t o_quick = o_fold + al((size_t)nt * kWCh * sizeof(WFold));
     const size_t o_pbase = o_quick + al((size_t)nt * kWCh * sizeof(WQuick));
-    const size_t o_res = o_pbase + al((size_t)nt * 2 * sizeof(uint32_t));
+    const size_t o_gen = o_pbase + al((size_t)nt * 2 * sizeof(uint32_t));
+    const size_t o_res = o_gen + al((size_t)nt * sizeof(uint32_t));
     const size_t o_act = o_res + al((size_t)nn * sizeof(NodeResult));
     const size_t bytes = o_act + 256;
     if (bytes > cap_wnodes_) {
@@ -1885,6 +1886,7 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     wa.fold = reinterpret_cast<WFold*>(db + o_fold);
     wa.quick = reinterpret_cast<WQuick*>(db + o_quick);
     wa.pbase = reinterpret_cast<uint32_t*>(db + o_pbase);
+    wa.gen = reinterpret_cast<uint32_t*>(db + o_gen);
     wa.res = reinterpret_cast<NodeResult*>(db + o_res);
     wa.active = reinterpret_cast<uint32_t*>(db + o_act);
     wa.nn = nn;

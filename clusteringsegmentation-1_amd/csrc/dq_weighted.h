@@ -97,6 +97,7 @@ struct WArgs {
   WQuick* quick;              // [tile][kWCh]
   uint32_t* pbase;            // [tile][2] partition bases (old, new) inside the node
   uint32_t* active;           // device word: nodes not final after the pass
+  uint32_t* gen;              // [tile] folds whose description needs the general classify (bit ch)
   NodeResult* res;            // [node]
   int32_t nn, ntiles, max_iters, fixed_point, it, pad;
 };

@@ -240,7 +240,92 @@ __device__ __forceinline__ int w_binade(double v) {
   return (int)((__double_as_longlong(v) >> 52) & 0x7FF) - 1023;
 }
 
-// Pass step 3: per tile and fold, each summand's class (zero, run member of
+// Pass step 3a: one workgroup per tile, the folds whose tile lies in one
+// binade.  With the tile's prefix estimate P0 and its sum estimate Tt, every
+// summand's interval lies inside [P0 (1 - 2^-20), (P0 + Tt) (1 + 2^-20)] (the
+// prefixes grow from P0, the summands are >= 0, and the estimates' errors are
+// far inside the margin), so when that interval is in one binade e every
+// nonzero summand of the fold is a run member of e: the description is one
+// segment (e, sum of RNE(x / 2^(e-52))) -- no scans, no slots, and the order
+// of the summands does not matter (an integer sum).  Nearly every tile past a
+// node's first few is one-binade in all seven folds: the tile is loaded ONCE,
+// coalesced, for all of them (the round-5 form loaded it once per fold, seven
+// workgroups per tile).  A tie anywhere in a fold's tile (x / u exactly
+// halfway) and the folds that are not one-binade go to wk_classify (gen).
+__global__ __launch_bounds__(kWThreads) void wk_classify_fast(WArgs a, int pass) {
+  const uint32_t ti = blockIdx.x;
+  const WTile t = a.tiles[ti];
+  const WState& st = a.nodes[t.node];
+  if (st.done) return;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int kW = kWThreads / 64;
+  __shared__ long long s_fm[kW][kWCh];
+  __shared__ uint32_t s_tie[kW];
+  uint32_t fast = 0;   // (block-uniform: tile values)
+  int el[kWCh];
+#pragma unroll
+  for (int ch = 0; ch < kWCh; ++ch) {
+    const double P0 = a.tpre[(size_t)ti * 8 + ch], Tt = a.tsum[(size_t)ti * 8 + ch];
+    const double lo = P0 * (1.0 - kWMargin), hi = (P0 + Tt) * (1.0 + kWMargin);
+    el[ch] = lo > 0.0 ? w_binade(lo) : 0;
+    if (lo > 0.0 && el[ch] == w_binade(hi)) fast |= 1u << ch;
+  }
+  uint32_t tie = 0;
+  if (fast) {
+    WPts qc;
+    w_load_co(a, st, t, pass, qc);
+#pragma unroll
+    for (int ch = 0; ch < kWCh; ++ch) {
+      if (!((fast >> ch) & 1u)) continue;
+      long long mm = 0;
+      bool tch = false;
+#pragma unroll
+      for (int k = 0; k < kWPer; ++k) {
+        const double tt = ldexp(w_x(qc, k, ch), 52 - el[ch]);   // exact (x < 2^(el+1)); 0 for a non-summand
+        const double fl = floor(tt), fr = tt - fl;
+        tch |= fr == 0.5;
+        mm += (long long)fl + (fr > 0.5 ? 1 : 0);
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mm += __shfl_xor(mm, o, 64);
+      if (lane == 0) s_fm[wv][ch] = mm;
+      if (__ballot(tch)) tie |= 1u << ch;
+    }
+  }
+  if (lane == 0) s_tie[wv] = tie;
+  __syncthreads();
+  uint32_t ties = 0;
+#pragma unroll
+  for (int w = 0; w < kW; ++w) ties |= s_tie[w];
+  const uint32_t done = fast & ~ties;
+  if (threadIdx.x < (uint32_t)kWCh && ((done >> threadIdx.x) & 1u)) {
+    const int ch = (int)threadIdx.x;
+    long long M = 0;
+    for (int w = 0; w < kW; ++w) M += s_fm[w][ch];
+    WFold& f = a.fold[(size_t)ti * kWCh + ch];
+    WQuick& qk = a.quick[(size_t)ti * kWCh + ch];
+    if (M == 0) {
+      f.nseg = 0;
+      qk.e = kWNone;
+      qk.m = 0;
+    } else {
+      WSegment g;
+      g.e = el[ch];
+      g.pad = 0;
+      g.v = (int64_t)M;
+      f.seg[0] = g;
+      f.nseg = 1;
+      qk.e = el[ch];
+      qk.m = (int64_t)M;
+    }
+  }
+  if (threadIdx.x == 0) {
+    a.gen[ti] = ~done & ((1u << kWCh) - 1u);
+    a.quick[(size_t)ti * kWCh].cnt = (uint32_t)a.tsum[(size_t)ti * 8 + 7];
+  }
+}
+
+// Pass step 3b: per tile and fold (the folds wk_classify_fast left), each summand's class (zero, run member of
 // binade e with integer m = RNE(x / 2^(e-52)), or special) from the prefix
 // estimate, then the tile's description: its segments in sequence order --
 // every special, and every maximal stretch of run members with m != 0 and
@@ -265,7 +350,7 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
   const WTile t = a.tiles[ti];
   const WState& st = a.nodes[t.node];
   if (st.done) return;
-  if (ch == 0 && threadIdx.x == 0) a.quick[(size_t)ti * kWCh].cnt = (uint32_t)a.tsum[(size_t)ti * 8 + 7];
+  if (!((a.gen[ti] >> ch) & 1u)) return;   // described by wk_classify_fast
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   constexpr int kW = kWThreads / 64;
   __shared__ double s_wt[kW];
@@ -273,61 +358,6 @@ __global__ __launch_bounds__(kWThreads) void wk_classify(WArgs a, int pass) {
   __shared__ int s_wk[kW][3];              // per wave: first / last member key (-1: none), starts
   __shared__ unsigned long long s_m[kWSeg];
   __shared__ int s_e[kWSeg];
-  __shared__ long long s_fm[kW];
-  // One-binade tile (nearly every tile past a node's first few): with the
-  // tile's prefix estimate P0 and its sum estimate Tt, every summand's
-  // interval lies inside [P0 (1 - 2^-20), (P0 + Tt) (1 + 2^-20)] (the
-  // prefixes grow from P0, the summands are >= 0, and the estimates' errors
-  // are far inside the margin), so when that interval is in one binade e
-  // every nonzero summand is a run member of e: the description is one
-  // segment (e, sum of RNE(x / 2^(e-52))) -- no scans, no slots, and the
-  // order of the summands does not matter (an integer sum): the tile is
-  // loaded coalesced.  A tie anywhere in the tile (x / u exactly halfway)
-  // takes the general path.
-  {
-    const double P0 = a.tpre[(size_t)ti * 8 + ch], Tt = a.tsum[(size_t)ti * 8 + ch];
-    const double lo = P0 * (1.0 - kWMargin), hi = (P0 + Tt) * (1.0 + kWMargin);
-    const int el = lo > 0.0 ? w_binade(lo) : 0;
-    if (lo > 0.0 && el == w_binade(hi)) {   // (block-uniform: tile values)
-      WPts qc;
-      w_load_co(a, st, t, pass, qc);
-      long long mm = 0;
-      int tie = 0;
-#pragma unroll
-      for (int k = 0; k < kWPer; ++k) {
-        const double tt = ldexp(w_x(qc, k, ch), 52 - el);   // exact (x < 2^(el+1)); 0 for a non-summand
-        const double fl = floor(tt), fr = tt - fl;
-        tie |= fr == 0.5;
-        mm += (long long)fl + (fr > 0.5 ? 1 : 0);
-      }
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) mm += __shfl_xor(mm, o, 64);
-      if (lane == 0) s_fm[wv] = mm;
-      if (!__syncthreads_or(tie)) {
-        long long M = 0;
-        for (int w = 0; w < kW; ++w) M += s_fm[w];
-        if (threadIdx.x == 0) {
-          WFold& f = a.fold[(size_t)ti * kWCh + ch];
-          WQuick& qk = a.quick[(size_t)ti * kWCh + ch];
-          if (M == 0) {
-            f.nseg = 0;
-            qk.e = kWNone;
-            qk.m = 0;
-          } else {
-            WSegment g;
-            g.e = el;
-            g.pad = 0;
-            g.v = (int64_t)M;
-            f.seg[0] = g;
-            f.nseg = 1;
-            qk.e = el;
-            qk.m = (int64_t)M;
-          }
-        }
-        return;
-      }
-    }
-  }
   WPts q;
   w_load(a, st, t, pass, q);
   {
@@ -996,6 +1026,7 @@ void launch_wpass(int pass, const WArgs& a, hipStream_t stream) {
   if (a.ntiles <= 0 || a.nn <= 0) return;
   wk_tilesum<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_prefix<<<dim3(a.nn), dim3(64 * kWCh), 0, stream>>>(a);
+  wk_classify_fast<<<dim3(a.ntiles), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_classify<<<dim3(((a.ntiles + 7) / 8) * 8 * kWCh), dim3(kWThreads), 0, stream>>>(a, pass);
   wk_chain<<<dim3(a.nn), dim3(kWChainThreads), 0, stream>>>(a, pass);
 }
