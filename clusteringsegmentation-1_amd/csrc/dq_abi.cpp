@@ -1070,11 +1070,13 @@ void cut_bits(const uint32_t* inPixels, const uint32_t numPixels, uint32_t* outP
   }
 }
 
-// DivQuantMapColors.cpp:82-203: unique colours with weights count*norm in the
-// reference's output order -- hash buckets ascending (HASH(R,G,B) =
+// DivQuantMapColors.cpp:82-203 on the device (dq_weighted.hip's colour
+// table, the weighted path's own): unique colours with weights count*norm in
+// the reference's output order -- hash buckets ascending (HASH(R,G,B) =
 // (R*33023 + G*30013 + B*27011) & 0x7fffffff) % 20023), and inside a bucket
-// the most recently first-seen colour first (the chains are prepended).
-// The pixel index quirk inPixels[ic + ir*numRows] is kept (:124).
+// the most recently first-seen colour first (the chains are prepended).  The
+// pixel index quirk inPixels[ic + ir*numRows] is kept (:124); numPixels is
+// not read, as in the reference.
 double* calc_color_table(const uint32_t* inPixels, const uint32_t numPixels, uint32_t* outPixels,
                          const uint32_t numRows, const uint32_t numCols, const int dec_factor,
                          int* num_colors) {
@@ -1083,36 +1085,11 @@ double* calc_color_table(const uint32_t* inPixels, const uint32_t numPixels, uin
     std::fprintf(stderr, "Decimation factor ( %d ) should be positive !\n", dec_factor);
     return NULL;
   }
-  struct Ent { uint32_t color; uint32_t first; uint32_t count; uint32_t hash; };
-  std::unordered_map<uint32_t, uint32_t> where;
-  std::vector<Ent> ents;
-  for (uint32_t ir = 0; ir < numRows; ir += dec_factor) {
-    for (uint32_t ic = 0; ic < numCols; ic += dec_factor) {
-      const uint32_t p = inPixels[ic + (ir * numRows)] & 0xFFFFFF;
-      auto it = where.find(p);
-      if (it != where.end()) {
-        ents[it->second].count++;
-      } else {
-        const long R = (p >> 16) & 0xFF, G = (p >> 8) & 0xFF, B = p & 0xFF;
-        const uint32_t h = (uint32_t)(((R * 33023 + G * 30013 + B * 27011) & 0x7fffffff) % 20023);
-        where.emplace(p, (uint32_t)ents.size());
-        ents.push_back({p, (uint32_t)ents.size(), 1u, h});
-      }
-    }
-  }
-  std::vector<uint32_t> order(ents.size());
-  for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
-  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-    if (ents[a].hash != ents[b].hash) return ents[a].hash < ents[b].hash;
-    return ents[a].first > ents[b].first;
-  });
-  *num_colors = (int)ents.size();
-  double* weights = new double[ents.size()];
-  const double norm = 1.0 / (ceil(numRows / (double)dec_factor) * ceil(numCols / (double)dec_factor));
-  for (size_t i = 0; i < order.size(); ++i) {
-    const Ent& en = ents[order[i]];
-    outPixels[i] = en.color;
-    weights[i] = norm * en.count;
-  }
+  const uint64_t nr = (numRows + (uint64_t)dec_factor - 1) / dec_factor;
+  const uint64_t nc = (numCols + (uint64_t)dec_factor - 1) / dec_factor;
+  double* weights = new double[std::max<uint64_t>(1, nr * nc)];
+  Engine& e = engine_for(current_device());
+  std::lock_guard<std::mutex> g(e.mutex());
+  *num_colors = (int)e.color_table(inPixels, numRows, numCols, (uint32_t)dec_factor, outPixels, weights, e.stream());
   return weights;
 }

@@ -1715,6 +1715,56 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
 }
 
 // ---------------------------------------------------------------------------
+// The colour table's scratch (dq_weighted.hip launch_color_table).
+void Engine::ensure_color_scratch(uint32_t n, hipStream_t stream) {
+  const size_t need_scratch = color_table_scratch_bytes(n);
+  if (need_scratch > cap_wscratch_) {
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (d_wscratch_) DQ_HIP(hipFree(d_wscratch_));
+    DQ_HIP(hipMalloc(&d_wscratch_, need_scratch));
+    cap_wscratch_ = need_scratch;
+  }
+}
+
+// calc_color_table for a host caller: the points staged (the reference reads
+// inPixels[ic + ir*numRows] whatever numPixels says, :124 -- the staged range
+// ends at the last index it reads), gathered when decimated or 2-D, the
+// device colour table, the records back.
+uint32_t Engine::color_table(const uint32_t* h_in, uint32_t rows, uint32_t cols, uint32_t dec, uint32_t* h_colors,
+                             double* h_weights, hipStream_t stream) {
+  DQ_HIP(hipSetDevice(device_));
+  if (!stream) stream = stream_;
+  DQ_CHECK(dec >= 1, "dec_factor >= 1");
+  if (rows == 0 || cols == 0) return 0;
+  const uint64_t nr = (rows + (uint64_t)dec - 1) / dec, nc = (cols + (uint64_t)dec - 1) / dec;
+  const uint64_t last = (nc - 1) * dec + (nr - 1) * (uint64_t)dec * rows;
+  DQ_CHECK(last < 0xFFFFFFF0ull && nr * nc <= 0xFFFFFFF0ull, "too many points");
+  const uint32_t m = (uint32_t)(nr * nc);
+  stage_in(h_in, (uint32_t)(last + 1), stream);
+  ensure_color_scratch(m, stream);
+  ensure_pixels(2 * (size_t)m + 8);
+  const uint32_t* pts = staged_in();
+  if (nr != 1 || nc != last + 1) {   // not the plain run [0, m)
+    launch_cut_gather(staged_in(), d_p1_, (uint32_t)nr, (uint32_t)nc, dec, rows, 0, 0, 0, stream);
+    pts = d_p1_;
+  }
+  uint32_t nu = 0;
+  const int rc = launch_color_table(pts, m, d_wscratch_, cap_wscratch_, reinterpret_cast<uint64_t*>(d_p0_), &nu,
+                                    stream);
+  DQ_CHECK(rc == 0, "colour table failed");
+  std::vector<uint64_t> rec(nu);
+  if (nu) DQ_HIP(hipMemcpyAsync(rec.data(), d_p0_, (size_t)nu * 8, hipMemcpyDeviceToHost, stream));
+  DQ_HIP(hipStreamSynchronize(stream));
+  // norm_factor (:184), the weight norm_factor * count (:195)
+  const double norm = 1.0 / (std::ceil((double)rows / (double)dec) * std::ceil((double)cols / (double)dec));
+  for (uint32_t i = 0; i < nu; ++i) {
+    h_colors[i] = (uint32_t)rec[i];
+    h_weights[i] = norm * (double)(uint32_t)(rec[i] >> 32);
+  }
+  return nu;
+}
+
+// ---------------------------------------------------------------------------
 // The weighted path: quant_varpart_fast's calc_color_table dedup and
 // DivQuantCluster<false,*,true> (DivQuantCluster.cpp:1133-1138, :1163-1166).
 // Rounds as run(): a round splits every node the greedy replay needs, each in
@@ -1748,14 +1798,7 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     return;
   if (!h_wactive_) DQ_HIP(hipHostMalloc((void**)&h_wactive_, 64, hipHostMallocDefault));
   ensure_round(2 * (size_t)job.k + 64, 1024, 0, 0, max_iters, stream);   // staging, results
-  // scratch: colour table, unique colours + weights, two id buffers (P0/P1)
-  const size_t need_scratch = color_table_scratch_bytes(n);
-  if (need_scratch > cap_wscratch_) {
-    DQ_HIP(hipStreamSynchronize(stream));
-    if (d_wscratch_) DQ_HIP(hipFree(d_wscratch_));
-    DQ_HIP(hipMalloc(&d_wscratch_, need_scratch));
-    cap_wscratch_ = need_scratch;
-  }
+  ensure_color_scratch(n, stream);
   // P0 / P1 hold the points' 8-B records (colour | count << 32): 2 words each
   ensure_pixels(2 * (size_t)n + 8);
   // norm_factor = 1 / (ceil(numRows / dec) * ceil(numCols / dec)) (:184)

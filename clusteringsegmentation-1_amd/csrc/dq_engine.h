@@ -160,6 +160,13 @@ class Engine {
   // (dq_weighted.hip); dedup + map as run().  last_sizes / last_trace count
   // points = unique colours, as the reference's size[].
   void run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream);
+  // calc_color_table (DivQuantMapColors.cpp:82-203) on the device for a host
+  // input: the points inPixels[ic + ir*numRows] (ir < rows, ic < cols, step
+  // dec), their unique colours and weights norm * count in the reference's
+  // order into h_colors / h_weights (room for rows * cols / dec^2 entries).
+  // Returns the number of colours.
+  uint32_t color_table(const uint32_t* h_in, uint32_t rows, uint32_t cols, uint32_t dec, uint32_t* h_colors,
+                       double* h_weights, hipStream_t stream);
 
   // map_colors_mps (DivQuantMapColors.cpp:243-539) on device buffers.
   void map(const uint32_t* d_in, uint32_t n, uint32_t* d_out,
@@ -459,7 +466,7 @@ class Engine {
   size_t cap_mapstage_ = 0;
   void ensure_map_stage(size_t nmaps);
   // weighted path buffers
-  void* d_wscratch_ = nullptr;        // colour-table scratch (sorts)
+  void* d_wscratch_ = nullptr;        // colour-table scratch (runs, group tables)
   size_t cap_wscratch_ = 0;
   void* d_wnodes_ = nullptr;          // a round's WState records, tiles, fold tables, results
   uint32_t* h_wactive_ = nullptr;     // pinned: the round's nodes not final after the split
@@ -468,6 +475,7 @@ class Engine {
   WSmallResult* d_wsres_ = nullptr;
   WsMapTab* d_wsmap_ = nullptr;       // device: its palette for the grid map
   bool run_weighted_small(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream);
+  void ensure_color_scratch(uint32_t n, hipStream_t stream);
   size_t cap_wnodes_ = 0;
 
   std::vector<Node> nodes_;

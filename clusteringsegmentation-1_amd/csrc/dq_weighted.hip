@@ -9,9 +9,9 @@
 // uniform-weight outputs differ on duplicate-heavy inputs (tests/golden/
 // weighted2.json: 55 of 352 cases), so this path reproduces the folds
 // exactly:
-//   * the colour table: radix sort of (colour, pixel index), run heads ->
-//     unique colours with counts and first occurrences, a second sort by
-//     (hash bucket, first occurrence descending) -- the order the reference's
+//   * the colour table: runs of equal pixels partitioned by hash-bucket
+//     group, one LDS hash table per group, each colour ranked inside its
+//     bucket by first occurrence descending -- the order the reference's
 //     prepended hash chains emit, weights norm * count (:184-195);
 //   * the node splits of a round, pass by pass over tiles of every node:
 //     the init folds (root), the split pass, the local 2-means passes to a
@@ -36,8 +36,7 @@
 // The result is the sequential fold's double, bit for bit.
 // MUST be compiled with -ffp-contract=off (the Makefile does).
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
+#include <algorithm>
 
 #include "dq_weighted.h"
 
@@ -46,47 +45,298 @@ namespace dq {
 namespace {
 
 // --- colour table ----------------------------------------------------------
-__global__ void ct_keys_kernel(const uint32_t* __restrict__ px, uint32_t n, uint32_t* __restrict__ key,
-                               uint32_t* __restrict__ idx) {
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-    key[i] = px[i] & 0xFFFFFFu;
-    idx[i] = i;
+// calc_color_table (DivQuantMapColors.cpp:82-203) without a sort.  Its output
+// order is the hash chains': bucket HASH(c) = ((R*33023 + G*30013 + B*27011)
+// & 0x7fffffff) % 20023 ascending (:56-62, :186-201), and inside a bucket the
+// first occurrence DESCENDING (each new colour is prepended to its chain,
+// :132-158).  So colours never need a global order, only a bucket and a rank
+// inside it:
+//   1. ct_runs<COUNT>: per block of kCtChunk consecutive pixels, the runs of
+//      equal colour (a lane's 16 consecutive pixels; a run ends at the next
+//      different pixel in the wave's 1024 or at a 256-pixel boundary), each a
+//      record (first index, length, colour), counted per bucket GROUP
+//      (kCtGB consecutive buckets) in LDS -> hist[block][group];
+//   2. ct_colscan + ct_gscan: the records' exclusive offsets, group-major;
+//   3. ct_runs<SCATTER>: the same runs scattered to their group's range;
+//   4. ct_group: one workgroup per group -- an LDS hash table of the group's
+//      colours (count = sum of lengths, first = min of firsts; a group holds
+//      at most kCtGB * 844 colours: no bucket has more than 844 of the 2^24),
+//      then per bucket each colour's rank by first occurrence descending (in
+//      sub-buckets: 16 bins of the first occurrence), and
+//      the colours as records colour | count << 32 in calc_color_table's
+//      order, at the group's offset;
+//   5. ct_gscan + ct_compact: the groups' outputs packed into rec.
+// LDS atomics only (a device-wide table of global atomics measured ~27 G
+// atomic ops/s on this part, profiles/r06_ct/atomic_bench.txt: slower than
+// the sorts it would replace).
+constexpr uint32_t kCtBuckets = 20023;
+constexpr uint32_t kCtGB = 4;                                       // buckets per group
+constexpr uint32_t kCtGroups = (kCtBuckets + kCtGB - 1) / kCtGB;    // 5006
+constexpr uint32_t kCtMaxPerGroup = kCtGB * 844;                    // colours of one group, at most
+constexpr uint32_t kCtSlots = 4096;                                 // LDS hash slots (> kCtMaxPerGroup)
+constexpr int kCtSlotShift = 20;                                    // 32 - log2(kCtSlots)
+constexpr int kCtThreads = 1024;                                    // ct_runs: 16 waves x 1024 pixels a step
+constexpr int kCtGroupThreads = 1024;
+constexpr uint32_t kCtEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kCtSub = 16;                                     // first-occurrence bins per bucket
+constexpr uint32_t kCtList = kCtMaxPerGroup + 4 * kCtGB * kCtSub;   // the firsts by sub-bucket, each padded to 4
+constexpr size_t kCtGroupLds = (size_t)kCtSlots * 12 + (size_t)kCtList * 6 + 64;
+static_assert(kCtSlots > kCtMaxPerGroup, "the group table never fills");
+
+__device__ __forceinline__ uint32_t ct_bucket(uint32_t c) {   // HASH (:56-62): the sum is < 2^31
+  const uint32_t R = (c >> 16) & 0xFFu, G = (c >> 8) & 0xFFu, B = c & 0xFFu;
+  return (R * 33023u + G * 30013u + B * 27011u) % kCtBuckets;
+}
+
+// The runs of one wave's 1024 pixels [wb, wb + 1024) of px[0..n): lane l
+// holds pixels wb + 16 l + k.  f(c, first, len) for every run head, len <= 256.
+template <typename F>
+__device__ __forceinline__ void ct_wave_runs(const uint32_t* __restrict__ px, uint32_t n, uint32_t wb, F&& f) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t p0 = wb + 16u * lane;
+  uint32_t c[16];
+  if (p0 + 16u <= n && ((uintptr_t)px & 15u) == 0) {
+    const uint4* v = reinterpret_cast<const uint4*>(px + p0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint4 x = v[j];
+      c[4 * j] = x.x & 0xFFFFFFu;
+      c[4 * j + 1] = x.y & 0xFFFFFFu;
+      c[4 * j + 2] = x.z & 0xFFFFFFu;
+      c[4 * j + 3] = x.w & 0xFFFFFFu;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c[k] = p0 + (uint32_t)k < n ? (px[p0 + k] & 0xFFFFFFu) : kCtEmpty;
+  }
+  const uint32_t prev = __shfl_up(c[15], 1, 64);
+  // brk bit k: a run starts at k, or k is past the input
+  uint32_t brk = (lane & 15u) == 0u || prev != c[0] ? 1u : 0u;
+#pragma unroll
+  for (int k = 1; k < 16; ++k) brk |= (c[k] != c[k - 1] ? 1u : 0u) << k;
+  // lane slots inside the input
+  const uint32_t valid = p0 + 16u <= n ? 0xFFFFu : (n > p0 ? (1u << (n - p0)) - 1u : 0u);
+  brk |= 0xFFFFu & ~valid;
+  // the first break of the later lanes (suffix minimum; 1024: none)
+  const uint32_t mine = brk ? 16u * lane + (uint32_t)__builtin_ctz(brk) : 1024u;
+  uint32_t nx = __shfl_down(mine, 1, 64);
+  if (lane == 63u) nx = 1024u;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_down(nx, d, 64);
+    if (lane + (uint32_t)d < 64u) nx = min(nx, u);
+  }
+  uint32_t heads = brk & valid;   // runs start inside the input only
+  while (heads) {
+    const int k = __builtin_ctz(heads);
+    heads &= heads - 1u;
+    const uint32_t later = brk >> (k + 1);
+    const uint32_t end = later ? 16u * lane + (uint32_t)k + 1u + (uint32_t)__builtin_ctz(later) : nx;
+    uint32_t ck = c[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) ck = k == j ? c[j] : ck;
+    f(ck, p0 + (uint32_t)k, end - (16u * lane + (uint32_t)k));
   }
 }
 
-__global__ void ct_heads_kernel(const uint32_t* __restrict__ skey, uint32_t n, uint32_t* __restrict__ flag) {
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
-    flag[i] = (i == 0 || skey[i] != skey[i - 1]) ? 1u : 0u;
-}
-
-// Run heads -> unique colour u: its colour, first occurrence (the sort is
-// stable, so the run's first index) and the run start; the ordering key
-// (hash << nb) | (n - 1 - first) sorts by bucket ascending, first occurrence
-// descending.
-__global__ void ct_scatter_kernel(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ sidx,
-                                  const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
-                                  uint32_t n, uint32_t* __restrict__ ucol, uint32_t* __restrict__ head,
-                                  uint32_t nb, uint64_t* __restrict__ okey) {
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-    if (!flag[i]) continue;
-    const uint32_t u = pos[i], c = skey[i];
-    const long R = (c >> 16) & 0xFF, G = (c >> 8) & 0xFF, B = c & 0xFF;
-    const uint64_t h = (uint64_t)(((R * 33023 + G * 30013 + B * 27011) & 0x7fffffff) % 20023);   // HASH, :56-62
-    ucol[u] = c;
-    head[u] = i;
-    okey[u] = (h << nb) | (uint64_t)(n - 1u - sidx[i]);   // (hash, descending index) in 15 + nb bits
+// Steps 1 and 3.  COUNT: hist[block][group] = the block's runs per group.
+// SCATTER: each run to part[gstart[group] + off[block][group] + its rank in
+// the block] as (first << 32) | (len - 1) << 24 | colour.
+template <bool COUNT>
+__global__ __launch_bounds__(kCtThreads) void ct_runs(const uint32_t* __restrict__ px, uint32_t n, uint32_t chunk,
+                                                      uint32_t* __restrict__ hist, const uint32_t* __restrict__ gstart,
+                                                      uint64_t* __restrict__ part) {
+  __shared__ uint32_t s_h[kCtGroups];
+  uint32_t* row = hist + (size_t)blockIdx.x * kCtGroups;
+  for (uint32_t g = threadIdx.x; g < kCtGroups; g += kCtThreads) s_h[g] = COUNT ? 0u : gstart[g] + row[g];
+  __syncthreads();
+  const uint32_t b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+  for (uint32_t wb = b0 + (threadIdx.x >> 6) * 1024u; wb < b1; wb += (kCtThreads / 64) * 1024u)
+    ct_wave_runs(px, b1, wb, [&](uint32_t c, uint32_t first, uint32_t len) {
+      const uint32_t g = ct_bucket(c) / kCtGB;
+      if (COUNT) {
+        atomicAdd(&s_h[g], 1u);
+      } else {
+        const uint32_t pos = atomicAdd(&s_h[g], 1u);
+        part[pos] = ((uint64_t)first << 32) | ((uint64_t)(len - 1u) << 24) | c;
+      }
+    });
+  if (COUNT) {
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < kCtGroups; g += kCtThreads) row[g] = s_h[g];
   }
 }
 
-// The points in calc_color_table's order as (colour | count << 32) records:
-// a pass reads a point's colour and its weight norm * count (:195) from its
-// own record, in node order (the partitions move records, not ids).
-__global__ void ct_records_kernel(const uint32_t* __restrict__ ucol_tmp, const uint32_t* __restrict__ head,
-                                  uint32_t nu, uint32_t n, uint64_t* __restrict__ orec) {
-  for (uint32_t u = blockIdx.x * 256u + threadIdx.x; u < nu; u += gridDim.x * 256u) {
-    const uint32_t count = (u + 1 < nu ? head[u + 1] : n) - head[u];
-    orec[u] = (uint64_t)ucol_tmp[u] | ((uint64_t)count << 32);
+// Step 2a: per group, the exclusive prefix over blocks of hist[b][g] (in
+// place) and the group's total.  64 groups per workgroup (coalesced rows),
+// 16 block ranges per group.
+__global__ __launch_bounds__(1024) void ct_colscan(uint32_t* __restrict__ hist, uint32_t nblk,
+                                                   uint32_t* __restrict__ gtot) {
+  __shared__ uint32_t s_p[16][64];
+  const uint32_t gl = threadIdx.x & 63u, part = threadIdx.x >> 6;
+  const uint32_t g = blockIdx.x * 64u + gl;
+  const uint32_t per = (nblk + 15u) / 16u, bb = part * per, be = min(nblk, bb + per);
+  uint32_t s = 0;
+  if (g < kCtGroups)
+    for (uint32_t b = bb; b < be; ++b) s += hist[(size_t)b * kCtGroups + g];
+  s_p[part][gl] = s;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+  for (uint32_t q = 0; q < 16u; ++q) {
+    if (q < part) run += s_p[q][gl];
+    tot += s_p[q][gl];
   }
+  if (g < kCtGroups) {
+    for (uint32_t b = bb; b < be; ++b) {
+      uint32_t* h = hist + (size_t)b * kCtGroups + g;
+      const uint32_t v = *h;
+      *h = run;
+      run += v;
+    }
+    if (part == 0) gtot[g] = tot;
+  }
+}
+
+// Step 2b / 5a: out[0..m] = exclusive prefix of in[0..m), out[m] = total (one
+// workgroup; m = kCtGroups).
+__global__ __launch_bounds__(1024) void ct_gscan(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint32_t m) {
+  __shared__ uint32_t s_w[16];
+  const uint32_t per = (m + 1023u) / 1024u, i0 = threadIdx.x * per, i1 = min(m, i0 + per);
+  uint32_t s = 0;
+  for (uint32_t i = i0; i < i1; ++i) s += in[i];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint32_t inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += u;
+  }
+  if (lane == 63u) s_w[wv] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t w = 0; w < wv; ++w) base += s_w[w];
+  uint32_t run = base + inc - s;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t v = in[i];
+    out[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 1023u) out[m] = base + inc;
+}
+
+// Step 4: one workgroup per group.  Reads the group's runs part[gstart[g] ..
+// gstart[g + 1]) and writes its colours in calc_color_table's order to the
+// same range's front (every read is done before the first write), ucnt[g]
+// their number.
+__global__ __launch_bounds__(kCtGroupThreads) void ct_group(uint64_t* __restrict__ part,
+                                                            const uint32_t* __restrict__ gstart,
+                                                            uint32_t* __restrict__ ucnt, uint32_t binshift) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t ct_lds[];
+  uint32_t* key = reinterpret_cast<uint32_t*>(ct_lds);
+  uint32_t* cnt = key + kCtSlots;
+  uint32_t* fst = cnt + kCtSlots;
+  uint32_t* lf = fst + kCtSlots;                          // [kCtList] firsts, by bucket (16-B aligned runs)
+  uint16_t* ls = reinterpret_cast<uint16_t*>(lf + kCtList); // [kCtList] their slots
+  __shared__ uint32_t s_bc[64], s_bs[65], s_b4[65], s_cur[64];
+  const uint32_t g = blockIdx.x, t = threadIdx.x;
+  const uint32_t r0 = gstart[g], r1 = gstart[g + 1];
+  // the first kCtPre runs per thread loaded before the table is cleared (the
+  // loads' latency under the clear)
+  constexpr int kCtPre = 2;   // (pre[0], pre[1] below)
+  uint64_t pre[kCtPre];
+#pragma unroll
+  for (int q = 0; q < kCtPre; ++q) {
+    const uint32_t i = r0 + t + (uint32_t)q * kCtGroupThreads;
+    pre[q] = i < r1 ? part[i] : 0ull;
+  }
+  for (uint32_t s = t; s < kCtSlots; s += kCtGroupThreads) {
+    key[s] = kCtEmpty;
+    cnt[s] = 0u;
+    fst[s] = 0xFFFFFFFFu;
+  }
+  if (t < 64u) s_bc[t] = s_cur[t] = 0u;
+  __syncthreads();
+  for (uint32_t i = r0 + t, q = 0; i < r1; i += kCtGroupThreads, ++q) {
+    const uint64_t r = q == 0 ? pre[0] : (q == 1 ? pre[1] : part[i]);
+    const uint32_t c = (uint32_t)r & 0xFFFFFFu, len = (((uint32_t)r >> 24) & 0xFFu) + 1u, first = (uint32_t)(r >> 32);
+    uint32_t s = (c * 2654435761u) >> kCtSlotShift;
+    for (;;) {
+      const uint32_t k = atomicCAS(&key[s], kCtEmpty, c);
+      if (k == kCtEmpty || k == c) break;
+      s = (s + 1u) & (kCtSlots - 1u);
+    }
+    atomicAdd(&cnt[s], len);
+    atomicMin(&fst[s], first);
+  }
+  __syncthreads();
+  // sub-buckets: (bucket ascending, first-occurrence bin descending), the
+  // bins monotone in the first occurrence (its top 4 bits below n), so
+  // ranking by first occurrence inside a sub-bucket is ranking inside the
+  // bucket at 1/16 of the comparisons
+  const uint32_t bb = g * kCtGB;
+  auto sub = [&](uint32_t s) { return (ct_bucket(key[s]) - bb) * kCtSub + (kCtSub - 1u) - (fst[s] >> binshift); };
+  for (uint32_t s = t; s < kCtSlots; s += kCtGroupThreads)
+    if (key[s] != kCtEmpty) atomicAdd(&s_bc[sub(s)], 1u);
+  __syncthreads();
+  if (t < 64u) {   // s_bs: the sub-buckets' output offsets; s_b4: their lists' (padded to 4)
+    static_assert(kCtGB * kCtSub == 64, "one wave scans the sub-buckets");
+    const uint32_t c = s_bc[t], c4 = (c + 3u) & ~3u;
+    uint32_t inc = c, inc4 = c4;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64), u4 = __shfl_up(inc4, o, 64);
+      if (t >= (uint32_t)o) {
+        inc += u;
+        inc4 += u4;
+      }
+    }
+    s_bs[t] = inc - c;
+    s_b4[t] = inc4 - c4;
+    if (t == 63u) {
+      s_bs[64] = inc;
+      s_b4[64] = inc4;
+    }
+  }
+  __syncthreads();
+  for (uint32_t x = t; x < s_b4[64]; x += kCtGroupThreads) {   // (pads: first 0 is never > f)
+    lf[x] = 0u;
+    ls[x] = 0xFFFFu;
+  }
+  __syncthreads();
+  for (uint32_t s = t; s < kCtSlots; s += kCtGroupThreads)
+    if (key[s] != kCtEmpty) {
+      const uint32_t j = sub(s);
+      const uint32_t x = s_b4[j] + atomicAdd(&s_cur[j], 1u);
+      lf[x] = fst[s];
+      ls[x] = (uint16_t)s;
+    }
+  __syncthreads();
+  // rank inside the sub-bucket: colours first seen later come first
+  // (:132-158); 4 firsts a read
+  const uint32_t tot4 = s_b4[64];
+  const uint4* l4 = reinterpret_cast<const uint4*>(lf);
+  for (uint32_t x = t; x < tot4; x += kCtGroupThreads) {
+    const uint32_t s = ls[x];
+    if (s == 0xFFFFu) continue;   // a pad
+    const uint32_t j = sub(s), f = lf[x];
+    uint32_t rank = 0;
+#pragma unroll 2
+    for (uint32_t y = s_b4[j] / 4u; y < s_b4[j + 1] / 4u; ++y) {
+      const uint4 v = l4[y];
+      rank += (v.x > f ? 1u : 0u) + (v.y > f ? 1u : 0u) + (v.z > f ? 1u : 0u) + (v.w > f ? 1u : 0u);
+    }
+    part[r0 + s_bs[j] + rank] = (uint64_t)key[s] | ((uint64_t)cnt[s] << 32);
+  }
+  const uint32_t tot = s_bs[64];
+  if (t == 0) ucnt[g] = tot;
+}
+
+// Step 5b: group g's colours to rec[uoff[g] ..).
+__global__ __launch_bounds__(256) void ct_compact(const uint64_t* __restrict__ part, const uint32_t* __restrict__ gstart,
+                                                  const uint32_t* __restrict__ uoff, uint64_t* __restrict__ rec) {
+  const uint32_t g = blockIdx.x, o = uoff[g], m = uoff[g + 1] - o;
+  const uint64_t* src = part + gstart[g];
+  for (uint32_t i = threadIdx.x; i < m; i += 256u) rec[o + i] = src[i];
 }
 
 
@@ -926,74 +1176,53 @@ static inline uint32_t grid_for(uint32_t n) {
   return g == 0 ? 1u : (g > 65535u ? 65535u : g);
 }
 
-// rocPRIM's device-wide radix sort (stable, LSD) and exclusive scan: the
-// temporary storage each needs for n items.
-// The second sort's key: the colour's hash (15 bits, < 20023) above the
-// point's index reversed in nb bits, nb = the bits of n - 1 (fewer radix
-// passes than a 32-bit field for n < 2^25).
-static uint32_t index_bits(uint32_t n) {
-  uint32_t nb = 1;
-  while (nb < 32 && ((n - 1u) >> nb) != 0) ++nb;
-  return nb;
-}
-
-static void temp_sizes(uint32_t n, size_t* sort1, size_t* sort2, size_t* scan) {
-  (void)rocprim::radix_sort_pairs(nullptr, *sort1, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 24);
-  (void)rocprim::radix_sort_pairs(nullptr, *sort2, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                  (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)n, 0, 15 + index_bits(n));
-  (void)rocprim::exclusive_scan(nullptr, *scan, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
-                                rocprim::plus<uint32_t>());
+// The colour table's scratch: the runs (at most one per pixel), hist / off
+// [blocks][groups], the groups' totals, offsets and colour counts.
+static uint32_t ct_chunk(uint32_t n) {   // pixels per ct_runs block: at most kCtMaxBlocks blocks
+  constexpr uint32_t kCtMaxBlocks = 256, kStep = (kCtThreads / 64) * 1024u;
+  const uint64_t per = ((uint64_t)n + kCtMaxBlocks - 1) / kCtMaxBlocks;
+  return (uint32_t)std::max<uint64_t>(kStep, (per + kStep - 1) / kStep * kStep);
 }
 
 size_t color_table_scratch_bytes(uint32_t n) {
-  size_t sort1 = 0, sort2 = 0, scan = 0;
-  temp_sizes(n, &sort1, &sort2, &scan);
-  const size_t tmp = std::max(sort1, std::max(sort2, scan));
-  // key, idx, skey, sidx, flag, pos, ucol_tmp, head (u32) + okey, sokey, orec (u64)
-  return ((tmp + 255) & ~(size_t)255) + (size_t)n * (8 * 4 + 3 * 8) + 16 * 256;
+  const uint32_t nblk = (uint32_t)(((uint64_t)n + ct_chunk(n) - 1) / ct_chunk(n));
+  return (((size_t)n * 8 + 255) & ~(size_t)255) + (((size_t)nblk * kCtGroups * 4 + 255) & ~(size_t)255) +
+         4 * ((((size_t)kCtGroups + 1) * 4 + 255) & ~(size_t)255);
 }
 
 int launch_color_table(const uint32_t* px, uint32_t n, void* scratch, size_t scratch_bytes, uint64_t* rec,
                        uint32_t* h_nu, hipStream_t stream) {
-  size_t sort1 = 0, sort2 = 0, scan = 0;
-  temp_sizes(n, &sort1, &sort2, &scan);
-  size_t tmp = std::max(sort1, std::max(sort2, scan));
-  tmp = (tmp + 255) & ~(size_t)255;
+  if (n == 0) {
+    *h_nu = 0;
+    return 0;
+  }
   if (scratch_bytes < color_table_scratch_bytes(n)) return -1;
+  if (hipFuncSetAttribute((const void*)ct_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCtGroupLds) !=
+      hipSuccess)
+    return -2;
+  const uint32_t chunk = ct_chunk(n), nblk = (uint32_t)(((uint64_t)n + chunk - 1) / chunk);
   char* p = static_cast<char*>(scratch);
-  void* temp = p;
-  p += tmp;
-  auto take32 = [&]() { uint32_t* q = reinterpret_cast<uint32_t*>(p); p += ((size_t)n * 4 + 255) & ~(size_t)255; return q; };
-  auto take64 = [&]() { uint64_t* q = reinterpret_cast<uint64_t*>(p); p += ((size_t)n * 8 + 255) & ~(size_t)255; return q; };
-  uint32_t *key = take32(), *idx = take32(), *skey = take32(), *sidx = take32(), *flag = take32(), *pos = take32();
-  uint32_t *ucol_tmp = take32(), *head = take32();
-  uint64_t *okey = take64(), *sokey = take64(), *orec = take64();
-  const dim3 g(grid_for(n)), b(256);
-  ct_keys_kernel<<<g, b, 0, stream>>>(px, n, key, idx);
-  size_t t1 = sort1;
-  if (rocprim::radix_sort_pairs(temp, t1, key, skey, idx, sidx, (size_t)n, 0, 24, stream) != hipSuccess)
-    return -2;
-  ct_heads_kernel<<<g, b, 0, stream>>>(skey, n, flag);
-  size_t t3 = scan;
-  if (rocprim::exclusive_scan(temp, t3, flag, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), stream) != hipSuccess)
-    return -2;
-  // U = pos[n-1] + flag[n-1]
-  uint32_t last[2];
-  if (hipMemcpyAsync(&last[0], pos + n - 1, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-      hipMemcpyAsync(&last[1], flag + n - 1, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+  auto take = [&](size_t bytes) { char* q = p; p += (bytes + 255) & ~(size_t)255; return q; };
+  uint64_t* part = reinterpret_cast<uint64_t*>(take((size_t)n * 8));
+  uint32_t* hist = reinterpret_cast<uint32_t*>(take((size_t)nblk * kCtGroups * 4));
+  uint32_t* gtot = reinterpret_cast<uint32_t*>(take(((size_t)kCtGroups + 1) * 4));
+  uint32_t* gstart = reinterpret_cast<uint32_t*>(take(((size_t)kCtGroups + 1) * 4));
+  uint32_t* ucnt = reinterpret_cast<uint32_t*>(take(((size_t)kCtGroups + 1) * 4));
+  uint32_t* uoff = reinterpret_cast<uint32_t*>(take(((size_t)kCtGroups + 1) * 4));
+  ct_runs<true><<<dim3(nblk), dim3(kCtThreads), 0, stream>>>(px, n, chunk, hist, nullptr, nullptr);
+  ct_colscan<<<dim3((kCtGroups + 63) / 64), dim3(1024), 0, stream>>>(hist, nblk, gtot);
+  ct_gscan<<<dim3(1), dim3(1024), 0, stream>>>(gtot, gstart, kCtGroups);
+  ct_runs<false><<<dim3(nblk), dim3(kCtThreads), 0, stream>>>(px, n, chunk, hist, gstart, part);
+  uint32_t nb = 1;   // bits of n - 1: first >> (nb - 4) is a 4-bit bin, monotone in first
+  while (nb < 32 && ((n - 1u) >> nb) != 0) ++nb;
+  const uint32_t binshift = nb > 4 ? nb - 4 : 0;
+  ct_group<<<dim3(kCtGroups), dim3(kCtGroupThreads), kCtGroupLds, stream>>>(part, gstart, ucnt, binshift);
+  ct_gscan<<<dim3(1), dim3(1024), 0, stream>>>(ucnt, uoff, kCtGroups);
+  ct_compact<<<dim3(kCtGroups), dim3(256), 0, stream>>>(part, gstart, uoff, rec);
+  if (hipGetLastError() != hipSuccess) return -2;
+  if (hipMemcpyAsync(h_nu, uoff + kCtGroups, 4, hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return -2;
-  const uint32_t nu = last[0] + last[1];
-  const uint32_t nb = index_bits(n);
-  ct_scatter_kernel<<<g, b, 0, stream>>>(skey, sidx, flag, pos, n, ucol_tmp, head, nb, okey);
-  // The records are built in unique-colour order (coalesced) and sorted as
-  // 8-byte payloads straight into rec: no gather after the sort.
-  ct_records_kernel<<<dim3(grid_for(nu)), b, 0, stream>>>(ucol_tmp, head, nu, n, orec);
-  size_t t2 = sort2;
-  if (rocprim::radix_sort_pairs(temp, t2, okey, sokey, orec, rec, (size_t)nu, 0, 15 + nb, stream) != hipSuccess)
-    return -2;
-  *h_nu = nu;
   return 0;
 }
 

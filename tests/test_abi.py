@@ -101,8 +101,10 @@ def test_cut_bits(lib):
         assert "%016x" % fx.fnv(out) == c["out_fnv"], c
 
 
+@pytest.mark.gpu
 def test_calc_color_table(lib):
-    """Unique colours in the reference's hash-bucket order with count/N weights."""
+    """Unique colours in the reference's hash-bucket order with count/N weights
+    (the device colour table behind the reference's host signature)."""
     cct = _cpp(lib, "_Z16calc_color_tablePKjjPjjjiPi", ctypes.POINTER(ctypes.c_double),
                [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                 ctypes.c_int, ctypes.POINTER(ctypes.c_int)])
