@@ -1796,7 +1796,6 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
   // in one launch; more colours than it holds -> the rounds below
   if (wsmall_ && !gather && n <= kWsMaxN && job.k <= kWsMaxK && run_weighted_small(job, max_iters, dedup_map, stream))
     return;
-  if (!h_wactive_) DQ_HIP(hipHostMalloc((void**)&h_wactive_, 64, hipHostMallocDefault));
   ensure_round(2 * (size_t)job.k + 64, 1024, 0, 0, max_iters, stream);   // staging, results
   ensure_color_scratch(n, stream);
   // P0 / P1 hold the points' 8-B records (colour | count << 32): 2 words each
@@ -1920,6 +1919,18 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     launch_upload(db, d_stage_view_, up_bytes, stream);
     DQ_HIP(hipEventRecord(stage_ev_, stream));
     stage_pending_ = true;
+    // the round's results and its "still active" word in host-coherent memory
+    // (written by the kernels; read by the host after a stream sync -- no
+    // copies; the stream is idle here: the previous round ended with a sync)
+    const size_t wres_bytes = 64 + (size_t)nn * sizeof(NodeResult);
+    if (wres_bytes > cap_wres_) {
+      if (h_wres_) DQ_HIP(hipHostFree(h_wres_));
+      cap_wres_ = std::max<size_t>(wres_bytes, 64 + 256 * sizeof(NodeResult));
+      DQ_HIP(hipHostMalloc((void**)&h_wres_, cap_wres_, hipHostMallocCoherent | hipHostMallocMapped));
+      DQ_HIP(hipHostGetDevicePointer((void**)&d_wres_view_, h_wres_, 0));
+    }
+    volatile uint32_t* h_active = reinterpret_cast<volatile uint32_t*>(h_wres_);
+    *h_active = 0u;
     WArgs wa;
     wa.nodes = reinterpret_cast<WState*>(db);
     wa.tiles = reinterpret_cast<const WTile*>(db + o_tiles);
@@ -1930,8 +1941,8 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     wa.quick = reinterpret_cast<WQuick*>(db + o_quick);
     wa.pbase = reinterpret_cast<uint32_t*>(db + o_pbase);
     wa.gen = reinterpret_cast<uint32_t*>(db + o_gen);
-    wa.res = reinterpret_cast<NodeResult*>(db + o_res);
-    wa.active = reinterpret_cast<uint32_t*>(db + o_act);
+    wa.res = reinterpret_cast<NodeResult*>(d_wres_view_ + 64);
+    wa.active = reinterpret_cast<uint32_t*>(d_wres_view_);
     wa.nn = nn;
     wa.ntiles = nt;
     wa.max_iters = max_iters;
@@ -1939,21 +1950,19 @@ void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStrea
     wa.it = 0;
     wa.pad = 0;
     if (has_root) launch_wpass(WP_INIT, wa, stream);   // (a round holding the root holds only it)
-    DQ_HIP(hipMemsetAsync(wa.active, 0, 4, stream));
     launch_wpass(WP_SPLIT, wa, stream);
     // 2-means passes only when some split is not proven final at the split
-    DQ_HIP(hipMemcpyAsync(h_wactive_, wa.active, 4, hipMemcpyDeviceToHost, stream));
     DQ_HIP(hipStreamSynchronize(stream));
-    if (*h_wactive_ != 0) {
+    if (*h_active != 0) {
       for (int it = 0; it < max_iters; ++it) {
         wa.it = it;
         launch_wpass(WP_KM, wa, stream);
       }
     }
     launch_wfinish(wa, stream);
-    res.resize(nn);
-    DQ_HIP(hipMemcpyAsync(res.data(), wa.res, (size_t)nn * sizeof(NodeResult), hipMemcpyDeviceToHost, stream));
     DQ_HIP(hipStreamSynchronize(stream));
+    res.resize(nn);
+    std::memcpy(res.data(), h_wres_ + 64, (size_t)nn * sizeof(NodeResult));
     last_rounds++;
     for (int a = 0; a < nn; ++a) {
       const int id = active[a];

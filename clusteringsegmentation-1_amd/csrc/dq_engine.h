@@ -469,7 +469,9 @@ class Engine {
   void* d_wscratch_ = nullptr;        // colour-table scratch (runs, group tables)
   size_t cap_wscratch_ = 0;
   void* d_wnodes_ = nullptr;          // a round's WState records, tiles, fold tables, results
-  uint32_t* h_wactive_ = nullptr;     // pinned: the round's nodes not final after the split
+  char* h_wres_ = nullptr;            // host-coherent: a weighted round's "still active" word, then its results
+  char* d_wres_view_ = nullptr;
+  size_t cap_wres_ = 0;
   bool wsmall_ = true;                // small weighted calls in one launch (DQ_HIP_TUNE wsmall)
   WSmallResult* h_wsres_ = nullptr;   // host-coherent: its result
   WSmallResult* d_wsres_ = nullptr;

@@ -96,9 +96,9 @@ struct WArgs {
   WFold* fold;                // [tile][kWCh]
   WQuick* quick;              // [tile][kWCh]
   uint32_t* pbase;            // [tile][2] partition bases (old, new) inside the node
-  uint32_t* active;           // device word: nodes not final after the pass
+  uint32_t* active;           // host-coherent flag: 1 when a node is not final after the split pass
   uint32_t* gen;              // [tile] folds whose description needs the general classify (bit ch)
-  NodeResult* res;            // [node]
+  NodeResult* res;            // [node] (host-coherent)
   int32_t nn, ntiles, max_iters, fixed_point, it, pad;
 };
 void launch_wpass(int pass, const WArgs& a, hipStream_t stream);   // one statistics pass + epilogues

@@ -1041,7 +1041,8 @@ __global__ __launch_bounds__(kWChainThreads) void wk_chain(WArgs a, int pass) {
   }
   if (lane == 0) {
     st = w;
-    if (!w.done && pass != WP_INIT) atomicAdd(a.active, 1u);
+    if (!w.done && pass != WP_INIT)   // (host-coherent: a flag, every writer stores 1)
+      __hip_atomic_store(a.active, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
