@@ -17,12 +17,11 @@
 //      a stable partition of the node's records (point order kept: the
 //      reference gathers by ascending index), and STEP 4's greedy choice.
 //      Every statistic is a SEQUENTIAL FP64 fold in point order, as the
-//      reference's: one wave per fold walks the node 64 summands at a time,
-//      and adds a group as ONE exact integer run u * sum(RNE(x / u)) when the
-//      running sum s provably stays in its binade [2^e, 2^(e+1)) (grid u =
-//      2^(e-52)) and no summand is a rounding tie -- exactly the sequential
-//      sums (dq_weighted.hip's "exact parallel fold", here with s known
-//      exactly at every group) -- else one summand at a time;
+//      reference's: 15 waves compute a chunk's summands into LDS while lanes
+//      0-6 of wave 0 -- one per fold -- add the previous chunk's, one
+//      v_add_f64 per summand in point order (exact integer runs of 64
+//      summands, dq_weighted.hip's "exact parallel fold", measured slower at
+//      these sizes: their scans and checks cost about 25 adds per run);
 //   C. the final centres (:1029-1096), the first-occurrence dedup
 //      (quant_util.cpp:93-118) and, for at most kWsMapMax deduped colours,
 //      map_colors_mps: the palette sorted by R+G+B -- for <= 16 entries
@@ -447,21 +446,44 @@ __global__ __launch_bounds__(kWsThreads) void wsmall_kernel(WSmallArgs a) {
         // buffer and are never added)
         const double* xb = xs + (size_t)((c - 1) & 1) * (kWsSeqChunk + 16) * 8 + lane;
         const uint32_t cl = min(kWsSeqChunk, len - (c - 1) * kWsSeqChunk);
+        // two register sets in turn (a copy between them made the compiler
+        // wait for every read before the next were issued)
         constexpr uint32_t U = 8;
-        double v[U];
+        double va[U], vb[U];
 #pragma unroll
-        for (uint32_t u = 0; u < U; ++u) v[u] = xb[(size_t)u * 8];
+        for (uint32_t u = 0; u < U; ++u) va[u] = xb[(size_t)u * 8];
         uint32_t t = 0;
-        for (; t + U <= cl; t += U) {
-          double nv[U];
+        // (sched_barrier: the scheduler merged the two read groups and then
+        // waited for the first right after issuing both)
+        for (; t + 2 * U <= cl; t += 2 * U) {
 #pragma unroll
-          for (uint32_t u = 0; u < U; ++u) nv[u] = xb[(size_t)(t + U + u) * 8];
+          for (uint32_t u = 0; u < U; ++u) vb[u] = xb[(size_t)(t + U + u) * 8];
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (uint32_t u = 0; u < U; ++u) s += v[u];
+          for (uint32_t u = 0; u < U; ++u) s += va[u];
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (uint32_t u = 0; u < U; ++u) v[u] = nv[u];
+          for (uint32_t u = 0; u < U; ++u) va[u] = xb[(size_t)(t + 2 * U + u) * 8];
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (uint32_t u = 0; u < U; ++u) s += vb[u];
+          __builtin_amdgcn_sched_barrier(0);
         }
-        for (uint32_t u = 0; t < cl; ++t, ++u) s += v[u];
+        // the last < 16 (va holds t .. t + 7)
+        if (t + U <= cl) {
+#pragma unroll
+          for (uint32_t u = 0; u < U; ++u) vb[u] = xb[(size_t)(t + U + u) * 8];
+#pragma unroll
+          for (uint32_t u = 0; u < U; ++u) s += va[u];
+          t += U;
+#pragma unroll
+          for (uint32_t u = 0; u < U; ++u)
+            if (t + u < cl) s += vb[u];
+        } else {
+#pragma unroll
+          for (uint32_t u = 0; u < U; ++u)
+            if (t + u < cl) s += va[u];
+        }
       }
       __syncthreads();
     }
