@@ -669,7 +669,7 @@ def main():
         detail["weighted_c3"] = {"ms_per_frame": round(dtw * 1e3 / sw_, 3),
                                  "Mpix_per_s": round(n * world * sw_ / dtw / 1e6, 2), "steps": sw_,
                                  "workload": "one 3840x2160 frame per call, K=256, quant_recurse(allPixelsUnique=0): "
-                                             "GPU calc_color_table (rocPRIM sorts) + exact ordered FP64 folds, %d "
+                                             "GPU calc_color_table (hand-written: bucket-group runs + LDS tables) + exact ordered FP64 folds, %d "
                                              "rank(s)" % world,
                                  "verified": okw}
         if okw is False:
