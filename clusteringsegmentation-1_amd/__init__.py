@@ -84,6 +84,7 @@ def lib():
         "dq_hip_last_points_swept": ([c.c_int], c.c_uint64),
         "dq_hip_last_points_full": ([c.c_int], c.c_uint64),
         "dq_hip_last_seq_tiles": ([c.c_int], c.c_uint64),
+        "dq_hip_last_cursor_fixes": ([c.c_int], c.c_uint64),
         "dq_hip_set_fixed_point": ([c.c_int, c.c_int], None),
         "dq_hip_set_planned_rounds": ([c.c_int, c.c_int], None),
         "dq_hip_last_planned_rounds": ([c.c_int], c.c_int),
@@ -126,7 +127,10 @@ def lib():
         "dq_hip_loopback_rows_dev": ([c.c_int, c.c_int, c.c_int, vp, c.c_uint32, c.c_uint32, vp, c.c_uint32,
                                       vp, vp, c.c_int, vp, c.c_int, vp], c.c_int),
     }
+    ab = "DQ_HIP_LIB" in os.environ   # (A/B runs against an older build: its newer entry points absent)
     for name, (args, res) in sigs.items():
+        if ab and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
@@ -561,6 +565,12 @@ def last_points_full(device=0):
 def last_seq_tiles(device=0):
     """Weighted path: tiles of the last run folded one summand at a time."""
     return int(lib().dq_hip_last_seq_tiles(device))
+
+
+def last_cursor_fixes(device=0):
+    """Records of the last run partitioned after a frame's last planned round
+    (PS_STATS: no cursors counted there) whose cursors were counted then."""
+    return int(lib().dq_hip_last_cursor_fixes(device))
 
 
 def set_fixed_point(on, device=0):

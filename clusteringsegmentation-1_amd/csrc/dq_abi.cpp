@@ -402,12 +402,13 @@ static int quant_batch(int device, std::vector<dq::FrameJob>& jobs, int max_iter
     // lane 0 reports for the batch: the last frame's diagnostics, summed counters
     Engine& el = engine_for(device, lanes - 1);
     std::lock_guard<std::mutex> g(e0.mutex());
-    uint64_t swept = 0, full = 0;
+    uint64_t swept = 0, full = 0, fixes = 0;
     int rounds = 0;
     for (int l = 0; l < lanes; ++l) {
       Engine& e = engine_for(device, l);
       swept += e.last_points_swept;
       full += e.last_points_full;
+      fixes += e.last_cursor_fixes;
       rounds = std::max(rounds, e.last_rounds);
       if (l > 0) e0.absorb_stats(e);
     }
@@ -417,6 +418,7 @@ static int quant_batch(int device, std::vector<dq::FrameJob>& jobs, int max_iter
     e0.last_rounds = rounds;
     e0.last_points_swept = swept;
     e0.last_points_full = full;
+    e0.last_cursor_fixes = fixes;
   }
   int empty = 0;
   for (int i = 0; i < nframes; ++i) empty += jobs[i].num_empty;
@@ -865,6 +867,7 @@ int dq_hip_last_rounds(int device) { return engine_for(device).last_rounds; }
 uint64_t dq_hip_last_points_swept(int device) { return engine_for(device).last_points_swept; }
 uint64_t dq_hip_last_points_full(int device) { return engine_for(device).last_points_full; }
 uint64_t dq_hip_last_seq_tiles(int device) { return engine_for(device).last_seq_tiles; }
+uint64_t dq_hip_last_cursor_fixes(int device) { return engine_for(device).last_cursor_fixes; }
 
 int dq_hip_last_wsmall_profile(int device, uint64_t* out, int nout) {
   const std::vector<uint64_t>& p = engine_for(device).last_wsmall_prof;

@@ -766,6 +766,11 @@ int Engine::enqueue_host_round(const std::vector<int>& active_in, bool root_roun
     launch_partsplit(ma, (int)nmat, src_fmt(mat), stream);
     timed_end(ST_PARTITION, 0.0, stream);
   }
+  // parents finalised at a PS_STATS round's split: their cursors first
+  // (their points exist by now: PS_WRITE above), before this round's own
+  // split pass reuses the tile-partial scratch the count pass writes
+  for (int p : parents)
+    if (nodes_[p].cursors_pending) fix_cursors(p, stream);
   const double bytes_all = 4.0 * (double)total;
   const int nt = (int)ntiles;
   auto pass = [&](int kind, int st, int tiles, double pbytes, double units) {
@@ -1329,10 +1334,13 @@ int Engine::finish_round(int ri, int max_iters, hipStream_t stream, bool specula
     nodes_.push_back(co);
     nodes_.push_back(cn);
     segs_.resize((size_t)(io + 2) * S);
+    nodes_[id].cursors_pending = R.stats_only && r.proven;   // (PS_STATS counts no cursors)
     for (int sh = 0; sh < S; ++sh) {
       Seg& ps = seg(id, sh);
       ps.dnode = R.dn + a * S + sh;
       ps.dtiles = R.dt + R.tbeg[a * S + sh];
+      ps.dwparts = R.ra.wparts + (size_t)R.tbeg[a * S + sh] * kTileWaves;
+      ps.rec = a * S + sh;
       ps.ntiles = R.tend[a * S + sh] - R.tbeg[a * S + sh];
       const uint32_t n_new = res[a * S + sh].n_new_local;
       const uint32_t n_old = ps.len - n_new;
@@ -1478,6 +1486,7 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
   last_rounds = 0;
   last_points_swept = 0;
   last_points_full = 0;
+  last_cursor_fixes = 0;
   nshard_ = jobs[0].nshard;
   DQ_CHECK(nshard_ >= 1 && nshard_ <= kMaxShard, "shards per frame must be in [1, 8]");
   const int S = nshard_;
@@ -1712,6 +1721,26 @@ void Engine::run(FrameJob* jobs, int nframes, int max_iters, bool dedup_map,
                  nframes, S, last_rounds, tr_first_us_, t_clu - t_run0, tr_build_us_, tr_wait_us_,
                  tr_replay_us_, t_end - t_clu, t_end - tr_entry_t0_);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Partition cursors of a node finalised at a PS_STATS round's split (that
+// partition counts none): its split decision's per-(tile, wave) counts over
+// its points and the cursor scan, into its round's tiles -- what the
+// children's chunk walk would have left there.
+void Engine::fix_cursors(int id, hipStream_t stream) {
+  for (int sh = 0; sh < nshard_; ++sh) {
+    const Seg& sg = seg(id, sh);
+    RoundArgs fa{};
+    fa.tiles = const_cast<Tile*>(sg.dtiles);
+    fa.nodes = const_cast<DevNode*>(sg.dnode) - sg.rec;
+    fa.wparts = sg.dwparts;
+    fa.parts = d_parts_;
+    fa.plane = cap_px_;
+    launch_fix_cursors(fa, sg.ntiles, stream);
+  }
+  nodes_[id].cursors_pending = false;
+  last_cursor_fixes++;
 }
 
 // ---------------------------------------------------------------------------

@@ -52,6 +52,8 @@ struct Node {
   bool partitioned = false;          // children's segments assigned in child_buf(buf)
   bool points = true;                // its segment holds its points (false: a PS_STATS round
                                      //   computed its split without writing them)
+  bool cursors_pending = false;      // final at a PS_STATS round's split: its partition cursors
+                                     //   were not counted (fix_cursors before it is partitioned)
   double w = 0.0;                    // weight[]   (:290, :862-863)
   double mean[3] = {0, 0, 0};        // mean[]     (:309)
   double var[3] = {0, 0, 0};         // var[]      (:314)
@@ -72,6 +74,8 @@ struct Seg {
   int32_t ntiles = 0;
   const DevNode* dnode = nullptr;
   const Tile* dtiles = nullptr;
+  uint32_t* dwparts = nullptr;       // its tiles' per-(tile, wave) count words in its round's block
+  int32_t rec = 0;                   // its record's index in its round (Tile::node)
 };
 
 // One quant_recurse / DivQuantCluster input.
@@ -233,6 +237,7 @@ class Engine {
   uint64_t last_points_swept = 0;     // sum over passes of points read (all frames)
   uint64_t last_points_full = 0;      // the same without fixed-point finalisation
   uint64_t last_seq_tiles = 0;        // weighted: tiles folded one summand at a time
+  uint64_t last_cursor_fixes = 0;     // records whose cursors a later round counted (fix_cursors)
   std::vector<uint64_t> last_wsmall_prof;   // weighted, one launch: WSmallResult::prof (empty: not taken)
 
   void set_timing(bool on) { timing_ = on; }
@@ -478,6 +483,7 @@ class Engine {
   WsMapTab* d_wsmap_ = nullptr;       // device: its palette for the grid map
   bool run_weighted_small(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream);
   void ensure_color_scratch(uint32_t n, hipStream_t stream);
+  void fix_cursors(int id, hipStream_t stream);
   size_t cap_wnodes_ = 0;
 
   std::vector<Node> nodes_;

@@ -186,6 +186,12 @@ void launch_kpass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream);
 // totals per a.tot_mode, the record's own partials for its local counts;
 // publishes the next pass's decision (or the split's results).
 void launch_epilogue(int kind, const RoundArgs& a, int nnodes, hipStream_t stream);
+// The partition cursors of ONE record finalised at a PS_STATS round's split
+// (that partition counts no children): its split decision's per-(tile, wave)
+// counts over its points (pass_kernel<PASS_SPLIT> on a.tiles[0 .. ntiles),
+// into a.wparts), then the cursor scan into its tiles.  a.nodes: its round's
+// records (Tile::node indexes them).
+void launch_fix_cursors(const RoundArgs& a, int ntiles, hipStream_t stream);
 // TOT_ALLREDUCE rounds: per logical node, the sums of the pass over all its
 // shard records' tiles into a.tot (to be allreduced across processes).
 void launch_nodesum(int kind, const RoundArgs& a, int nlogical, hipStream_t stream);

@@ -1701,10 +1701,15 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
   const uint32_t sh0 = (uint32_t)pt.shift[0], sh1 = (uint32_t)pt.shift[1];
   const int32_t thr0 = pt.thr[0], thr1 = pt.thr[1];
   constexpr bool kStore = MODE != PS_STATS, kSums = MODE == PS_FULL || MODE == PS_STATS;
-  ChunkAcc cx, cy;   // (the children's per-(tile, wave) counts: PS_FULL and PS_STATS)
+  // the children's per-(tile, wave) counts (their partition cursors): PS_FULL
+  // only.  A PS_STATS round is a frame's last planned one; the few of its
+  // records a later host round partitions get theirs then (launch_fix_cursors)
+  // -- the walk cost PS_STATS a third of its time.
+  constexpr bool kCounts = MODE == PS_FULL;
+  ChunkAcc cx, cy;
   ChildInfo off{0u, 0u, 1u, 0u, 0};
-  chunk_init(cx, kSums ? ci0 : off, wparts, oc0);
-  chunk_init(cy, kSums ? ci1 : off, wparts, nc0);
+  chunk_init(cx, kCounts ? ci0 : off, wparts, oc0);
+  chunk_init(cy, kCounts ? ci1 : off, wparts, nc0);
   Stage g;
   constexpr uint32_t kPnOff = kStageRun;
   g.cbo = oc0 & ~15u;
@@ -1802,17 +1807,21 @@ __device__ __forceinline__ void partsplit_run(const PartTile& pt, g_cnode& nd, g
     // this wave's points into the runs (PS_STATS: the run positions only --
     // the children's per-(tile, wave) counts are the partition cursors a
     // later round may need -- no stores)
-    const uint32_t oc = g.cbo + g.po, nc = g.cbn + g.pn - kPnOff;
-    stage_sweep<kStore>(sw, om, nm, full, st, g, l);
-    chunk_sweep(cx, oc, g.cbo + g.po, om, xm, xc);
-    chunk_sweep(cy, nc, g.cbn + g.pn - kPnOff, nm, ym, yc);
+    if (kStore || kCounts) {
+      const uint32_t oc = g.cbo + g.po, nc = g.cbn + g.pn - kPnOff;
+      stage_sweep<kStore>(sw, om, nm, full, st, g, l);
+      chunk_sweep(cx, oc, g.cbo + g.po, om, xm, xc);
+      chunk_sweep(cy, nc, g.cbn + g.pn - kPnOff, nm, ym, yc);
+    }
     if (kStore) stage_flush(st, d, g, l);
     vs = nvs;
     full = nfull;
   }
   if (kStore) stage_bytes(st, d, g, g.cbo + g.po, g.cbn + g.pn - kStageRun, l);   // the runs' last partial chunks
-  chunk_finish(cx);
-  chunk_finish(cy);
+  if (kCounts) {
+    chunk_finish(cx);
+    chunk_finish(cy);
+  }
 }
 
 // One part tile's partition + children's split pass (pt: the parent's tile,
@@ -3319,8 +3328,21 @@ __global__ __launch_bounds__(kMapLdsBlock) void map_lds_kernel(const MapTask* __
   }
 }
 
+// The cursor scan of one record's tiles from their per-(tile, wave) counts
+// (launch_fix_cursors).
+__global__ __launch_bounds__(kEpiBlock) void cursor_scan_kernel(Tile* tiles, const uint32_t* wp, int ntiles) {
+  __shared__ uint64_t s_tot[kEpiBlock / 64];
+  block_cursors<kEpiBlock>(tiles, wp, 0, ntiles, s_tot);
+}
+
 // ---------------------------------------------------------------------------
 // Launchers.
+void launch_fix_cursors(const RoundArgs& a, int ntiles, hipStream_t stream) {
+  if (ntiles <= 0) return;
+  pass_kernel<PASS_SPLIT><<<dim3(ntiles), dim3(kBlock), 0, stream>>>(a);
+  cursor_scan_kernel<<<dim3(1), dim3(kEpiBlock), 0, stream>>>(a.tiles, a.wparts, ntiles);
+}
+
 void launch_pass(int kind, const RoundArgs& a, int ntiles, hipStream_t stream) {
   if (ntiles <= 0) return;
   const dim3 g(ntiles), b(kBlock);

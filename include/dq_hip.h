@@ -211,6 +211,10 @@ uint64_t dq_hip_last_points_full(int device);
 /* Weighted path: tiles of the last run whose folds ran one summand at a time
  * (the exact parallel fold's fallback). */
 uint64_t dq_hip_last_seq_tiles(int device);
+/* Records of the last run finalised at a frame's last planned round (whose
+ * partition counts no partition cursors) that a later round partitioned:
+ * their cursors counted then. */
+uint64_t dq_hip_last_cursor_fixes(int device);
 /* Fixed-point finalisation (default on; DQ_HIP_TUNE=full_iters=1 turns the
  * default off).  A split whose 2-means pass reproduces the previous pass's exact
  * integer sums is final: the remaining iterations of the reference's loop
