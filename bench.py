@@ -435,6 +435,26 @@ def pick_roofline(stats, pmc_key):
     return roof
 
 
+def copy_rate_gbs(torch, dev, mib=1024, reps=10):
+    """Context for the roofline: the device-to-device copy rate of a buffer
+    four times the 256-MB Infinity Cache (bytes read + written per second)
+    -- the practical ceiling of a kernel that reads and writes its bytes
+    once, measured live on this box."""
+    a = torch.empty(mib << 18, dtype=torch.int32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2.0 * (mib << 20) / (ms / 1e3) / 1e9
+
+
 def upload_frames(torch, pkg, dev, w, h, ids, rows=None):
     """Synthetic frames `ids` on the device (whole, or rows [r0, r1) of each)."""
     ts = []
@@ -761,6 +781,12 @@ def main():
     if rank == 0:
         pmc_key = "%s_%s_f%d_n%d" % (a.mode, a.config, nf, world)
         roof = pick_roofline(stats, pmc_key) if stats else None
+        if roof:
+            cgbs = copy_rate_gbs(torch, dev)
+            roof["copy_GBps_measured"] = round(cgbs, 1)
+            roof["frac_of_copy"] = round(roof["achieved"] / cgbs, 4)
+            roof["copy_note"] = ("a 1-GiB device-to-device copy (read + write) timed on this box: the "
+                                 "practical ceiling of a read+write kernel; frac stays against the nominal peak")
         # engine-model bytes of all kernels of the roofline region, per step,
         # over the timed step's wall time (<= 1: they are bytes the kernels move)
         eng_bytes = sum(v[2] for v in stats.values()) / max(1, a.steps)
