@@ -283,6 +283,60 @@ def weighted_regions(pkg, torch, dev, stream, k, sides, image="batman", calls=0,
     return rows
 
 
+def weighted_regions_batch(pkg, torch, dev, stream, k, side, image="batman", reps=5, cpu=True):
+    """The same call for EVERY side x side tile of the sample image at once
+    (dq_hip_quant_weighted_regions_dev: one launch, one workgroup per
+    region), beside the reference build running the tiles one after another
+    (the app's loop); every tile's output checked against the reference's."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import dq_fixtures as fx
+    img, w, h = fx.load_png_u32(os.path.join(GOLDEN, "png", image + ".png"))
+    img = img.reshape(h, w)
+    regions = [np.ascontiguousarray(img[y:y + side, x:x + side]).reshape(-1)
+               for y in range(0, h - side + 1, side) for x in range(0, w - side + 1, side)]
+    ts = [torch.from_numpy(p.view(np.int32)).to(dev) for p in regions]
+    outs = [torch.empty_like(t) for t in ts]
+    wr = pkg.WeightedRegions(ts, outs, k)   # (argument arrays built once: the library call is timed)
+    last = {}
+
+    def one():
+        wr.run(max_iters=10, stream=stream)
+        last["cts"] = [wr.colortable(i) for i in range(wr.nr)]
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        wr.run(max_iters=10, stream=stream)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    one()
+    row = {"side": side, "regions": len(regions), "pixels": int(sum(p.size for p in regions)),
+           "gpu_ms_per_call": round(dt * 1e3, 3), "gpu_us_per_region": round(dt * 1e6 / len(regions), 2)}
+    if cpu:
+        ref_so = os.path.join(ROOT, "oracle", "_ref", "libdqref.so")
+        if os.path.exists(ref_so):
+            lib = ctypes.CDLL(ref_so)
+            ok, t = True, 0.0
+            with _Quiet():
+                for i, px in enumerate(regions):
+                    out = np.zeros(px.size, np.uint32)
+                    ct = np.zeros(k, np.uint32)
+                    kk = ctypes.c_uint32(k)
+                    t0 = time.perf_counter()
+                    lib.quant_recurse(ctypes.c_uint32(px.size), fx.vp(px), fx.vp(out), ctypes.byref(kk), fx.vp(ct),
+                                      ctypes.c_int(0))
+                    t += time.perf_counter() - t0
+                    ok = ok and np.array_equal(last["cts"][i], ct[:kk.value]) and \
+                        np.array_equal(outs[i].cpu().numpy().view(np.uint32), out)
+            row["ref_cpu_ms_all_regions"] = round(t * 1e3, 2)
+            row["ref_cpu_us_per_region"] = round(t * 1e6 / len(regions), 2)
+            row["gpu_over_cpu_speedup"] = round(t / dt, 2)
+            row["verified"] = bool(ok)
+    del ts, outs
+    return row
+
+
 def init_dist():
     """(rank, world, local_rank) from the torchrun environment; one process
     per GPU over RCCL ("nccl"), or gloo without a GPU (CPU tests)."""
@@ -709,6 +763,18 @@ def main():
             "regions": rows}
         if any(r.get("verified") is False for r in rows):
             fail("weighted-region outputs differ from the reference build's", rank, regions=rows)
+        # every tile of the image at once: the app's loop over its regions as
+        # one batched call (dq_hip_quant_weighted_regions_dev), the reference
+        # running the same tiles one by one
+        cpu_b = rank == 0 and world == 1 and not a.no_cpu_baseline
+        brows = [weighted_regions_batch(pkg, torch, dev, stream, 4, sd, cpu=cpu_b) for sd in (32, 100)]
+        detail["weighted_regions_batched"] = {
+            "workload": "quant_recurse(N, K=4, allPixelsUnique=0) for every side x side tile of "
+                        "tests/golden/png/batman.png in ONE call (one workgroup per region), device-resident "
+                        "pixels; ref_cpu = the reference build running the tiles one after another, one core",
+            "batches": brows}
+        if any(r.get("verified") is False for r in brows):
+            fail("batched weighted-region outputs differ from the reference build's", rank, batches=brows)
     # --- the same frames as OpenCV BGR24 Mats: read directly by
     # the root's passes, partition and map (3 B per pixel, no packing pass);
     # one frame per call (C3 shape) and the rank's batch in one call

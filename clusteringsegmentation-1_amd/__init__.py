@@ -78,6 +78,8 @@ def lib():
         "dq_hip_cluster_dev": ([c.c_int, vp, c.c_uint32, u32p, vp, c.c_int, vp], c.c_int),
         "dq_hip_map_dev": ([c.c_int, vp, c.c_uint32, vp, vp, c.c_int, vp], c.c_int),
         "dq_hip_quant_weighted_dev": ([c.c_int, vp, c.c_uint32, vp, u32p, vp, c.c_int, vp], c.c_int),
+        "dq_hip_quant_weighted_regions_dev": ([c.c_int, c.c_int, vp, vp, vp, vp, vp, c.c_uint32, vp, c.c_int, vp],
+                                              c.c_int),
         "dq_hip_last_centroids": ([c.c_int, vp, vp, c.c_int], c.c_int),
         "dq_hip_last_trace": ([c.c_int, vp, c.c_int], c.c_int),
         "dq_hip_last_rounds": ([c.c_int], c.c_int),
@@ -254,6 +256,51 @@ def quant_device(t_in, t_out, num_clusters, max_iters=10, device=0, n=None, stre
     if r < 0:
         raise DivQuantError("dq_hip_quant_dev: bad arguments")
     return ct[:k.value].copy(), r
+
+
+class WeightedRegions:
+    """A set of device-resident regions for dq_hip_quant_weighted_regions_dev
+    with its argument arrays built once (for repeated calls on the same
+    buffers: the per-call marshalling of thousands of pointers is Python's
+    cost, not the library's)."""
+
+    def __init__(self, t_ins, t_outs, num_clusters):
+        nr = len(t_ins)
+        self.nr = nr
+        self.ks = np.array(num_clusters if hasattr(num_clusters, "__len__") else [num_clusters] * nr, np.uint32)
+        self.stride = int(self.ks.max()) if nr else 1
+        self.ins = (ctypes.c_void_p * max(nr, 1))(*[_dptr(t).value for t in t_ins])
+        self.outs = (ctypes.c_void_p * max(nr, 1))(*[_dptr(t).value for t in t_outs]) if t_outs is not None else None
+        self.ns = np.array([t.numel() for t in t_ins], np.uint32)
+        self.ct = np.zeros((max(nr, 1), self.stride), np.uint32)
+        self.kout = np.zeros(max(nr, 1), np.uint32)
+        self._refs = (t_ins, t_outs)   # (keep the buffers alive)
+
+    def run(self, max_iters=10, device=0, stream=None):
+        """One call over every region; returns the total of empty clusters
+        (colortables: self.colortable(i))."""
+        r = lib().dq_hip_quant_weighted_regions_dev(
+            device, self.nr, ctypes.cast(self.ins, ctypes.c_void_p), _ptr(self.ns),
+            ctypes.cast(self.outs, ctypes.c_void_p) if self.outs is not None else None,
+            _ptr(self.ks), _ptr(self.ct), self.stride, _ptr(self.kout), max_iters, _stream_ptr(stream))
+        if r < 0:
+            raise DivQuantError("dq_hip_quant_weighted_regions_dev: bad arguments")
+        return r
+
+    def colortable(self, i):
+        return self.ct[i, :self.kout[i]].copy()
+
+
+def quant_weighted_regions_device(t_ins, t_outs, num_clusters, max_iters=10, device=0, stream=None):
+    """The app's per-superpixel-region calls quant_recurse(N_region, .., K,
+    allPixelsUnique=0) (ClusteringSegmentation.cpp:1779-1803) for many
+    device-resident regions in one call (one launch for every region of at
+    most 131071 pixels / 6144 colours / K <= 64).  num_clusters: one K or a
+    list.  t_outs may be None (cluster + dedup only).  Returns ([colortable
+    per region], total_empty)."""
+    w = WeightedRegions(t_ins, t_outs, num_clusters)
+    r = w.run(max_iters, device, stream)
+    return [w.colortable(i) for i in range(w.nr)], r
 
 
 def quant_batch_device(t_ins, t_outs, num_clusters, max_iters=10, device=0, stream=None):

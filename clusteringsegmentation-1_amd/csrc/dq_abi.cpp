@@ -244,6 +244,34 @@ int dq_hip_quant_weighted_dev(int device, const uint32_t* d_in, uint32_t n, uint
   return j.num_empty;
 }
 
+// Many weighted quant_recurse calls (the app's per-superpixel-region calls,
+// ClusteringSegmentation.cpp:1779-1803) in one: region i = d_ins[i][0..ns[i])
+// -> d_outs[i], K = ks[i], colortable at cts + i * ct_stride, its size at
+// k_outs[i].  Returns the total of empty clusters, or < 0.
+int dq_hip_quant_weighted_regions_dev(int device, int nregions, const uint32_t* const* d_ins, const uint32_t* ns,
+                                      uint32_t* const* d_outs, const uint32_t* ks, uint32_t* cts,
+                                      uint32_t ct_stride, uint32_t* k_outs, int max_iters, void* stream) {
+  if (nregions < 0 || (nregions > 0 && (!d_ins || !ns || !ks || !cts || !k_outs)) || max_iters < 1) return -1;
+  std::vector<dq::FrameJob> jobs((size_t)nregions);
+  for (int i = 0; i < nregions; ++i) {
+    if (!d_ins[i] || ns[i] == 0 || ks[i] == 0 || ks[i] > ct_stride) return -1;
+    jobs[i].d_in = d_ins[i];
+    jobs[i].n = ns[i];
+    jobs[i].d_out = d_outs ? d_outs[i] : nullptr;
+    jobs[i].k = (int)ks[i];
+    jobs[i].ct = cts + (size_t)i * ct_stride;
+  }
+  Engine& e = engine_for(device);
+  std::lock_guard<std::mutex> g(e.mutex());
+  e.run_weighted_regions(jobs.data(), nregions, max_iters, dev_stream(e, stream));
+  int empty = 0;
+  for (int i = 0; i < nregions; ++i) {
+    k_outs[i] = (uint32_t)jobs[i].k_out;
+    empty += jobs[i].num_empty;
+  }
+  return empty;
+}
+
 static hipStream_t engine_stream(int device, void* stream);
 
 int dq_hip_varpart_dev(int device, const uint32_t* d_in, uint32_t n, uint32_t rows, uint32_t cols,

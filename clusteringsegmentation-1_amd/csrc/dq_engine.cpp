@@ -2132,6 +2132,77 @@ bool Engine::run_weighted_small(FrameJob& job, int max_iters, bool dedup_map, hi
   return true;
 }
 
+// A batch of weighted calls (superpixel regions): one launch, one workgroup
+// per region the small-path kernel holds; the results read back as
+// run_weighted_small's, the rest through run_weighted.
+int Engine::run_weighted_regions(FrameJob* jobs, int njobs, int max_iters, hipStream_t stream) {
+  DQ_HIP(hipSetDevice(device_));
+  if (!stream) stream = stream_;
+  std::vector<int> take, rest;
+  for (int i = 0; i < njobs; ++i) {
+    const FrameJob& j = jobs[i];
+    const bool plain = j.num_bits == 8 && j.dec == 1 && (j.rows == 0 || j.rows == 1) && (j.cols == 0 || j.cols == j.n);
+    if (wsmall_ && plain && j.n >= 1 && j.n <= kWsMaxN && j.k >= 1 && j.k <= kWsMaxK) take.push_back(i);
+    else rest.push_back(i);
+  }
+  const size_t nb = take.size();
+  if (nb > cap_wb_) {
+    DQ_HIP(hipStreamSynchronize(stream));
+    if (h_wbargs_) DQ_HIP(hipHostFree(h_wbargs_));
+    if (h_wbres_) DQ_HIP(hipHostFree(h_wbres_));
+    cap_wb_ = std::max<size_t>(nb, 64);
+    DQ_HIP(hipHostMalloc((void**)&h_wbargs_, cap_wb_ * sizeof(WSmallArgs), hipHostMallocCoherent | hipHostMallocMapped));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_wbargs_, h_wbargs_, 0));
+    DQ_HIP(hipHostMalloc((void**)&h_wbres_, cap_wb_ * sizeof(WSmallResult), hipHostMallocCoherent | hipHostMallocMapped));
+    DQ_HIP(hipHostGetDevicePointer((void**)&d_wbres_, h_wbres_, 0));
+  }
+  for (size_t t = 0; t < nb; ++t) {
+    const FrameJob& j = jobs[take[t]];
+    WSmallArgs& wa = h_wbargs_[t];
+    wa.px = j.d_in;
+    wa.out = j.d_out;
+    wa.res = d_wbres_ + t;
+    wa.maptab = nullptr;
+    wa.norm = 1.0 / (std::ceil(1.0 / 1.0) * std::ceil((double)j.n / 1.0));   // (:184), rows = dec = 1
+    wa.n = j.n;
+    wa.k = j.k;
+    wa.max_iters = max_iters;
+    wa.fixed_point = fixed_point_ ? 1 : 0;
+    __atomic_store_n(&h_wbres_[t].status, 0u, __ATOMIC_RELEASE);
+  }
+  if (nb > 0) {
+    DQ_HIP(launch_wsmall_batch(d_wbargs_, (int)nb, stream));
+    sync_stream(stream);
+  }
+  int taken = 0;
+  for (size_t t = 0; t < nb; ++t) {
+    FrameJob& job = jobs[take[t]];
+    const WSmallResult& r = h_wbres_[t];
+    const uint32_t st = __atomic_load_n(&r.status, __ATOMIC_ACQUIRE);
+    if (st == 2) {   // more colours than the kernel holds
+      rest.push_back(take[t]);
+      continue;
+    }
+    DQ_CHECK(st == 1, st == 3 ? "small weighted kernel: partition count differs from the fold count"
+                              : "small weighted kernel: no result");
+    ++taken;
+    job.k_out = (int)r.k_raw;
+    job.num_empty = (int)r.num_empty;
+    for (uint32_t i = 0; i < r.k_raw; ++i) job.ct[i] = r.ct[i];
+    int m = 0;   // first-occurrence dedup (quant_util.cpp:93-118), as run_weighted
+    for (int i = 0; i < job.k_out; ++i) {
+      bool seen = false;
+      for (int q = 0; q < m && !seen; ++q) seen = job.ct[q] == job.ct[i];
+      if (!seen) job.ct[m++] = job.ct[i];
+    }
+    DQ_CHECK(m == (int)r.m, "small weighted kernel: dedup count differs from the host's");
+    job.k_out = m;
+    if (job.d_out && !r.mapped) map(job.d_in, job.n, job.d_out, job.ct, m, stream);
+  }
+  for (int i : rest) run_weighted(jobs[i], max_iters, true, stream);
+  return taken;
+}
+
 // ---------------------------------------------------------------------------
 // RCCL communicator (row-tile sharding across processes, one GPU each).
 void Engine::comm_unique_id(char id[128]) {

@@ -164,6 +164,12 @@ class Engine {
   // (dq_weighted.hip); dedup + map as run().  last_sizes / last_trace count
   // points = unique colours, as the reference's size[].
   void run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream);
+  // Many weighted calls (the app's superpixel regions, each with its own
+  // pixels, output and K; dedup + map as run_weighted(.., true, ..)): every
+  // region the one-workgroup kernel holds in ONE launch, one workgroup each;
+  // the others (and any with more colours than it holds) one by one through
+  // run_weighted.  Returns how many the batch launch took.
+  int run_weighted_regions(FrameJob* jobs, int njobs, int max_iters, hipStream_t stream);
   // calc_color_table (DivQuantMapColors.cpp:82-203) on the device for a host
   // input: the points inPixels[ic + ir*numRows] (ir < rows, ic < cols, step
   // dec), their unique colours and weights norm * count in the reference's
@@ -479,6 +485,11 @@ class Engine {
   size_t cap_wres_ = 0;
   bool wsmall_ = true;                // small weighted calls in one launch (DQ_HIP_TUNE wsmall)
   WSmallResult* h_wsres_ = nullptr;   // host-coherent: its result
+  WSmallArgs* h_wbargs_ = nullptr;    // host-coherent: a region batch's argument records
+  WSmallArgs* d_wbargs_ = nullptr;
+  WSmallResult* h_wbres_ = nullptr;   // ... and their results
+  WSmallResult* d_wbres_ = nullptr;
+  size_t cap_wb_ = 0;
   WSmallResult* d_wsres_ = nullptr;
   WsMapTab* d_wsmap_ = nullptr;       // device: its palette for the grid map
   bool run_weighted_small(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream);

@@ -160,5 +160,9 @@ struct WSmallArgs {
   int32_t k, max_iters, fixed_point;
 };
 hipError_t launch_wsmall(const WSmallArgs& a, hipStream_t stream);   // (the launch's error, if any)
+// Many inputs in one launch, one workgroup each (d_args: nregions argument
+// records in device-visible memory, maptab null: a region whose map needs
+// the grid kernel is left unmapped, res->mapped = 0).
+hipError_t launch_wsmall_batch(const WSmallArgs* d_args, int nregions, hipStream_t stream);
 
 }  // namespace dq

@@ -224,7 +224,9 @@ __device__ __forceinline__ void ws_store_status(WSmallResult* r, uint32_t v) {
   __hip_atomic_store(&r->status, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kWsThreads) void wsmall_kernel(WSmallArgs a) {
+// The whole call of one input (one workgroup); the single-call kernel and
+// the batch kernel (one workgroup per region) below.
+__device__ __forceinline__ void wsmall_body(const WSmallArgs& a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ WsClu clu[kWsMaxK];
   __shared__ WsCtl ctl;
@@ -713,7 +715,9 @@ __global__ __launch_bounds__(kWsThreads) void wsmall_kernel(WSmallArgs a) {
     res->num_empty = empty;
     res->m = m;
     res->passes = ctl.passes;
-    const bool map = a.out != nullptr && m <= (uint32_t)kWsMapMax && ctl.status == 1;
+    // (a batch has no grid map behind it: a larger region's map is the host's)
+    const bool map = a.out != nullptr && m <= (uint32_t)kWsMapMax && ctl.status == 1 &&
+                     (n <= kWsMapInline || a.maptab != nullptr);
     res->mapped = map ? 1u : 0u;
     ctl.done = map ? 1 : 0;
     if (map) {
@@ -765,6 +769,15 @@ __global__ __launch_bounds__(kWsThreads) void wsmall_kernel(WSmallArgs a) {
   }
 }
 
+__global__ __launch_bounds__(kWsThreads) void wsmall_kernel(WSmallArgs a) { wsmall_body(a); }
+
+// Many inputs (the app's superpixel regions) in one launch: workgroup b runs
+// region b's whole call (as[b]; maptab null).
+__global__ __launch_bounds__(kWsThreads) void wsmall_batch_kernel(const WSmallArgs* __restrict__ as) {
+  const WSmallArgs a = as[blockIdx.x];
+  wsmall_body(a);
+}
+
 // The map of a larger small-path input (n > kWsMapInline) over a grid, from
 // the palette and lut_init wsmall_kernel left in `t` (go = 0: it did not map:
 // nothing to do).
@@ -793,6 +806,18 @@ hipError_t launch_wsmall(const WSmallArgs& a, hipStream_t stream) {
     const uint32_t grid = std::min<uint32_t>(1024u, (a.n + 256u * 8u - 1u) / (256u * 8u));
     wsmap_kernel<<<dim3(grid), dim3(256), 0, stream>>>(a.px, a.out, a.n, a.maptab);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_wsmall_batch(const WSmallArgs* d_args, int nregions, hipStream_t stream) {
+  if (nregions <= 0) return hipSuccess;
+  static hipError_t attr = hipErrorNotReady;
+  if (attr != hipSuccess) {
+    attr = hipFuncSetAttribute((const void*)wsmall_batch_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kWsLds);
+    if (attr != hipSuccess) return attr;
+  }
+  wsmall_batch_kernel<<<dim3(nregions), dim3(kWsThreads), kWsLds, stream>>>(d_args);
   return hipGetLastError();
 }
 

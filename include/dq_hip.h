@@ -151,6 +151,19 @@ int dq_hip_cluster_dev(int device, const uint32_t *d_in, uint32_t n,
 int dq_hip_quant_weighted_dev(int device, const uint32_t *d_in, uint32_t n,
                               uint32_t *d_out, uint32_t *k, uint32_t *ct,
                               int max_iters, void *stream);
+/* Many weighted calls at once -- the app's per-superpixel-region
+ * quant_recurse(N_region, .., K, allPixelsUnique=0)
+ * (ClusteringSegmentation.cpp:1779-1803): region i reads d_ins[i][0..ns[i]),
+ * writes its mapped colours to d_outs[i] (d_outs may be NULL: cluster + dedup
+ * only), its deduped colortable to cts + i*ct_stride (ks[i] <= ct_stride
+ * entries of room) and its size to k_outs[i].  Regions of at most 131071
+ * pixels, 6144 colours and K <= 64 run in ONE launch, one workgroup each;
+ * the others one by one.  Every result equals the region's own call.
+ * Returns the total of empty clusters, or < 0 (bad arguments). */
+int dq_hip_quant_weighted_regions_dev(int device, int nregions, const uint32_t *const *d_ins,
+                                      const uint32_t *ns, uint32_t *const *d_outs, const uint32_t *ks,
+                                      uint32_t *cts, uint32_t ct_stride, uint32_t *k_outs,
+                                      int max_iters, void *stream);
 /* quant_varpart_fast semantics (DivQuantCluster.cpp:1099-1179) on device
  * pixels for every (num_bits, dec_factor, allPixelsUnique): uniform weights
  * when uniq && num_bits == 8 && dec_factor == 1, else cut_bits to num_bits

@@ -104,3 +104,39 @@ def test_small_device_pointers_and_no_map(gpu):
     fx.oracle().dqo_cluster_weighted(ctypes.c_uint32(u), fx.vp(col), fx.vp(w), ctypes.byref(kk), fx.vp(rct),
                                      ctypes.c_int(10), None, None, None)
     assert np.array_equal(ct, rct[:kk.value])
+
+
+def test_regions_batch_equals_single_calls(gpu):
+    """The app's per-region calls batched (dq_hip_quant_weighted_regions_dev):
+    one launch for every region the kernel holds -- crops of the sample
+    images from 1 to ~10^5 pixels at K 1-64 -- plus regions it does not
+    (more than 6144 colours, more than 131071 pixels, K above 64) taken one
+    by one; every region equals its own single call, and a subset the
+    oracle's sequential folds."""
+    import torch
+    rng = np.random.default_rng(21)
+    regions = []
+    for name in ("batman", "cookie"):
+        img, w, h = fx.load_png_u32(fx.GOLDEN + "/png/%s.png" % name)
+        img = img.reshape(h, w)
+        for side in (1, 3, 16, 32, 64, 100, 128, 200, 316):
+            y0, x0 = int(rng.integers(0, h - side + 1)), int(rng.integers(0, w - side + 1))
+            regions.append(np.ascontiguousarray(img[y0:y0 + side, x0:x0 + side]).reshape(-1))
+    regions.append(rng.integers(0, 1 << 24, 20000, dtype=np.uint32))                    # > 6144 colours
+    regions.append(rng.integers(0, 1 << 24, 140000, dtype=np.uint32) & 0xE0E0E0)        # > 131071 px
+    ks = [int(k) for k in rng.choice([1, 2, 4, 7, 16, 64], len(regions))]
+    ks[-3] = 100                                                                          # K > 64
+    ts = [torch.from_numpy(p.view(np.int32)).to("cuda:0") for p in regions]
+    outs = [torch.empty_like(t) for t in ts]
+    cts, _ = gpu.quant_weighted_regions_device(ts, outs, ks)
+    torch.cuda.synchronize()
+    for i, (t, k) in enumerate(zip(ts, ks)):
+        o = torch.empty_like(t)
+        ct, _ = gpu.quant_device(t, o, k, all_pixels_unique=0)
+        torch.cuda.synchronize()
+        assert np.array_equal(cts[i], ct), (i, len(regions[i]), k)
+        assert torch.equal(outs[i], o), (i, len(regions[i]), k)
+    for i in (2, 5, 8, 12):
+        ref_out, ref_ct = _oracle(regions[i], ks[i])
+        assert np.array_equal(cts[i], ref_ct), i
+        assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), ref_out), i
