@@ -1796,9 +1796,10 @@ uint32_t Engine::color_table(const uint32_t* h_in, uint32_t rows, uint32_t cols,
 // ---------------------------------------------------------------------------
 // The weighted path: quant_varpart_fast's calc_color_table dedup and
 // DivQuantCluster<false,*,true> (DivQuantCluster.cpp:1133-1138, :1163-1166).
-// Rounds as run(): a round splits every node the greedy replay needs, each in
-// one workgroup of wsplit_kernel (its folds are sequential in point order);
-// the host replays the reference's greedy order over the results.
+// Rounds as run(): a round splits every node the greedy replay needs, its
+// passes' folds exact parallel folds over tiles (dq_weighted.hip), the host
+// replaying the reference's greedy order over the results.  An input the
+// one-workgroup kernel holds takes it instead (run_weighted_small).
 void Engine::run_weighted(FrameJob& job, int max_iters, bool dedup_map, hipStream_t stream) {
   DQ_CHECK(job.n > 0, "num_points must be > 0 (DivQuantCluster.cpp:211)");
   DQ_CHECK(job.k > 0, "num_colors must be > 0 (DivQuantCluster.cpp:229)");
