@@ -94,6 +94,7 @@ void Engine::apply_tune(const char* spec) {
     else if (k == "spin_sync") spin_sync_ = v != 0;
     else if (k == "eager_replan") eager_replan_ = v != 0;
     else if (k == "stats_only") stats_only_ = v != 0;
+    else if (k == "stats_min") stats_min_ = (uint64_t)std::max<long>(0, v);   // last rounds above this many points: PS_STATS
     else if (k == "fuse_plan") fuse_plan_ = v != 0;
     else if (k == "fold_split") fold_split_ = v != 0;                   // split totals from the partition
     else if (k == "persist") persist_ = v != 0;                         // kpersist_kernel rounds
@@ -878,7 +879,7 @@ int Engine::enqueue_planned_round(int prev, const std::vector<int32_t>& plist, i
   // (rounds of at most one 4K frame's points write them all instead: the
   // single-frame chain's PS_STATS + PS_LATE launches cost more than PS_FULL's
   // writes -- C3 -1.5-2 %, C2 -0.5 %; batches keep the stats-only form)
-  R.stats_only = stats_only_ && total > kFusePlanMaxPoints;
+  R.stats_only = stats_only_ && total > stats_min_;
   for (int32_t a : plist) {
     const FrameState& f = frames_[nodes_[P.order[a]].frame];
     R.stats_only = R.stats_only && f.splits_queued >= f.job->k - 1;

@@ -433,6 +433,7 @@ class Engine {
   bool stage_pending_ = false;
   bool plan_ = true;                  // device-planned rounds (DQ_HIP_TUNE plan=0: host only)
   bool stats_only_ = true;            // a frame's last planned round: PS_STATS + PS_LATE (DQ_HIP_TUNE stats_only)
+  uint64_t stats_min_ = 12u << 20;    // ... when the round has more points than this (DQ_HIP_TUNE stats_min)
   bool eager_replan_ = true;          // finish_round: all 2-means iterations + the re-plan at
                                       //   once when a planned successor waits (DQ_HIP_TUNE eager_replan)
   uint64_t seq_ = 0;                  // round sequence number
